@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: acquire decisions/s of the MI355X token-bucket engine (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): TokenBucket over 100M keys,
+uniform keys, batches of 2^26 requests, permits = 1, TokenLimit 10, 1 token / 1 s,
+batch b spans 10 ms of injected time.  A "step" is one batch: the full decision
+pipeline (partition, fold, un-partition) over 2^26 requests already resident in HBM.
+
+Multi-GPU (torchrun, one rank per GPU): keys are hash-partitioned, each rank owns
+100M / N keys in its own HBM and decides its own 2^26-request batches (no data-path
+collective: weak scaling).  value = all ranks' decisions / max-over-ranks time.
+
+Also reported: per-stage device time, the roofline of the dominant kernel (HIP events
+on the engine stream over the timed region), and the CPU baseline (the C restatement
+of the reference script, oracle/tb_ref.c, on a bounded sample of the same trace).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+SEED_B = 0x5EED000B
+T0_US = 1_760_000_000_000_000
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--keys", type=int, default=100_000_000)
+    ap.add_argument("--batch", type=int, default=1 << 26)
+    ap.add_argument("--interval-us", type=int, default=10_000)
+    ap.add_argument("--token-limit", type=int, default=10)
+    ap.add_argument("--tokens-per-period", type=int, default=1)
+    ap.add_argument("--period-ticks", type=int, default=10_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="approximate CPU-baseline budget (0 disables)")
+    ap.add_argument("--no-stage-timing", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as td
+        torch.cuda.set_device(local_rank)
+        td.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank if dist else 0)
+
+    from distributedratelimiting.redis_amd import TokenBucketEngine, _capi
+
+    lib = _capi.load()
+    lib.tbe_gen_batch_device.restype = ctypes.c_int
+    lib.tbe_gen_batch_device.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_int32] * 2 + \
+        [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 4
+
+    # Hash partition: this rank owns keys_local = ceil(K / world) dense local ids.  The
+    # synthetic stream is generated directly in the rank's local id space (uniform keys
+    # stay uniform under a hash partition); seeds differ per rank.
+    keys_local = (args.keys + world - 1) // world
+    n = args.batch
+    eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
+                            args.period_ticks, device=dev.index,
+                            stage_timing=not args.no_stage_timing, max_batch=n)
+    total_steps = args.warmup + args.steps
+    seed = SEED_B + 7919 * rank
+    bufs = []
+    for s in range(total_steps):
+        k = torch.empty(n, dtype=torch.int64, device=dev)
+        p = torch.empty(n, dtype=torch.int32, device=dev)
+        t = torch.empty(n, dtype=torch.int64, device=dev)
+        rc = lib.tbe_gen_batch_device(seed, keys_local, s * n, n, 1, 1, T0_US + s * args.interval_us,
+                                      args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), None)
+        assert rc == 0
+        bufs.append((k, p, t))
+    granted = torch.empty(n, dtype=torch.uint8, device=dev)
+    remaining = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    for s in range(args.warmup):
+        eng.acquire_batch_device(*bufs[s], granted, remaining)
+    eng.synchronize()
+    eng.stage_times()  # discard warm-up stage times
+
+    if dist:
+        td.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, total_steps):
+        eng.acquire_batch_device(*bufs[s], granted, remaining)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        td.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        td.all_reduce(tt, op=td.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = eng.stage_times()
+    grant_rate = float(granted.float().mean().item())
+
+    decisions = n * args.steps * world
+    value = decisions / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
+    roofline = None
+    if stages and sum(stages.values()) > 0:
+        passes = eng_passes(keys_local)
+        launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
+                    "unscatter": passes}
+        name = max(stages, key=stages.get)
+        per_launch_ms = stages[name] / (args.steps * launches[name])
+        alg_bytes = algorithmic_bytes(name, n, keys_local, passes)
+        achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic(name), "alg_bytes_per_launch": alg_bytes,
+                    "avg_launch_ms": round(per_launch_ms, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, keys_local)
+
+    if rank == 0:
+        line = {
+            "metric": "acquire decisions/sec (node) at 100M keys, 1/2/4/8 GPU; % HBM roofline",
+            "value": round(value, 1),
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 seeded trace generated in HBM)",
+            "config": {"workload": "TokenBucket 100M keys uniform, 2^26-request batches (config B)",
+                       "keys_total": args.keys, "keys_per_gpu": keys_local, "batch_per_gpu": n,
+                       "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
+                       "period_ticks": args.period_ticks, "interval_us": args.interval_us,
+                       "partitioning": f"key-hash x{world}, no data-path collective"},
+            "grant_rate_last_batch": round(grant_rate, 4),
+            "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        td.destroy_process_group()
+
+
+def eng_passes(n_keys: int) -> int:
+    kb = max(0, (n_keys - 1).bit_length())
+    r_bits = min(11, max(4, kb - 10))
+    nb = (n_keys + (1 << r_bits) - 1) >> r_bits
+    bb = max(0, (nb - 1).bit_length())
+    return max(1, (bb + 7) // 8)
+
+
+def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int) -> int:
+    """Bytes a launch of `stage` must move at minimum (DESIGN.md "Algorithmic bytes")."""
+    if stage == "fold":
+        # sorted records (key 4 + permits 4 + ts 8) + packed reply 4 per request, plus the
+        # touched table rows (16 B read + 16 B written per distinct key in the batch).
+        u = n_keys * (1.0 - np.exp(-n / n_keys))
+        return int(n * 20 + u * 32)
+    if stage == "scatter":
+        return n * (36 if passes == 1 else 34)   # averaged over passes: 20 in/16 out, 16/16
+    if stage == "hist":
+        return n * 6                              # 8 B keys (pass 0), 4 B after
+    if stage == "unscatter":
+        return n * 14                             # 12 B (inner passes) / 17 B (final)
+    if stage == "bounds":
+        return n * 4
+    return n * 4
+
+
+def pmc_traffic(stage: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(stage, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, n_keys: int):
+    """The C restatement of the reference script (oracle/tb_ref.c, serial like Redis'
+    single script thread) timed on the same trace: the first `sample` requests of each
+    batch, batches in order, until ~args.cpu_seconds of CPU work."""
+    from oracle import cref  # CPU baseline leg (checker library), never the product path
+    from distributedratelimiting.redis_amd import fill_rate
+
+    ref = cref.CTokenBucket(n_keys, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks))
+    sample = min(args.batch, 1 << 22)
+    done, spent, b = 0, 0.0, 0
+    while spent < args.cpu_seconds and b < 64:
+        k, p, t = cref.gen_batch(SEED_B, n_keys, b, args.batch, args.interval_us)
+        k, p, t = k[:sample], p[:sample], t[:sample]
+        t0 = time.perf_counter()
+        ref.acquire_batch(k, p, t, threads=1)
+        spent += time.perf_counter() - t0
+        done += sample
+        b += 1
+    ref.close()
+    return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} requests of each of {b} config-B batches "
+                      f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
+            "host_cpus": os.cpu_count()}
+
+
+if __name__ == "__main__":
+    main()

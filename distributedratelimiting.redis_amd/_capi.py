@@ -1,0 +1,95 @@
+"""ctypes binding of ``include/tbe.h`` (the engine's C ABI).
+
+This is the same surface a .NET host would P/Invoke.  Loading fails
+loudly when ``libtbe.so`` has not been built: there is no CPU fallback anywhere in
+the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_int32, c_int64, c_uint8,
+                    c_uint32, c_uint64, c_void_p)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtbe.so")
+
+TBE_OK, TBE_EINVAL, TBE_ENOMEM, TBE_EDEVICE, TBE_EDISPOSED, TBE_ERANGE = range(6)
+STATUS_NAMES = {0: "TBE_OK", 1: "TBE_EINVAL", 2: "TBE_ENOMEM", 3: "TBE_EDEVICE",
+                4: "TBE_EDISPOSED", 5: "TBE_ERANGE"}
+TBE_KIND_TOKEN_BUCKET, TBE_KIND_QUEUEING, TBE_KIND_APPROXIMATE = 0, 1, 2
+TBE_FLAG_STAGE_TIMING = 0x1
+STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter")
+
+# Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).
+EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe_acquire_batch",
+            "tbe_acquire_batch_device", "tbe_synchronize", "tbe_query", "tbe_export_state",
+            "tbe_stage_times")
+
+
+class TbeConfig(Structure):
+    _fields_ = [
+        ("struct_size", c_uint32),
+        ("kind", c_int32),
+        ("n_keys", c_uint64),
+        ("token_limit", c_int32),
+        ("tokens_per_period", c_int32),
+        ("replenishment_period_ticks", c_int64),
+        ("queue_limit", c_int32),
+        ("queue_order", c_int32),
+        ("device", c_int32),
+        ("flags", c_uint32),
+        ("max_batch", c_uint64),
+    ]
+
+
+class TbeError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libtbe.so (once).  Raises FileNotFoundError if it was never built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(
+            f"{path} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(path)
+    lib.tbe_fill_rate.restype = c_double
+    lib.tbe_fill_rate.argtypes = [c_int32, c_int64]
+    lib.tbe_create.restype = c_int32
+    lib.tbe_create.argtypes = [POINTER(TbeConfig), POINTER(c_void_p)]
+    lib.tbe_destroy.restype = None
+    lib.tbe_destroy.argtypes = [c_void_p]
+    lib.tbe_last_error.restype = c_char_p
+    lib.tbe_last_error.argtypes = [c_void_p]
+    lib.tbe_acquire_batch.restype = c_int32
+    lib.tbe_acquire_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+                                      c_void_p]
+    lib.tbe_acquire_batch_device.restype = c_int32
+    lib.tbe_acquire_batch_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64,
+                                             c_void_p, c_void_p, c_void_p]
+    lib.tbe_synchronize.restype = c_int32
+    lib.tbe_synchronize.argtypes = [c_void_p]
+    lib.tbe_query.restype = c_int32
+    lib.tbe_query.argtypes = [c_void_p, c_uint64, c_int64, POINTER(c_double), POINTER(c_double),
+                              POINTER(c_int32)]
+    lib.tbe_export_state.restype = c_int32
+    lib.tbe_export_state.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]
+    lib.tbe_stage_times.restype = c_int32
+    lib.tbe_stage_times.argtypes = [c_void_p, POINTER(c_double), c_uint32, POINTER(c_uint32)]
+    _lib = lib
+    return lib
+
+
+def make_config(n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
+                kind: int = TBE_KIND_TOKEN_BUCKET, queue_limit: int = 0, queue_order: int = 0,
+                device: int = -1, flags: int = 0, max_batch: int = 0) -> TbeConfig:
+    return TbeConfig(ctypes.sizeof(TbeConfig), kind, n_keys, token_limit, tokens_per_period,
+                     period_ticks, queue_limit, queue_order, device, flags, max_batch)

@@ -1,0 +1,51 @@
+"""Build the HIP engine in-tree: ``libtbe.so`` next to this file (gfx950 only).
+
+Flags that matter for parity: ``-ffp-contract=off`` (the reference script's
+``v + dt*rate`` is two roundings; an FMA would differ in ~3% of refills)
+and no fast-math (f64 division must stay the IEEE-correct sequence).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SOURCES = [os.path.join(HERE, "csrc", "tbe_engine.hip"), os.path.join(HERE, "csrc", "tbe_tools.hip")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", "tbe_device.hpp"),
+                  os.path.join(ROOT, "include", "tbe.h"), os.path.join(ROOT, "include", "tbe_tools.h")]
+LIB = os.path.join(HERE, "libtbe.so")
+ARCH = "gfx950"
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+               "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise FileNotFoundError("hipcc not found")
+
+
+def up_to_date(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date(LIB, DEPS):
+        return LIB
+    cmd = [hipcc()] + HIPCC_FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_engine(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,782 @@
+// tbe_engine.hip -- MI355X batched token-bucket engine: kernels, orchestration, C ABI.
+//
+// Replaces the reference's per-request Redis script round-trip
+// (TokenBucket/RedisTokenBucketRateLimiter.cs:63, PartitionedRedisTokenBucketRateLimiter.cs:42)
+// with one batched pipeline over an HBM-resident bucket table.  Per batch of n requests
+// (arrival order i = 0..n-1):
+//
+//   bucket b(key) = key >> r_bits  (2^r_bits keys per bucket; 2^11 at 1e8 keys)
+//   1. LSD stable partition of the requests by b, P = ceil(bits(b)/8) passes of 8 bits:
+//        k_hist    per-tile digit histograms (+ running in-block prefix)
+//        k_colscan digit-column scan of the per-block sums -> global digit offsets
+//        k_scatter stable local rank (wave ballot-match) -> LDS staging -> coalesced runs
+//      After the last pass the requests are grouped by bucket, arrival order kept inside.
+//   2. k_bounds: first sorted position of every bucket.
+//   3. k_fold: one workgroup per bucket.  The bucket's 2^r_bits table rows are the only
+//      state it touches; rows a request needs are pulled into LDS on first touch.
+//      Requests are taken in arrival order, 1024 at a time; within such a chunk, lanes
+//      whose keys differ decide concurrently while requests for the same key go in
+//      rounds, earliest first (LDS atomicMin "owner" election), so per-key order is the
+//      reference's serial order.  Dirty rows are written back once.
+//   4. k_unscatter: the P partitions run backwards (same local ranks recomputed from the
+//      keys) to return {granted, remaining} in arrival order with coalesced runs.
+//
+// Memory-bound integer/byte work plus a little FP64; no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/tbe.h"
+#include "tbe_device.hpp"
+
+#pragma clang fp contract(off)
+
+using namespace tbe;
+
+namespace {
+
+constexpr int kScatterItems = 8;                       // elements per thread per tile
+constexpr int kTile = kBlock * kScatterItems;          // 2048 requests per tile
+constexpr int kMaxHistBlocks = 1024;
+constexpr int kFoldItems = 4;                          // requests per thread per chunk
+constexpr int kChunk = kBlock * kFoldItems;            // 1024
+constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
+
+// ----------------------------------------------------------------------------- kernels
+// Per-tile digit histograms.  Block j walks tiles [j*tpb, (j+1)*tpb) in order and
+// writes for each tile the exclusive running count per digit within its block
+// (tileprefix) and, at the end, the block's totals (blocksum).  Pass 0 also validates
+// keys (key < n_keys).
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
+                                                 int shift, uint32_t tiles_per_blk,
+                                                 uint32_t ntiles, uint32_t *__restrict__ tileprefix,
+                                                 uint32_t *__restrict__ blocksum, uint64_t n_keys,
+                                                 uint32_t *__restrict__ err, int validate) {
+    __shared__ uint32_t h[kDigits];
+    const int tid = threadIdx.x;
+    const uint32_t t0 = blockIdx.x * tiles_per_blk;
+    const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
+    uint32_t run = 0;
+    bool bad = false;
+    for (uint32_t t = t0; t < t1; ++t) {
+        h[tid] = 0;
+        __syncthreads();
+        const uint64_t base = (uint64_t)t * kTile;
+#pragma unroll
+        for (int it = 0; it < kScatterItems; ++it) {
+            const uint64_t i = base + it * kBlock + tid;
+            if (i < n) {
+                const uint64_t k = (uint64_t)keys[i];
+                bad |= validate && (k >= n_keys);
+                // Digit of the 32-bit key, exactly as k_scatter computes it, so the
+                // counts stay consistent even for an (invalid) key >= 2^32.
+                atomicAdd(&h[((uint32_t)k >> shift) & (kDigits - 1)], 1u);
+            }
+        }
+        __syncthreads();
+        const uint32_t c = h[tid];
+        tileprefix[(uint64_t)t * kDigits + tid] = run;
+        run += c;
+        __syncthreads();
+    }
+    blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
+    if (__any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
+}
+
+// Digit-column scan over the per-block sums: blockprefix[j][d] = global position of the
+// first element with digit d that block j owns (digit base + earlier blocks' counts).
+__global__ __launch_bounds__(kBlock) void k_colscan(const uint32_t *__restrict__ blocksum,
+                                                    uint32_t nblk,
+                                                    uint32_t *__restrict__ blockprefix) {
+    __shared__ uint32_t wsum[kWaves];
+    const int d = threadIdx.x;
+    uint32_t s = 0;
+    uint32_t j = 0;
+    for (; j + 8 <= nblk; j += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = blocksum[(uint64_t)(j + u) * kDigits + d];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            blockprefix[(uint64_t)(j + u) * kDigits + d] = s;
+            s += c[u];
+        }
+    }
+    for (; j < nblk; ++j) {
+        const uint32_t c = blocksum[(uint64_t)j * kDigits + d];
+        blockprefix[(uint64_t)j * kDigits + d] = s;
+        s += c;
+    }
+    uint32_t total;
+    const uint32_t base = block_excl_scan(s, wsum, &total);
+    for (j = 0; j < nblk; ++j) blockprefix[(uint64_t)j * kDigits + d] += base;
+}
+
+// Stable partition of one tile by digit d = (key >> shift) & 255.  Payload travels as
+// SoA {key u32, permits i32, ts i64}.  Two staging rounds (8 B each) keep LDS at 32 KB.
+template <typename KeyIn>
+__global__ __launch_bounds__(kBlock) void k_scatter(
+    const KeyIn *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
+    uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
+    const uint32_t *__restrict__ blockprefix, uint32_t tiles_per_blk, uint32_t *__restrict__ kout,
+    int32_t *__restrict__ pout, int64_t *__restrict__ tout, uint32_t *__restrict__ err,
+    int validate) {
+    __shared__ uint16_t cnt[kScatterItems * kWaves * kDigits];
+    __shared__ uint32_t lstart[kDigits];
+    __shared__ uint32_t goff[kDigits];
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint64_t stage[kTile];
+
+    const int tid = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * kTile;
+    const int nvalid = (int)min<uint64_t>(kTile, n - base);
+    goff[tid] = blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
+                tileprefix[(uint64_t)tile * kDigits + tid];
+
+    // Issue every load of the tile up front; the payload waits in registers while the
+    // ranks are computed.
+    uint32_t key[kScatterItems], dig[kScatterItems], lpos[kScatterItems], gpos[kScatterItems];
+    int32_t pm[kScatterItems];
+    int64_t tv[kScatterItems];
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int e = it * kBlock + tid;
+        const bool v = e < nvalid;
+        key[it] = v ? (uint32_t)kin[base + e] : 0u;
+        pm[it] = v ? pin[base + e] : 0;
+        tv[it] = v ? tin[base + e] : 0;
+        dig[it] = (key[it] >> shift) & (kDigits - 1);
+    }
+    rank_tile<kScatterItems>(dig, nvalid, cnt, lstart, wsum, lpos);
+
+    bool bad = false;
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int e = it * kBlock + tid;
+        if (e < nvalid) {
+            bad |= validate && (pm[it] < 0 || tv[it] < 0);
+            stage[lpos[it]] = ((uint64_t)key[it] << 32) | (uint32_t)pm[it];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int j = it * kBlock + tid;
+        if (j < nvalid) {
+            const uint64_t s = stage[j];
+            const uint32_t k = (uint32_t)(s >> 32);
+            const uint32_t d = (k >> shift) & (kDigits - 1);
+            gpos[it] = goff[d] + (uint32_t)j - lstart[d];
+            kout[gpos[it]] = k;
+            pout[gpos[it]] = (int32_t)(uint32_t)s;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int e = it * kBlock + tid;
+        if (e < nvalid) stage[lpos[it]] = (uint64_t)tv[it];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int j = it * kBlock + tid;
+        if (j < nvalid) tout[gpos[it]] = (int64_t)stage[j];
+    }
+    if (validate && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
+}
+
+// bstart[b] = first sorted position with bucket >= b, for b in [0, nb]; bstart[nb] = n.
+__global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t *__restrict__ skeys, uint64_t n,
+                                                   int r_bits, uint32_t nb,
+                                                   uint32_t *__restrict__ bstart,
+                                                   const uint32_t *__restrict__ err) {
+    if (*err) return;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = (int64_t)(skeys[i] >> r_bits);
+    const int64_t prev = (i == 0) ? -1 : (int64_t)(skeys[i - 1] >> r_bits);
+    for (int64_t q = prev + 1; q <= b; ++q) bstart[q] = (uint32_t)i;
+    if (i == n - 1)
+        for (int64_t q = b + 1; q <= (int64_t)nb; ++q) bstart[q] = (uint32_t)n;
+}
+
+// Decide every request of one bucket (see file header).  res[q] is the packed reply of
+// sorted request q (bit 31 granted, bits 0-30 remaining).
+__global__ __launch_bounds__(kBlock) void k_fold(
+    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
+    const int64_t *__restrict__ sts, const uint32_t *__restrict__ bstart, int r_bits,
+    Slot *__restrict__ table, TbParams P, uint32_t *__restrict__ res,
+    const uint32_t *__restrict__ err) {
+    __shared__ Slot slot[1 << kMaxRBits];
+    __shared__ uint32_t own[1 << kMaxRBits];
+    __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
+    __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
+
+    if (*err) return;
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) return;
+    const uint32_t R = 1u << r_bits;
+    const uint32_t rmask = R - 1;
+    Slot *__restrict__ rows = table + ((uint64_t)b << r_bits);
+
+    for (uint32_t j = tid; j < R; j += kBlock) own[j] = kNoOwner;
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kBlock) {
+        loaded[j] = 0;
+        dirty[j] = 0;
+    }
+    __syncthreads();
+
+    for (uint32_t c = s; c < e; c += kChunk) {
+        uint32_t kl[kFoldItems];
+        int32_t pm[kFoldItems];
+        int64_t ts[kFoldItems];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldItems; ++r) {
+            const uint32_t q = c + r * kBlock + tid;
+            if (q < e) {
+                kl[r] = skeys[q] & rmask;
+                pm[r] = sperm[q];
+                ts[r] = sts[q];
+                pend |= 1u << r;
+            } else {
+                kl[r] = 0;
+                pm[r] = 0;
+                ts[r] = 0;
+            }
+        }
+        // First touch of a row in this bucket pulls it into LDS.
+#pragma unroll
+        for (int r = 0; r < kFoldItems; ++r) {
+            if (pend & (1u << r)) {
+                const uint32_t bit = 1u << (kl[r] & 31);
+                const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
+                if (!(old & bit)) slot[kl[r]] = rows[kl[r]];
+            }
+        }
+        __syncthreads();
+        // Owner rounds: the earliest pending request of each key decides this round.
+        for (;;) {
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kBlock + tid));
+            __syncthreads();
+            uint32_t won = 0;
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r) {
+                if ((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kBlock + tid)) {
+                    bool g;
+                    Slot st = slot[kl[r]];
+                    res[c + r * kBlock + tid] = tb_acquire(st, pm[r], ts[r], P, g);
+                    if (g) {
+                        slot[kl[r]] = st;
+                        atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                    }
+                    won |= 1u << r;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (won & (1u << r)) own[kl[r]] = kNoOwner;
+            pend &= ~won;
+            if (!__syncthreads_or(pend != 0)) break;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < R; j += kBlock)
+        if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = slot[j];
+}
+
+// Inverse of one k_scatter pass: recompute the tile's local ranks from the pass-input
+// keys, gather the replies from the pass-output positions, store them in pass-input
+// order.  FINAL = pass 0: unpack into granted (u8) / remaining (i32).
+template <typename KeyIn, bool FINAL>
+__global__ __launch_bounds__(kBlock) void k_unscatter(
+    const KeyIn *__restrict__ kin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
+    const uint32_t *__restrict__ blockprefix, uint32_t tiles_per_blk,
+    const uint32_t *__restrict__ res_in, uint32_t *__restrict__ res_out,
+    uint8_t *__restrict__ granted, int32_t *__restrict__ remaining) {
+    __shared__ uint16_t cnt[kScatterItems * kWaves * kDigits];
+    __shared__ uint32_t lstart[kDigits];
+    __shared__ uint32_t goff[kDigits];
+    __shared__ uint32_t wsum[kWaves];
+
+    const int tid = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * kTile;
+    const int nvalid = (int)min<uint64_t>(kTile, n - base);
+    goff[tid] = blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
+                tileprefix[(uint64_t)tile * kDigits + tid];
+    uint32_t dig[kScatterItems], lpos[kScatterItems];
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int e = it * kBlock + tid;
+        const uint32_t k = (e < nvalid) ? (uint32_t)kin[base + e] : 0u;
+        dig[it] = (k >> shift) & (kDigits - 1);
+    }
+    rank_tile<kScatterItems>(dig, nvalid, cnt, lstart, wsum, lpos);
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const int e = it * kBlock + tid;
+        if (e < nvalid) {
+            const uint32_t r = res_in[goff[dig[it]] + lpos[it] - lstart[dig[it]]];
+            if (FINAL) {
+                granted[base + e] = (uint8_t)(r >> 31);
+                remaining[base + e] = (int32_t)(r & 0x7FFFFFFFu);
+            } else {
+                res_out[base + e] = r;
+            }
+        }
+    }
+}
+
+__global__ void k_init_table(Slot *__restrict__ table, uint64_t n_keys, double cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = i; k < n_keys; k += stride) table[k] = Slot{cap, kAbsent};
+}
+
+__global__ void k_sticky(const uint32_t *__restrict__ err, uint32_t *__restrict__ sticky) {
+    if (threadIdx.x == 0 && *err) *sticky = 1u;
+}
+
+// ----------------------------------------------------------------------------- host side
+enum Stage { ST_HIST = 0, ST_COLSCAN, ST_SCATTER, ST_BOUNDS, ST_FOLD, ST_UNSCATTER, ST_COUNT };
+
+struct PassBufs {
+    uint32_t *keys = nullptr;    // pass output (u32 keys)
+    int32_t *permits = nullptr;
+    int64_t *ts = nullptr;
+    uint32_t *tileprefix = nullptr;
+    uint32_t *blockprefix = nullptr;
+};
+
+inline int ceil_log2(uint64_t x) {
+    int b = 0;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
+
+}  // namespace
+
+struct tbe_engine {
+    tbe_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    TbParams params{};
+    int r_bits = 0;          // bucket = key >> r_bits
+    uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
+    int passes = 0;          // 8-bit LSD passes over the bucket id
+    Slot *table = nullptr;
+
+    // workspace (sized for `cap_n` requests)
+    uint64_t cap_n = 0;
+    std::vector<PassBufs> pass;
+    uint32_t *blocksum = nullptr;
+    uint32_t *res[2] = {nullptr, nullptr};
+    uint32_t *bstart = nullptr;
+    uint32_t *err = nullptr;     // [0] per-batch flag, [1] sticky flag
+    // host-buffer path staging
+    uint64_t *d_keys = nullptr;
+    int32_t *d_permits = nullptr;
+    int64_t *d_ts = nullptr;
+    uint8_t *d_granted = nullptr;
+    int32_t *d_remaining = nullptr;
+
+    // Stage timing (TBE_FLAG_STAGE_TIMING): an event pair per stage per batch, recorded
+    // on the launch stream without any host synchronisation; read in tbe_stage_times.
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<std::pair<int, size_t>> ev_marks;   // (stage, index of start event)
+    int open_stage = -1;
+    std::string last_error = "ok";
+};
+
+namespace {
+
+tbe_status fail(tbe_engine *e, tbe_status st, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (e) e->last_error = buf;
+    return st;
+}
+
+#define HIP_TRY(e, expr)                                                                    \
+    do {                                                                                    \
+        hipError_t _rc = (expr);                                                            \
+        if (_rc != hipSuccess)                                                              \
+            return fail((e), _rc == hipErrorOutOfMemory ? TBE_ENOMEM : TBE_EDEVICE,         \
+                        "%s failed: %s", #expr, hipGetErrorString(_rc));                    \
+    } while (0)
+
+template <typename T>
+void dfree(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_workspace(tbe_engine *e) {
+    for (auto &pb : e->pass) {
+        dfree(pb.keys);
+        dfree(pb.permits);
+        dfree(pb.ts);
+        dfree(pb.tileprefix);
+        dfree(pb.blockprefix);
+    }
+    e->pass.clear();
+    dfree(e->blocksum);
+    dfree(e->res[0]);
+    dfree(e->res[1]);
+    dfree(e->d_keys);
+    dfree(e->d_permits);
+    dfree(e->d_ts);
+    dfree(e->d_granted);
+    dfree(e->d_remaining);
+    e->cap_n = 0;
+}
+
+void tiles_for(uint64_t n, uint32_t &ntiles, uint32_t &nblk, uint32_t &tpb) {
+    ntiles = (uint32_t)((n + kTile - 1) / kTile);
+    tpb = (ntiles + kMaxHistBlocks - 1) / kMaxHistBlocks;
+    if (tpb == 0) tpb = 1;
+    nblk = (ntiles + tpb - 1) / tpb;
+}
+
+tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
+    if (n <= e->cap_n) return TBE_OK;
+    free_workspace(e);
+    uint64_t cap = std::max<uint64_t>(n, 1u << 16);
+    uint32_t ntiles, nblk, tpb;
+    tiles_for(cap, ntiles, nblk, tpb);
+    e->pass.resize(e->passes);
+    for (auto &pb : e->pass) {
+        HIP_TRY(e, hipMalloc(&pb.keys, cap * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
+        HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
+        HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
+    }
+    HIP_TRY(e, hipMalloc(&e->blocksum, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&e->res[0], cap * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&e->res[1], cap * sizeof(uint32_t)));
+    e->cap_n = cap;
+    return TBE_OK;
+}
+
+tbe_status ensure_host_staging(tbe_engine *e, uint64_t n) {
+    // Staging for the host-buffer entry point lives with the workspace; reallocated with it.
+    if (e->d_keys && n <= e->cap_n) return TBE_OK;
+    tbe_status st = ensure_workspace(e, n);
+    if (st != TBE_OK) return st;
+    if (!e->d_keys) {
+        HIP_TRY(e, hipMalloc(&e->d_keys, e->cap_n * sizeof(uint64_t)));
+        HIP_TRY(e, hipMalloc(&e->d_permits, e->cap_n * sizeof(int32_t)));
+        HIP_TRY(e, hipMalloc(&e->d_ts, e->cap_n * sizeof(int64_t)));
+        HIP_TRY(e, hipMalloc(&e->d_granted, e->cap_n * sizeof(uint8_t)));
+        HIP_TRY(e, hipMalloc(&e->d_remaining, e->cap_n * sizeof(int32_t)));
+    }
+    return TBE_OK;
+}
+
+hipEvent_t next_event(tbe_engine *e) {
+    if (e->ev_used == e->ev_pool.size()) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        e->ev_pool.push_back(ev);
+    }
+    return e->ev_pool[e->ev_used++];
+}
+inline void stage_begin(tbe_engine *e, int s, hipStream_t st) {
+    if (!e->timing) return;
+    const size_t idx = e->ev_used;
+    hipEvent_t a = next_event(e), b = next_event(e);
+    if (!a || !b) return;
+    (void)hipEventRecord(a, st);
+    e->ev_marks.emplace_back(s, idx);
+    (void)b;
+}
+inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
+    if (!e->timing || e->ev_marks.empty() || e->ev_marks.back().first != s) return;
+    (void)hipEventRecord(e->ev_pool[e->ev_marks.back().second + 1], st);
+}
+
+// Enqueue the whole pipeline for one device-resident batch.
+tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                     const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
+                     hipStream_t st) {
+    if (n == 0) return TBE_OK;
+    if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
+                                       (unsigned long long)n);
+    tbe_status rc = ensure_workspace(e, n);
+    if (rc != TBE_OK) return rc;
+    uint32_t ntiles, nblk, tpb;
+    tiles_for(n, ntiles, nblk, tpb);
+    HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(uint32_t), st));
+
+    for (int p = 0; p < e->passes; ++p) {
+        const int shift = e->r_bits + kDigitBits * p;
+        PassBufs &out = e->pass[p];
+        stage_begin(e, ST_HIST, st);
+        if (p == 0)
+            k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+                                                       e->blocksum, e->cfg.n_keys, e->err, 1);
+        else
+            k_hist<uint32_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].keys, n, shift, tpb, ntiles,
+                                                       out.tileprefix, e->blocksum, e->cfg.n_keys,
+                                                       e->err, 0);
+        stage_end(e, ST_HIST, st);
+        stage_begin(e, ST_COLSCAN, st);
+        k_colscan<<<1, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix);
+        stage_end(e, ST_COLSCAN, st);
+        stage_begin(e, ST_SCATTER, st);
+        if (p == 0)
+            k_scatter<uint64_t><<<ntiles, kBlock, 0, st>>>(
+                keys, permits, ts, n, shift, out.tileprefix, out.blockprefix, tpb, out.keys,
+                out.permits, out.ts, e->err, 1);
+        else
+            k_scatter<uint32_t><<<ntiles, kBlock, 0, st>>>(
+                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, n, shift,
+                out.tileprefix, out.blockprefix, tpb, out.keys, out.permits, out.ts, e->err, 0);
+        stage_end(e, ST_SCATTER, st);
+    }
+    const PassBufs &sorted = e->pass[e->passes - 1];
+    stage_begin(e, ST_BOUNDS, st);
+    k_bounds<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        sorted.keys, n, e->r_bits, e->nbuckets, e->bstart, e->err);
+    stage_end(e, ST_BOUNDS, st);
+    stage_begin(e, ST_FOLD, st);
+    k_fold<<<e->nbuckets, kBlock, 0, st>>>(sorted.keys, sorted.permits, sorted.ts, e->bstart,
+                                           e->r_bits, e->table, e->params, e->res[0], e->err);
+    stage_end(e, ST_FOLD, st);
+    stage_begin(e, ST_UNSCATTER, st);
+    int cur = 0;
+    for (int p = e->passes - 1; p >= 1; --p) {
+        k_unscatter<uint32_t, false><<<ntiles, kBlock, 0, st>>>(
+            e->pass[p - 1].keys, n, e->r_bits + kDigitBits * p, e->pass[p].tileprefix,
+            e->pass[p].blockprefix, tpb, e->res[cur], e->res[cur ^ 1], nullptr, nullptr);
+        cur ^= 1;
+    }
+    k_unscatter<uint64_t, true><<<ntiles, kBlock, 0, st>>>(
+        keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix, tpb, e->res[cur],
+        nullptr, granted, remaining);
+    stage_end(e, ST_UNSCATTER, st);
+    k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
+    HIP_TRY(e, hipGetLastError());
+    return TBE_OK;
+}
+
+}  // namespace
+
+// ============================================================================= C ABI
+extern "C" {
+
+double tbe_fill_rate(int32_t tokens_per_period, int64_t replenishment_period_ticks) {
+    const double total_seconds = (double)replenishment_period_ticks / 10000000.0;
+    return (double)tokens_per_period / total_seconds;
+}
+
+tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
+    if (!out_engine) return TBE_EINVAL;
+    *out_engine = nullptr;
+    if (!config || config->struct_size < sizeof(tbe_config)) return TBE_EINVAL;
+    const tbe_config &c = *config;
+    if (c.kind != TBE_KIND_TOKEN_BUCKET) return TBE_EINVAL;
+    if (c.n_keys == 0 || c.n_keys > (1ull << 32)) return TBE_EINVAL;
+    if (c.token_limit <= 0 || c.tokens_per_period <= 0) return TBE_EINVAL;   // TB:29-32
+    if (c.replenishment_period_ticks <= 0) return TBE_EINVAL;                // TB:34-37 (+ "∞")
+    const double rate = tbe_fill_rate(c.tokens_per_period, c.replenishment_period_ticks);
+    if (!std::isfinite(rate) || !(rate > 0.0)) return TBE_EINVAL;
+
+    tbe_engine *e = new (std::nothrow) tbe_engine();
+    if (!e) return TBE_ENOMEM;
+    e->cfg = c;
+    e->params.cap = (double)c.token_limit;
+    e->params.rate = rate;
+    {
+        // TB:234: math.ceil(math.min(math.max(capacity / fill_rate, 1), 31536000))
+        double q = (double)c.token_limit / rate;
+        q = (1.0 > q) ? 1.0 : q;
+        q = (31536000.0 < q) ? 31536000.0 : q;
+        e->params.ttl_ms = (int64_t)std::ceil(q) * 1000;
+    }
+    const int kb = ceil_log2(c.n_keys);
+    e->r_bits = std::min(kMaxRBits, std::max(4, kb - 10));
+    e->nbuckets = (uint32_t)((c.n_keys + (1ull << e->r_bits) - 1) >> e->r_bits);
+    const int bbits = ceil_log2(e->nbuckets);
+    e->passes = std::max(1, (bbits + kDigitBits - 1) / kDigitBits);
+    e->timing = (c.flags & TBE_FLAG_STAGE_TIMING) != 0;
+
+    auto bail = [&](tbe_status st) {
+        tbe_destroy(e);
+        return st;
+    };
+    if (c.device >= 0) {
+        if (hipSetDevice(c.device) != hipSuccess) return bail(TBE_EDEVICE);
+        e->device = c.device;
+    } else if (hipGetDevice(&e->device) != hipSuccess) {
+        return bail(TBE_EDEVICE);
+    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(TBE_EDEVICE);
+    e->own_stream = true;
+    if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (hipMalloc(&e->bstart, ((uint64_t)e->nbuckets + 1) * sizeof(uint32_t)) != hipSuccess)
+        return bail(TBE_ENOMEM);
+    if (hipMalloc(&e->err, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (hipMemsetAsync(e->err, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess)
+        return bail(TBE_EDEVICE);
+    k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
+    if (c.max_batch && ensure_workspace(e, c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(TBE_EDEVICE);
+    *out_engine = e;
+    return TBE_OK;
+}
+
+void tbe_destroy(tbe_engine *e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    free_workspace(e);
+    dfree(e->table);
+    dfree(e->bstart);
+    dfree(e->err);
+    for (auto &ev : e->ev_pool)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char *tbe_last_error(const tbe_engine *e) {
+    return e ? e->last_error.c_str() : "null engine";
+}
+
+tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                             const int64_t *ts_us, uint64_t n, uint8_t *granted,
+                             int32_t *remaining) {
+    if (!e) return TBE_EINVAL;
+    if (n == 0) return TBE_OK;
+    if (!keys || !permits || !ts_us || !granted || !remaining)
+        return fail(e, TBE_EINVAL, "null buffer");
+    HIP_TRY(e, hipSetDevice(e->device));
+    tbe_status rc = ensure_host_staging(e, n);
+    if (rc != TBE_OK) return rc;
+    hipStream_t st = e->stream;
+    HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    rc = run_batch(e, e->d_keys, e->d_permits, e->d_ts, n, e->d_granted, e->d_remaining, st);
+    if (rc != TBE_OK) return rc;
+    uint32_t flag = 0;
+    HIP_TRY(e, hipMemcpyAsync(&flag, e->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(granted, e->d_granted, n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipStreamSynchronize(st));
+    if (flag) {
+        HIP_TRY(e, hipMemsetAsync(e->err + 1, 0, sizeof(uint32_t), st));
+        HIP_TRY(e, hipStreamSynchronize(st));
+        return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
+    }
+    return TBE_OK;
+}
+
+tbe_status tbe_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys, const int32_t *d_permits,
+                                    const int64_t *d_ts_us, uint64_t n, uint8_t *d_granted,
+                                    int32_t *d_remaining, void *stream) {
+    if (!e) return TBE_EINVAL;
+    if (n == 0) return TBE_OK;
+    if (!d_keys || !d_permits || !d_ts_us || !d_granted || !d_remaining)
+        return fail(e, TBE_EINVAL, "null buffer");
+    HIP_TRY(e, hipSetDevice(e->device));
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    return run_batch(e, d_keys, d_permits, d_ts_us, n, d_granted, d_remaining, st);
+}
+
+tbe_status tbe_synchronize(tbe_engine *e) {
+    if (!e) return TBE_EINVAL;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());
+    uint32_t sticky = 0;
+    HIP_TRY(e, hipMemcpy(&sticky, e->err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (sticky) {
+        HIP_TRY(e, hipMemset(e->err + 1, 0, sizeof(uint32_t)));
+        return fail(e, TBE_EINVAL, "an enqueued batch held an invalid request and was skipped");
+    }
+    return TBE_OK;
+}
+
+tbe_status tbe_query(tbe_engine *e, uint64_t key, int64_t ts_us, double *v, double *t,
+                     int32_t *present) {
+    if (!e || !v || !t || !present) return TBE_EINVAL;
+    if (key >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
+    HIP_TRY(e, hipSetDevice(e->device));
+    Slot s;
+    HIP_TRY(e, hipMemcpyAsync(&s, e->table + key, sizeof(Slot), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    *present = 0;
+    *v = 0.0;
+    *t = 0.0;
+    if (s.t_us == kAbsent) return TBE_OK;
+    if (ts_us >= 0 && (ts_us / 1000) > (s.t_us / 1000) + e->params.ttl_ms) return TBE_OK;
+    *present = 1;
+    *v = s.v;
+    const int64_t sec = s.t_us / 1000000, usec = s.t_us - sec * 1000000;
+    *t = (double)sec + ((double)usec / 1000000.0);
+    return TBE_OK;
+}
+
+tbe_status tbe_export_state(tbe_engine *e, uint64_t first, uint64_t count, double *v, int64_t *t_us) {
+    if (!e || !v || !t_us) return TBE_EINVAL;
+    if (first > e->cfg.n_keys || count > e->cfg.n_keys - first)
+        return fail(e, TBE_EINVAL, "range out of bounds");
+    if (count == 0) return TBE_OK;
+    HIP_TRY(e, hipSetDevice(e->device));
+    std::vector<Slot> tmp(count);
+    HIP_TRY(e, hipMemcpyAsync(tmp.data(), e->table + first, count * sizeof(Slot),
+                              hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    for (uint64_t i = 0; i < count; ++i) {
+        v[i] = tmp[i].v;
+        t_us[i] = tmp[i].t_us;
+    }
+    return TBE_OK;
+}
+
+tbe_status tbe_stage_times(tbe_engine *e, double *out, uint32_t n_out, uint32_t *n_written) {
+    if (!e || !out || !n_written) return TBE_EINVAL;
+    double ms_sum[ST_COUNT] = {};
+    if (!e->ev_marks.empty()) {
+        HIP_TRY(e, hipSetDevice(e->device));
+        HIP_TRY(e, hipEventSynchronize(e->ev_pool[e->ev_marks.back().second + 1]));
+        for (const auto &m : e->ev_marks) {
+            float ms = 0.f;
+            HIP_TRY(e, hipEventElapsedTime(&ms, e->ev_pool[m.second], e->ev_pool[m.second + 1]));
+            ms_sum[m.first] += ms;
+        }
+    }
+    e->ev_marks.clear();
+    e->ev_used = 0;
+    const uint32_t m = std::min<uint32_t>(n_out, ST_COUNT);
+    for (uint32_t i = 0; i < m; ++i) out[i] = ms_sum[i];
+    *n_written = m;
+    return TBE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+/*
+ * tbe.h -- C ABI of the MI355X batched token-bucket engine ("tbe").
+ *
+ * This is the drop-in boundary.  In the reference every decision is one
+ * StackExchange.Redis script round-trip; the entry points below replace those
+ * call sites with batched calls into an HBM-resident bucket table on one GPU.
+ * References are to /root/reference/DistributedRateLimiting.Redis/ (aliases as in
+ * TB = TokenBucket/RedisTokenBucketRateLimiter.cs, PTB =
+ * TokenBucket/PartitionedRedisTokenBucketRateLimiter.cs, TBO = TokenBucket/
+ * RedisTokenBucketRateLimiterOptions.cs).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no C++ or HIP types cross this boundary.
+ *  - Every function returns a tbe_status; no exception ever crosses the ABI.
+ *  - An engine is NOT re-entrant: one submitting thread per engine.  Batch order
+ *    is arrival order: request i of a batch is decided after request i-1 of the
+ *    same batch and after every request of earlier batches (the order Redis
+ *    serialises script calls in, TB:63).
+ *  - Keys are dense ids in [0, n_keys).  Mapping InstanceName + resourceID
+ *    strings (PTB:42) to ids is the caller's job.
+ *  - Timestamps are injected microseconds since the Unix epoch (>= 0); they play
+ *    the role of Redis `TIME` inside the script (TB:202-203).
+ */
+#ifndef TBE_H_
+#define TBE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TBE_ABI_VERSION 1
+
+typedef enum tbe_status {
+    TBE_OK = 0,
+    TBE_EINVAL = 1,     /* bad argument / invalid request in a batch (nothing applied):
+                           ArgumentException / ArgumentOutOfRangeException (TB:24-42) */
+    TBE_ENOMEM = 2,     /* device or host allocation failed */
+    TBE_EDEVICE = 3,    /* HIP runtime error; the engine should be destroyed */
+    TBE_EDISPOSED = 4,  /* engine already disposed: ObjectDisposedException (TB:158-164) */
+    TBE_ERANGE = 5      /* permits > TokenLimit where the limiter forbids it (A:87-90) */
+} tbe_status;
+
+typedef enum tbe_kind {
+    TBE_KIND_TOKEN_BUCKET = 0,   /* TokenBucket/ (TB, PTB)                                */
+    TBE_KIND_QUEUEING = 1,       /* TokenBucketWithQueue/ (reserved) */
+    TBE_KIND_APPROXIMATE = 2     /* ApproximateTokenBucket/ (reserved; §8a a9-a12)        */
+} tbe_kind;
+
+/* Limiter options (TBO:9-85) plus engine sizing.  The Redis connection options
+ * (Configuration, ConfigurationOptions, ConnectionMultiplexerFactory, TBO:48-60) and
+ * the ProfilingSession (TBO:70) have no counterpart: the "connection" is the device. */
+typedef struct tbe_config {
+    uint32_t struct_size;                 /* sizeof(tbe_config) */
+    int32_t kind;                         /* tbe_kind */
+    uint64_t n_keys;                      /* table capacity, 1 <= n_keys <= 2^32 */
+    int32_t token_limit;                  /* TokenLimit (TBO:43), > 0 */
+    int32_t tokens_per_period;            /* TokensPerPeriod (TBO:30), > 0 */
+    int64_t replenishment_period_ticks;   /* ReplenishmentPeriod in .NET ticks (100 ns), > 0 */
+    int32_t queue_limit;                  /* QueueLimit (queueing kind; ignored otherwise) */
+    int32_t queue_order;                  /* 0 = OldestFirst, 1 = NewestFirst */
+    int32_t device;                       /* HIP device ordinal; -1 = current device */
+    uint32_t flags;                       /* TBE_FLAG_* */
+    uint64_t max_batch;                   /* expected largest batch (workspace pre-sizing); 0 = grow on demand */
+} tbe_config;
+
+#define TBE_FLAG_STAGE_TIMING 0x1u        /* record per-stage HIP events (tbe_stage_times) */
+
+typedef struct tbe_engine tbe_engine;
+
+/* Fill rate the engine computes from the options exactly like FillRatePerSecond
+ * (TBO:82-85): (double)tokens_per_period / (ticks / 1e7).  Raw f64, as the script
+ * literal `fill_rate` (TB:185) round-trips it. */
+double tbe_fill_rate(int32_t tokens_per_period, int64_t replenishment_period_ticks);
+
+/* Replaces the constructor + lazy connect (TB:22-46, TB:111-151).  Allocates the
+ * table (16 B per key) on the device, every key absent. */
+tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine);
+
+/* Replaces Dispose / DisposeAsyncCore (TB:85-109).  NULL is ignored. */
+void tbe_destroy(tbe_engine *engine);
+
+/* Human-readable description of the last non-OK status on this engine (never NULL). */
+const char *tbe_last_error(const tbe_engine *engine);
+
+/* Replaces n sequential IDatabase.ScriptEvaluateAsync(_acquireScript,
+ * {BucketId, PermitCount}) calls (TB:63; PTB:42) and their reply parsing (TB:64-81).
+ * Host buffers; synchronous.  granted[i] = 1 iff reply[0] == 1 (TB:76); remaining[i]
+ * = reply[1] = trunc(new_v) after the decision (TB:73, TB:238).
+ * Invalid batch (key >= n_keys, permits < 0, ts_us < 0): TBE_EINVAL, no state change,
+ * outputs unspecified. */
+tbe_status tbe_acquire_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
+                             const int64_t *ts_us, uint64_t n, uint8_t *granted,
+                             int32_t *remaining);
+
+/* Same decision on device-resident buffers, enqueued on `stream` (a hipStream_t, or
+ * NULL for the engine's own stream).  Returns once enqueued; a batch found invalid
+ * on the device is skipped (no state change) and reported by tbe_synchronize. */
+tbe_status tbe_acquire_batch_device(tbe_engine *engine, const uint64_t *d_keys,
+                                    const int32_t *d_permits, const int64_t *d_ts_us,
+                                    uint64_t n, uint8_t *d_granted, int32_t *d_remaining,
+                                    void *stream);
+
+/* Waits for every enqueued batch; TBE_EINVAL if any of them was invalid since the
+ * last call (the sticky flag is then cleared). */
+tbe_status tbe_synchronize(tbe_engine *engine);
+
+/* Bucket state exactly as the Redis hash would hold it (HGETALL of the key, TB:210):
+ * *present = 0 if absent or expired at ts_us (pass ts_us < 0 to skip the expiry test);
+ * otherwise *v = field v and *t = field t (= new_t of the last grant, TB:203/230). */
+tbe_status tbe_query(tbe_engine *engine, uint64_t key, int64_t ts_us, double *v, double *t,
+                     int32_t *present);
+
+/* Bulk state export for parity checks: v[k] and the last grant's injected timestamp
+ * t_us[k] (INT64_MIN when never granted) for keys [first, first + count). */
+tbe_status tbe_export_state(tbe_engine *engine, uint64_t first, uint64_t count, double *v,
+                            int64_t *t_us);
+
+/* Per-stage device time (ms) accumulated since the last call, when
+ * TBE_FLAG_STAGE_TIMING is set: out[0..n_out) = {hist, colscan, scatter, bounds,
+ * fold, unscatter}.  Returns the number of stages written via *n_written. */
+tbe_status tbe_stage_times(tbe_engine *engine, double *out, uint32_t n_out, uint32_t *n_written);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBE_H_ */

@@ -1,0 +1,31 @@
+/*
+ * tbe_tools.h -- test / benchmark utilities exported by libtbe.so.
+ *
+ * Not a reference interface (the reference has no trace generator):
+ * these helpers build synthetic request batches directly in device memory so that
+ * benchmarks keep PCIe out of the timed region.  Streams are bit-identical to
+ * oracle/trace.py and oracle/tb_ref.c.
+ */
+#ifndef TBE_TOOLS_H_
+#define TBE_TOOLS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Batch of n requests with global request counter g = g0 + i:
+ *   keys[i]    = ((mix64(seed + g*GAMMA) >> 32) * n_keys) >> 32
+ *   permits[i] = p_lo if p_lo == p_hi, else uniform on {p_lo..p_hi} from stream 0xA5..A5
+ *   ts[i]      = ts0_us + (i * interval_us) / n                       (non-decreasing)
+ * Enqueued on `stream` (hipStream_t or NULL).  Returns 0 on success. */
+int tbe_gen_batch_device(uint64_t seed, uint64_t n_keys, uint64_t g0, uint64_t n, int32_t p_lo,
+                         int32_t p_hi, int64_t ts0_us, int64_t interval_us, uint64_t *d_keys,
+                         int32_t *d_permits, int64_t *d_ts, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBE_TOOLS_H_ */

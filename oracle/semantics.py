@@ -1,0 +1,187 @@
+"""CPU restatement of the reference's rate-limiting decision semantics.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker (or, for bench, as the timed CPU baseline) -- never as the product path.
+The product path is the HIP engine behind ``include/tbe.h``; it fails loudly when
+its shared library is missing and never falls back to this code.
+
+Parity status: the reference (C# + Lua run inside Redis) has no tests, fixtures or
+golden vectors, and neither .NET, Redis nor a Lua VM exists in this
+image.  This restatement is pinned by
+  (1) the hand-derived known-answer tests of SURVEY.md Appendix A.6,
+  (2) bit-for-bit agreement with the independent C restatement ``oracle/tb_ref.c``,
+  (3) golden vectors produced by executing the reference's own Lua script text
+      (read from /root/reference at fixture-generation time) in the in-repo Lua
+      subset interpreter ``oracle/lua_replay.py`` (tests/golden/make_golden.py).
+Redis/SE.Redis/.NET conversion behaviour is restated from their published
+semantics; it is not pinned by any artefact the
+reference ships.
+
+Every arithmetic step is IEEE-754 binary64 round-to-nearest with no FMA -- Python
+floats give exactly that.  Argument order of ``math.min``/``math.max`` follows Lua
+5.1's ``lmathlib.c`` (first argument kept unless a later one is strictly
+better), which fixes signed-zero/NaN behaviour.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+US_PER_S = 1_000_000
+TICKS_PER_SECOND = 10_000_000          # System.TimeSpan.TicksPerSecond
+TTL_MAX_S = 31_536_000                  # TB:234 upper clamp (1 year)
+APPROX_TTL_S = 86_400                   # A:268
+
+
+# ---------------------------------------------------------------- Lua / Redis / .NET helpers
+def lua_max(a: float, b: float) -> float:
+    """Lua 5.1 ``math.max(a, b)``: keeps ``a`` unless ``b > a``."""
+    return b if b > a else a
+
+
+def lua_min(a: float, b: float) -> float:
+    """Lua 5.1 ``math.min(a, b)``: keeps ``a`` unless ``b < a``."""
+    return b if b < a else a
+
+
+def new_t_of(ts_us: int) -> float:
+    """``now[1] + (now[2] / 1000000)`` over Redis ``TIME`` (TB:202-203, A:241-242).
+
+    ``TIME`` returns two integer strings (seconds, microseconds); Lua coerces
+    them to numbers, divides the microseconds by 1e6 (one correctly rounded
+    division) and adds (one rounding).  The build injects ``ts_us`` (>= 0)."""
+    sec, usec = divmod(ts_us, US_PER_S)
+    return float(sec) + (float(usec) / 1000000.0)
+
+
+def fill_rate_per_second(tokens_per_period: int, period_ticks: int) -> float:
+    """``FillRatePerSecond = _tokensPerPeriod / _replenishmentPeriod.TotalSeconds``
+    (TBO:82-85, AO:97-100); .NET 7 ``TimeSpan.TotalSeconds`` = ticks / 1e7."""
+    total_seconds = float(period_ticks) / float(TICKS_PER_SECOND)
+    if total_seconds == 0.0:
+        return math.inf
+    return float(tokens_per_period) / total_seconds
+
+
+def tb_ttl_seconds(capacity: int, fill_rate: float) -> int:
+    """``math.ceil(math.min(math.max(capacity / fill_rate, 1), 31536000))`` (TB:234)."""
+    return int(math.ceil(lua_min(lua_max(float(capacity) / fill_rate, 1.0), float(TTL_MAX_S))))
+
+
+def redis_int_reply(x: float) -> int:
+    """Lua number -> RESP integer: C cast to ``long long`` (truncation toward 0)."""
+    return int(x)
+
+
+def lua_tostring(x: float) -> str:
+    """Lua 5.1 ``tostring(number)`` = ``LUA_NUMBER_FMT`` "%.14g" (A:270)."""
+    return "%.14g" % x
+
+
+def dotnet_round_half_even(x: float) -> float:
+    """``Math.Round(double)`` (banker's rounding, A:443)."""
+    if math.isinf(x) or math.isnan(x):
+        return x
+    return float(round(x))  # Python's round() on floats is round-half-even
+
+
+class ArgumentOutOfRange(ValueError):
+    """Mirrors ArgumentOutOfRangeException (permitCount < 0, or > TokenLimit in A/Q)."""
+
+
+# ---------------------------------------------------------------- token-bucket acquire script
+@dataclass
+class TokenBucketConfig:
+    """Inputs of ``GetAcquireLuaScript(capacity, fillRate)`` (TB:176-185)."""
+
+    token_limit: int                 # TBO:43 -> Lua ``capacity`` (TB:184)
+    fill_rate: float                 # TBO:80 -> Lua ``fill_rate`` (TB:185), raw f64 bits
+
+    @staticmethod
+    def from_options(token_limit: int, tokens_per_period: int, period_ticks: int) -> "TokenBucketConfig":
+        # Constructor validation, TB:29-37.
+        if token_limit <= 0 or tokens_per_period <= 0:
+            raise ValueError("Both TokenLimit and TokensPerPeriod must be set to values greater than 0.")
+        if period_ticks < 0:
+            raise ValueError("ReplenishmentPeriod must be set to a value greater than or equal to TimeSpan.Zero.")
+        rate = fill_rate_per_second(tokens_per_period, period_ticks)
+        if not math.isfinite(rate):
+            # ReplenishmentPeriod == 0 passes TB:34 but interpolates "∞" into the
+            # script, which Redis rejects at compile time.
+            raise ValueError("ReplenishmentPeriod must be > 0 (fill rate would be infinite)")
+        return TokenBucketConfig(token_limit, rate)
+
+
+@dataclass
+class BucketState:
+    v: float        # Redis hash field ``v`` (tokens), stored with round-trip precision
+    t_us: int       # injected TIME of the last grant; field ``t`` = new_t_of(t_us)
+
+
+class TokenBucketTable:
+    """The Redis key space seen by the acquire script (TB:181-238), one hash per key.
+
+    A key is *present* from its first grant until its TTL (TB:232-235) lapses with no
+    further grant.  Redis' passive expiry compares the command-time snapshot in ms
+    (frozen for the duration of a script) with ``grant_ms + ttl_s * 1000``; the build
+    models both snapshots as ``ts_us // 1000``."""
+
+    def __init__(self, cfg: TokenBucketConfig):
+        self.cfg = cfg
+        self.cap = float(cfg.token_limit)
+        self.rate = cfg.fill_rate
+        self.ttl_ms = tb_ttl_seconds(cfg.token_limit, cfg.fill_rate) * 1000
+        self.state: Dict[int, BucketState] = {}
+
+    # HGETALL with passive expiry (TB:210-215)
+    def load(self, key: int, ts_us: int) -> Optional[BucketState]:
+        st = self.state.get(key)
+        if st is None:
+            return None
+        if ts_us // 1000 > st.t_us // 1000 + self.ttl_ms:
+            del self.state[key]
+            return None
+        return st
+
+    def refill(self, key: int, ts_us: int) -> Tuple[float, float, Optional[BucketState]]:
+        """TB:202-221: returns (new_t, x, prev) where x is the refilled, clamped count."""
+        new_t = new_t_of(ts_us)                                   # TB:202-203
+        prev = self.load(key, ts_us)                              # TB:210
+        if prev is None:                                          # TB:213-215
+            pv, pt = self.cap, new_t
+        else:                                                     # TB:211-212
+            pv, pt = prev.v, new_t_of(prev.t_us)
+        delta_t = lua_max(0.0, new_t - pt)                        # TB:218
+        x = lua_max(0.0, lua_min(self.cap, pv + (delta_t * self.rate)))   # TB:221
+        return new_t, x, prev
+
+    def acquire(self, key: int, permits: int, ts_us: int) -> Tuple[bool, int]:
+        """One ``ScriptEvaluateAsync(_acquireScript, {BucketId, PermitCount})`` (TB:63)
+        plus the C# reply parse (TB:64-81).  Returns (granted, remaining)."""
+        if permits < 0:
+            raise ArgumentOutOfRange("permitCount")
+        _, x, _ = self.refill(key, ts_us)
+        success = x >= float(permits)                             # TB:224
+        if success:
+            x = x - float(permits)                                # TB:227
+            self.state[key] = BucketState(x, ts_us)               # TB:230 HSET v,t (+ EXPIRE TB:234-235)
+        # TB:238 ``return {success, new_v}``: true -> 1, false -> nil (-> 0 in SE.Redis),
+        # new_v -> RESP integer (truncation).  TB:71-81 reads them back.
+        return success, redis_int_reply(x)
+
+    def acquire_batch(self, keys, permits, ts_us) -> Tuple[List[int], List[int]]:
+        granted, remaining = [], []
+        for k, p, t in zip(keys, permits, ts_us):
+            g, r = self.acquire(int(k), int(p), int(t))
+            granted.append(1 if g else 0)
+            remaining.append(r)
+        return granted, remaining
+
+    def query(self, key: int, ts_us: Optional[int] = None) -> Optional[Tuple[float, float]]:
+        """(v, t) exactly as stored in the Redis hash, or None when absent/expired."""
+        st = self.state.get(key) if ts_us is None else self.load(key, ts_us)
+        if st is None:
+            return None
+        return st.v, new_t_of(st.t_us)

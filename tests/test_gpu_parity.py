@@ -1,0 +1,180 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU restatement, bit for bit.
+
+Every test drives the same request trace through libtbe.so on cuda:0 and through the C
+oracle (oracle/tb_ref.c), then compares granted/remaining per request and the full
+bucket table (v bits and last-grant timestamps)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import cref, trace
+from oracle.semantics import new_t_of
+
+pytestmark = pytest.mark.gpu
+
+S_US = 1_760_572_800 * 1_000_000
+ABSENT = np.iinfo(np.int64).min
+
+
+def make_pair(n_keys, token_limit, tokens_per_period, period_ticks):
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
+    eng = TokenBucketEngine(n_keys, token_limit, tokens_per_period, period_ticks, device=0)
+    ref = cref.CTokenBucket(n_keys, token_limit, fill_rate(tokens_per_period, period_ticks))
+    return eng, ref
+
+
+def assert_same_state(eng, ref):
+    v, t = eng.export_state()
+    v_ref, t_ref = ref.export_state()
+    assert np.array_equal(t, t_ref), f"t mismatch at {np.flatnonzero(t != t_ref)[:10]}"
+    touched = t_ref != ABSENT
+    bad = np.flatnonzero(v[touched].view(np.uint64) != v_ref[touched].view(np.uint64))
+    assert bad.size == 0, f"v mismatch at {np.flatnonzero(touched)[bad[:10]]}"
+
+
+def run_and_compare(eng, ref, keys, permits, ts):
+    g, r = eng.acquire_batch(keys, permits, ts)
+    g_ref, r_ref = ref.acquire_batch(keys, permits, ts)
+    bad = np.flatnonzero((g != g_ref) | (r != r_ref))
+    assert bad.size == 0, (f"{bad.size} mismatches, first at {bad[:5]}: gpu {g[bad[:5]]},{r[bad[:5]]} "
+                           f"ref {g_ref[bad[:5]]},{r_ref[bad[:5]]}")
+    return g, r
+
+
+def test_kat_sequence(engine_lib, gpu):
+    eng, ref = make_pair(64, 10, 1, 10_000_000)
+    ps = np.array([1, 9, 1, 1, 0, 10, 11], dtype=np.int32)
+    offs = [0, 500_000, 600_000, 1_000_000, 1_100_000, 5_000_000, 9_000_000]
+    ts = np.array([S_US + o for o in offs], dtype=np.int64)
+    keys = np.full(7, 42, dtype=np.uint64)
+    g, r = run_and_compare(eng, ref, keys, ps, ts)
+    assert g.tolist() == [1, 1, 0, 1, 1, 0, 0] and r.tolist() == [9, 0, 0, 0, 0, 4, 8]
+    assert eng.query(42) == (float.fromhex("0x1.99998p-4"), new_t_of(S_US + 1_100_000))
+    # the same KATs one request per batch (state carried across batches)
+    eng2, _ = make_pair(64, 10, 1, 10_000_000)
+    for i in range(7):
+        g1, r1 = eng2.acquire_batch(keys[i:i + 1], ps[i:i + 1], ts[i:i + 1])
+        assert (g1[0], r1[0]) == (g[i], r[i])
+
+
+@pytest.mark.parametrize("n_keys,n,p_hi,interval,batches", [
+    (1, 5000, 2, 2_000_000, 2),             # single key: every request collides
+    (16, 4096, 3, 1_000_000, 3),            # r_bits floor, one bucket
+    (1000, 2047, 1, 300_000, 3),            # just under one tile
+    (1000, 2049, 4, 300_000, 3),            # just over one tile
+    (10_000, 100_000, 3, 2_000_000, 3),     # config A shape
+    (1 << 20, 300_000, 2, 10_000, 3),       # two LSD passes
+    (3_000_017, 500_000, 1, 10_000, 2),     # odd table size, partial last bucket
+])
+def test_random_traces(engine_lib, gpu, n_keys, n, p_hi, interval, batches):
+    eng, ref = make_pair(n_keys, 10, 3, 10_000_000)
+    for b in range(batches):
+        k, p, t = trace.make_batch(0x5EED000B + n_keys, n_keys, b, n, interval, 0, p_hi)
+        run_and_compare(eng, ref, k, p, t)
+    assert_same_state(eng, ref)
+
+
+def test_config_b_shape_small(engine_lib, gpu):
+    # Config B shape (100M keys, cap 10, 1 token/s, 10 ms batches), at 2^21 requests.
+    eng, ref = make_pair(100_000_000, 10, 1, 10_000_000)
+    for b in range(2):
+        k, p, t = trace.make_batch(0x5EED000B, 100_000_000, b, 1 << 21, 10_000)
+        g, _ = run_and_compare(eng, ref, k, p, t)
+        assert g.mean() > 0.99  # fresh keys: almost all grant
+
+
+def test_unsorted_timestamps_and_skew(engine_lib, gpu):
+    rng = np.random.default_rng(5)
+    n_keys, n = 500, 50_000
+    eng, ref = make_pair(n_keys, 7, 2, 30_000_000)
+    for b in range(3):
+        k = rng.integers(0, n_keys, n, dtype=np.uint64)
+        p = rng.integers(0, 9, n).astype(np.int32)             # includes p = 0 and p > cap
+        t = (S_US + rng.integers(0, 20_000_000, n)).astype(np.int64)  # out of order
+        run_and_compare(eng, ref, k, p, t)
+    assert_same_state(eng, ref)
+
+
+def test_fractional_rates(engine_lib, gpu):
+    # rate 1/3 exercises the mul-then-add rounding that an FMA would break.
+    rng = np.random.default_rng(9)
+    eng, ref = make_pair(2000, 1, 1, 30_000_000)
+    t = S_US
+    for b in range(4):
+        n = 40_000
+        k = rng.integers(0, 2000, n, dtype=np.uint64)
+        p = rng.integers(0, 2, n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 3_000_000, n))).astype(np.int64)
+        t += 3_000_000
+        run_and_compare(eng, ref, k, p, ts)
+    assert_same_state(eng, ref)
+
+
+def test_ttl_year_clamp_expiry(engine_lib, gpu):
+    # 1 token per 10^7 s -> cap/rate = 1e8 s > 1 year: TTL clamps to 31536000 s.
+    eng, ref = make_pair(4, 10, 1, 10**14)
+    year = 31_536_000 * 1_000_000
+    keys = np.zeros(3, dtype=np.uint64)
+    g, r = run_and_compare(eng, ref, keys, np.array([10, 5, 5], np.int32),
+                           np.array([S_US, S_US + year, S_US + year + 1000], np.int64))
+    assert g.tolist() == [1, 0, 1] and r.tolist() == [0, 3, 5]
+
+
+def test_empty_batch(engine_lib, gpu):
+    eng, _ = make_pair(10, 5, 1, 10_000_000)
+    g, r = eng.acquire_batch(np.zeros(0, np.uint64), np.zeros(0, np.int32), np.zeros(0, np.int64))
+    assert g.size == 0 and r.size == 0
+
+
+@pytest.mark.parametrize("bad", ["key", "permits", "ts"])
+def test_invalid_batch_rejected_without_state_change(engine_lib, gpu, bad):
+    from distributedratelimiting.redis_amd import TbeError
+    eng, ref = make_pair(100, 5, 1, 10_000_000)
+    k, p, t = trace.make_batch(3, 100, 0, 5000, 1_000_000)
+    run_and_compare(eng, ref, k, p, t)
+    k2, p2, t2 = trace.make_batch(3, 100, 1, 5000, 1_000_000)
+    if bad == "key":
+        k2[4321] = 100
+    elif bad == "permits":
+        p2[17] = -1
+    else:
+        t2[4999] = -5
+    with pytest.raises(TbeError) as ei:
+        eng.acquire_batch(k2, p2, t2)
+    assert ei.value.status == 1
+    assert_same_state(eng, ref)          # nothing applied
+    k3, p3, t3 = trace.make_batch(3, 100, 2, 5000, 1_000_000)
+    run_and_compare(eng, ref, k3, p3, t3)  # engine still usable
+
+
+def test_device_api_and_generator(engine_lib, gpu):
+    import torch
+    from distributedratelimiting.redis_amd import TokenBucketEngine, _capi, fill_rate
+    lib = _capi.load()
+    lib.tbe_gen_batch_device.restype = ctypes.c_int
+    lib.tbe_gen_batch_device.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_int32] * 2 + \
+        [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 4
+    n_keys, n = 1_000_000, 1 << 18
+    eng = TokenBucketEngine(n_keys, 10, 1, 10_000_000, device=0)
+    ref = cref.CTokenBucket(n_keys, 10, fill_rate(1, 10_000_000))
+    dk = torch.empty(n, dtype=torch.int64, device=gpu)
+    dp = torch.empty(n, dtype=torch.int32, device=gpu)
+    dt = torch.empty(n, dtype=torch.int64, device=gpu)
+    dg = torch.empty(n, dtype=torch.uint8, device=gpu)
+    dr = torch.empty(n, dtype=torch.int32, device=gpu)
+    for b in range(3):
+        rc = lib.tbe_gen_batch_device(0x5EED000B, n_keys, b * n, n, 1, 4,
+                                      trace.T0_US + b * 10_000, 10_000, dk.data_ptr(),
+                                      dp.data_ptr(), dt.data_ptr(), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        k, p, t = trace.make_batch(0x5EED000B, n_keys, b, n, 10_000, 1, 4)
+        assert np.array_equal(dk.cpu().numpy().view(np.uint64), k)
+        assert np.array_equal(dp.cpu().numpy(), p) and np.array_equal(dt.cpu().numpy(), t)
+        eng.acquire_batch_device(dk, dp, dt, dg, dr)
+        eng.synchronize()
+        g_ref, r_ref = ref.acquire_batch(k, p, t)
+        assert np.array_equal(dg.cpu().numpy(), g_ref)
+        assert np.array_equal(dr.cpu().numpy(), r_ref)
+    assert_same_state(eng, ref)
