@@ -52,11 +52,13 @@ class TbeError(RuntimeError):
 _lib = None
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libtbe.so (once).  Raises FileNotFoundError if it was never built."""
+def load(path: str = None) -> ctypes.CDLL:
+    """Load libtbe.so (once).  Raises FileNotFoundError if it was never built.
+    ``TBE_LIB`` overrides the path (ablation builds in tools/ only)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("TBE_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise FileNotFoundError(
             f"{path} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')")

@@ -36,15 +36,18 @@ def up_to_date(target: str, deps) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build_engine(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date(LIB, DEPS):
-        return LIB
-    cmd = [hipcc()] + HIPCC_FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SOURCES
+def build_engine(force: bool = False, verbose: bool = False, defines=(), out: str = LIB) -> str:
+    """Build libtbe.so (or, for ablation experiments, a variant with extra -D defines
+    written to `out`)."""
+    if not force and not defines and up_to_date(out, DEPS):
+        return out
+    cmd = [hipcc()] + HIPCC_FLAGS + [f"-D{d}" for d in defines] + \
+        ["-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

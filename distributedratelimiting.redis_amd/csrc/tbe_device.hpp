@@ -51,25 +51,32 @@ struct TbParams {
 
 // One evaluation of the acquire script against the state held in `s` (TB:202-238).
 // Returns the packed reply: bit 31 = success (TB:224/238), bits 0-30 = trunc(new_v)
-// (TB:238 -> RESP integer -> TB:73).  Writes s on success only (TB:225-236).
+// (TB:238 -> RESP integer -> TB:73).  `modified` is set when `s` changed: on a grant
+// (HSET, TB:225-236) and when Redis' passive expiry deleted the key on access (the
+// HGETALL at TB:210 finds it lapsed), which happens even if the request is then denied.
 __device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t ts_us,
-                                               const TbParams &P, bool &granted) {
+                                               const TbParams &P, bool &modified) {
     const double new_t = new_t_of(ts_us);
-    // HGETALL (TB:210) with Redis passive expiry: the key lapses when the command-time
-    // snapshot (ms) exceeds grant_ms + ttl (EXPIRE at TB:235).
-    const bool present = (s.t_us != kAbsent) && !((ts_us / 1000) > (s.t_us / 1000) + P.ttl_ms);
+    const bool had = s.t_us != kAbsent;
+    // EXPIRE at TB:235 lapses when the command-time snapshot (ms) exceeds grant_ms + ttl.
+    const bool expired = had && ((ts_us / 1000) > (s.t_us / 1000) + P.ttl_ms);
+    const bool present = had && !expired;
     const double pv = present ? s.v : P.cap;              // TB:211-215
     const double pt = present ? new_t_of(s.t_us) : new_t;
     const double delta_t = lua_max(0.0, new_t - pt);      // TB:218
     const double fill = delta_t * P.rate;                 // TB:221: mul ...
     double x = lua_max(0.0, lua_min(P.cap, pv + fill));   // ... then add (never fused)
     const double p = (double)permits;
-    granted = x >= p;                                     // TB:224
+    const bool granted = x >= p;                          // TB:224
     if (granted) {
         x = x - p;                                        // TB:227
         s.v = x;                                          // TB:230 HSET v, t
         s.t_us = ts_us;
+    } else if (expired) {
+        s.v = P.cap;                                      // key deleted by passive expiry
+        s.t_us = kAbsent;
     }
+    modified = granted || expired;
     return (granted ? 0x80000000u : 0u) | (uint32_t)(int32_t)x;   // {success, new_v}
 }
 
@@ -79,9 +86,11 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 }
 
-// Exclusive scan of one value per thread over a 256-thread block; *total gets the sum.
-// `wsum` is 4 words of LDS.  Contains two barriers.
+// Exclusive scan of one value per thread over a BLOCK-thread block; *total gets the
+// sum.  `wsum` is BLOCK/64 words of LDS.  Every thread must call it (two barriers).
+template <int BLOCK>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wsum, uint32_t *total) {
+    constexpr int W = BLOCK / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t v = x;
 #pragma unroll
@@ -93,7 +102,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wsum, 
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int j = 0; j < kWaves; ++j) {
+    for (int j = 0; j < W; ++j) {
         const uint32_t s = wsum[j];
         pre += (j < w) ? s : 0u;
         tot += s;
@@ -103,27 +112,39 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wsum, 
     return pre + v - x;
 }
 
-// Stable local ranking of a tile of kBlock*ITEMS elements by an 8-bit digit.
-// Element e = it*kBlock + threadIdx.x (striped, so global loads coalesce); tile order
-// is e order.  Produces, for every valid element, its position `lpos` in the tile
-// sorted stably by digit, and lstart[d] = first position of digit d.
-//   1. per (it, wave): ballot-match the 8 digit bits -> in-wave rank + wave count
-//   2. per digit: exclusive scan of the counts over (it, wave) in tile order
-//   3. block scan of the digit totals -> lstart
-// LDS: cnt[ITEMS*kWaves*kDigits] u16, lstart[kDigits] u32, wsum[4] u32.
-template <int ITEMS>
-__device__ __forceinline__ void rank_tile(const uint32_t (&dig)[ITEMS], int nvalid, uint16_t *cnt,
-                                          uint32_t *lstart, uint32_t *wsum,
-                                          uint32_t (&lpos)[ITEMS]) {
+// LDS needed by rank_tile<BLOCK, ITEMS>.
+template <int BLOCK>
+struct RankLds {
+    static constexpr int W = BLOCK / 64;
+    uint16_t wcnt[2][W][kDigits];   // per-wave digit counts, double-buffered by round
+    uint32_t run[kDigits];          // running per-digit count over the rounds so far
+    uint32_t lstart[kDigits];       // first tile position of each digit
+    uint32_t wsum[W];
+};
+
+// Stable local ranking of a tile of BLOCK*ITEMS elements by an 8-bit digit.
+// Element e = it*BLOCK + threadIdx.x (striped, so global loads coalesce); tile order is
+// e order, i.e. round `it` by round.  Per round: every wave ballot-matches the 8 digit
+// bits (in-wave rank + count), one thread per digit scans the wave counts on top of the
+// running count, each element reads its prefix.  Afterwards lstart = exclusive scan of
+// the digit totals and lpos = lstart[d] + rank is the element's position in the tile
+// sorted stably by digit.  Two barriers per round (the count buffer alternates).
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ void rank_tile(const uint32_t (&dig)[ITEMS], int nvalid,
+                                          RankLds<BLOCK> &L, uint32_t (&lpos)[ITEMS]) {
+    constexpr int W = BLOCK / 64;
+    static_assert(BLOCK >= kDigits, "one digit column per thread");
     const int tid = threadIdx.x, w = tid >> 6;
-    uint32_t *cnt32 = reinterpret_cast<uint32_t *>(cnt);
-    for (int i = tid; i < ITEMS * kWaves * kDigits / 2; i += kBlock) cnt32[i] = 0;
+    uint32_t *z = reinterpret_cast<uint32_t *>(&L.wcnt[0][0][0]);
+    for (int i = tid; i < 2 * W * kDigits / 2; i += BLOCK) z[i] = 0;
+    if (tid < kDigits) L.run[tid] = 0;
     __syncthreads();
     const uint64_t lt = lanemask_lt();
-    uint32_t wrank[ITEMS];
+    uint32_t rank[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-        const int e = it * kBlock + tid;
+        const int buf = it & 1;
+        const int e = it * BLOCK + tid;
         const bool valid = e < nvalid;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -132,31 +153,32 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&dig)[ITEMS], int nval
             const uint64_t m = __ballot(bit);
             peers &= bit ? m : ~m;
         }
-        wrank[it] = (uint32_t)__popcll(peers & lt);
-        if (valid && wrank[it] == 0)
-            cnt[(it * kWaves + w) * kDigits + dig[it]] = (uint16_t)__popcll(peers);
-    }
-    __syncthreads();
-    {
-        const int d = tid;  // kBlock == kDigits: one digit column per thread
-        uint32_t s = 0;
-#pragma unroll 8
-        for (int j = 0; j < ITEMS * kWaves; ++j) {
-            const uint32_t c = cnt[j * kDigits + d];
-            cnt[j * kDigits + d] = (uint16_t)s;
-            s += c;
+        const uint32_t r = (uint32_t)__popcll(peers & lt);
+        if (valid && r == 0) L.wcnt[buf][w][dig[it]] = (uint16_t)__popcll(peers);
+        __syncthreads();
+        if (tid < kDigits) {
+            uint32_t s = L.run[tid];
+#pragma unroll
+            for (int ww = 0; ww < W; ++ww) {
+                const uint32_t c = L.wcnt[buf][ww][tid];
+                L.wcnt[buf][ww][tid] = (uint16_t)s;   // exclusive prefix within the tile
+                L.wcnt[buf ^ 1][ww][tid] = 0;         // clear the other buffer for round it+1
+                s += c;
+            }
+            L.run[tid] = s;
         }
+        __syncthreads();
+        rank[it] = valid ? (uint32_t)L.wcnt[buf][w][dig[it]] + r : 0u;
+    }
+    {
         uint32_t total;
-        lstart[d] = block_excl_scan(s, wsum, &total);
+        const uint32_t x = (tid < kDigits) ? L.run[tid] : 0u;
+        const uint32_t ex = block_excl_scan<BLOCK>(x, L.wsum, &total);
+        if (tid < kDigits) L.lstart[tid] = ex;
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-        const int e = it * kBlock + tid;
-        lpos[it] = (e < nvalid)
-                       ? lstart[dig[it]] + cnt[(it * kWaves + w) * kDigits + dig[it]] + wrank[it]
-                       : 0u;
-    }
+    for (int it = 0; it < ITEMS; ++it) lpos[it] = L.lstart[dig[it]] + rank[it];
 }
 
 }  // namespace tbe

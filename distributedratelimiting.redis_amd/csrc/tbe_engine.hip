@@ -42,11 +42,13 @@ using namespace tbe;
 
 namespace {
 
-constexpr int kScatterItems = 8;                       // elements per thread per tile
-constexpr int kTile = kBlock * kScatterItems;          // 2048 requests per tile
+constexpr int kPartBlock = 512;                        // partition workgroup (8 waves)
+constexpr int kPartItems = 16;                         // elements per thread per tile
+constexpr int kTile = kPartBlock * kPartItems;         // 8192 requests per tile
+constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
 constexpr int kMaxHistBlocks = 1024;
-constexpr int kFoldItems = 4;                          // requests per thread per chunk
-constexpr int kChunk = kBlock * kFoldItems;            // 1024
+constexpr int kFoldItems = 8;                          // requests per thread per chunk
+constexpr int kChunk = kBlock * kFoldItems;            // 2048
 constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
 constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
@@ -54,7 +56,8 @@ constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 // Per-tile digit histograms.  Block j walks tiles [j*tpb, (j+1)*tpb) in order and
 // writes for each tile the exclusive running count per digit within its block
 // (tileprefix) and, at the end, the block's totals (blocksum).  Pass 0 also validates
-// keys (key < n_keys).
+// keys (key < n_keys).  Digits come from the 32-bit key exactly as k_scatter computes
+// them, so counts stay consistent even for an (invalid) key >= 2^32.
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
                                                  int shift, uint32_t tiles_per_blk,
@@ -71,15 +74,18 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
         h[tid] = 0;
         __syncthreads();
         const uint64_t base = (uint64_t)t * kTile;
+        KeyT kv[kHistItems];
 #pragma unroll
-        for (int it = 0; it < kScatterItems; ++it) {
+        for (int it = 0; it < kHistItems; ++it) {
+            const uint64_t i = base + it * kBlock + tid;
+            kv[it] = (i < n) ? keys[i] : (KeyT)0;
+        }
+#pragma unroll
+        for (int it = 0; it < kHistItems; ++it) {
             const uint64_t i = base + it * kBlock + tid;
             if (i < n) {
-                const uint64_t k = (uint64_t)keys[i];
-                bad |= validate && (k >= n_keys);
-                // Digit of the 32-bit key, exactly as k_scatter computes it, so the
-                // counts stay consistent even for an (invalid) key >= 2^32.
-                atomicAdd(&h[((uint32_t)k >> shift) & (kDigits - 1)], 1u);
+                bad |= validate && ((uint64_t)kv[it] >= n_keys);
+                atomicAdd(&h[((uint32_t)kv[it] >> shift) & (kDigits - 1)], 1u);
             }
         }
         __syncthreads();
@@ -92,131 +98,164 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
     if (__any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
-// Digit-column scan over the per-block sums: blockprefix[j][d] = global position of the
-// first element with digit d that block j owns (digit base + earlier blocks' counts).
+// Digit-column scan, one workgroup per digit d: blockprefix[j][d] = number of digit-d
+// elements in blocks < j; digit_total[d] = all of them.  The digit bases (exclusive scan
+// of digit_total) are formed by each consumer workgroup itself.
 __global__ __launch_bounds__(kBlock) void k_colscan(const uint32_t *__restrict__ blocksum,
                                                     uint32_t nblk,
-                                                    uint32_t *__restrict__ blockprefix) {
+                                                    uint32_t *__restrict__ blockprefix,
+                                                    uint32_t *__restrict__ digit_total) {
     __shared__ uint32_t wsum[kWaves];
-    const int d = threadIdx.x;
-    uint32_t s = 0;
-    uint32_t j = 0;
-    for (; j + 8 <= nblk; j += 8) {
-        uint32_t c[8];
+    const int d = blockIdx.x, tid = threadIdx.x;
+    constexpr int PER = kMaxHistBlocks / kBlock;   // 4 blocks per thread
+    uint32_t c[PER], s = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = blocksum[(uint64_t)(j + u) * kDigits + d];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            blockprefix[(uint64_t)(j + u) * kDigits + d] = s;
-            s += c[u];
-        }
-    }
-    for (; j < nblk; ++j) {
-        const uint32_t c = blocksum[(uint64_t)j * kDigits + d];
-        blockprefix[(uint64_t)j * kDigits + d] = s;
-        s += c;
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t j = tid * PER + u;
+        c[u] = (j < nblk) ? blocksum[(uint64_t)j * kDigits + d] : 0u;
+        s += c[u];
     }
     uint32_t total;
-    const uint32_t base = block_excl_scan(s, wsum, &total);
-    for (j = 0; j < nblk; ++j) blockprefix[(uint64_t)j * kDigits + d] += base;
+    uint32_t pre = block_excl_scan<kBlock>(s, wsum, &total);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t j = tid * PER + u;
+        if (j < nblk) blockprefix[(uint64_t)j * kDigits + d] = pre;
+        pre += c[u];
+    }
+    if (tid == 0) digit_total[d] = total;
+}
+
+// goff[d] = global output position of this tile's first digit-d element.
+template <int BLOCK>
+__device__ __forceinline__ void tile_offsets(uint32_t tile, uint32_t tiles_per_blk,
+                                             const uint32_t *__restrict__ tileprefix,
+                                             const uint32_t *__restrict__ blockprefix,
+                                             const uint32_t *__restrict__ digit_total,
+                                             uint32_t *goff, uint32_t *wsum) {
+    const int tid = threadIdx.x;
+    uint32_t tot = (tid < kDigits) ? digit_total[tid] : 0u;
+    uint32_t all;
+    const uint32_t base = block_excl_scan<BLOCK>(tot, wsum, &all);
+    if (tid < kDigits)
+        goff[tid] = base + blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
+                    tileprefix[(uint64_t)tile * kDigits + tid];
 }
 
 // Stable partition of one tile by digit d = (key >> shift) & 255.  Payload travels as
-// SoA {key u32, permits i32, ts i64}.  Two staging rounds (8 B each) keep LDS at 32 KB.
+// SoA {key u32, permits i32, ts i64}; it is staged through LDS in two 8-byte rounds so
+// each digit's run leaves the workgroup as one contiguous, coalesced write.
 template <typename KeyIn>
-__global__ __launch_bounds__(kBlock) void k_scatter(
+__global__ __launch_bounds__(kPartBlock, 4) void k_scatter(
     const KeyIn *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
-    const uint32_t *__restrict__ blockprefix, uint32_t tiles_per_blk, uint32_t *__restrict__ kout,
-    int32_t *__restrict__ pout, int64_t *__restrict__ tout, uint32_t *__restrict__ err,
-    int validate) {
-    __shared__ uint16_t cnt[kScatterItems * kWaves * kDigits];
-    __shared__ uint32_t lstart[kDigits];
+    const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
+    uint32_t tiles_per_blk, uint32_t *__restrict__ kout, int32_t *__restrict__ pout,
+    int64_t *__restrict__ tout, uint32_t *__restrict__ err, int validate) {
+    __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
-    __shared__ uint32_t wsum[kWaves];
     __shared__ uint64_t stage[kTile];
 
     const int tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * kTile;
     const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    goff[tid] = blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
-                tileprefix[(uint64_t)tile * kDigits + tid];
 
     // Issue every load of the tile up front; the payload waits in registers while the
     // ranks are computed.
-    uint32_t key[kScatterItems], dig[kScatterItems], lpos[kScatterItems], gpos[kScatterItems];
-    int32_t pm[kScatterItems];
-    int64_t tv[kScatterItems];
+    uint32_t key[kPartItems], dig[kPartItems], lpos[kPartItems];
+    int32_t pm[kPartItems];
+    int64_t tv[kPartItems];
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int e = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
         const bool v = e < nvalid;
         key[it] = v ? (uint32_t)kin[base + e] : 0u;
         pm[it] = v ? pin[base + e] : 0;
         tv[it] = v ? tin[base + e] : 0;
         dig[it] = (key[it] >> shift) & (kDigits - 1);
     }
-    rank_tile<kScatterItems>(dig, nvalid, cnt, lstart, wsum, lpos);
+    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
+    rank_tile<kPartBlock, kPartItems>(dig, nvalid, L, lpos);
 
     bool bad = false;
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int e = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
         if (e < nvalid) {
             bad |= validate && (pm[it] < 0 || tv[it] < 0);
             stage[lpos[it]] = ((uint64_t)key[it] << 32) | (uint32_t)pm[it];
         }
     }
     __syncthreads();
+    uint32_t gpos[kPartItems];
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int j = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int j = it * kPartBlock + tid;
         if (j < nvalid) {
             const uint64_t s = stage[j];
             const uint32_t k = (uint32_t)(s >> 32);
             const uint32_t d = (k >> shift) & (kDigits - 1);
-            gpos[it] = goff[d] + (uint32_t)j - lstart[d];
+            gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             kout[gpos[it]] = k;
             pout[gpos[it]] = (int32_t)(uint32_t)s;
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int e = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
         if (e < nvalid) stage[lpos[it]] = (uint64_t)tv[it];
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int j = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int j = it * kPartBlock + tid;
         if (j < nvalid) tout[gpos[it]] = (int64_t)stage[j];
     }
     if (validate && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
 // bstart[b] = first sorted position with bucket >= b, for b in [0, nb]; bstart[nb] = n.
+// Four sorted keys per thread.
 __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t *__restrict__ skeys, uint64_t n,
                                                    int r_bits, uint32_t nb,
                                                    uint32_t *__restrict__ bstart,
                                                    const uint32_t *__restrict__ err) {
     if (*err) return;
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const int64_t b = (int64_t)(skeys[i] >> r_bits);
-    const int64_t prev = (i == 0) ? -1 : (int64_t)(skeys[i - 1] >> r_bits);
-    for (int64_t q = prev + 1; q <= b; ++q) bstart[q] = (uint32_t)i;
-    if (i == n - 1)
-        for (int64_t q = b + 1; q <= (int64_t)nb; ++q) bstart[q] = (uint32_t)n;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (i0 >= n) return;
+    int64_t prev = (i0 == 0) ? -1 : (int64_t)(skeys[i0 - 1] >> r_bits);
+    uint32_t k4[4];
+    if (i0 + 4 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(skeys + i0);
+        k4[0] = v.x; k4[1] = v.y; k4[2] = v.z; k4[3] = v.w;
+    } else {
+        for (int u = 0; u < 4; ++u) k4[u] = (i0 + u < n) ? skeys[i0 + u] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint64_t i = i0 + u;
+        if (i >= n) break;
+        const int64_t b = (int64_t)(k4[u] >> r_bits);
+        for (int64_t q = prev + 1; q <= b; ++q) bstart[q] = (uint32_t)i;
+        prev = b;
+        if (i == n - 1)
+            for (int64_t q = b + 1; q <= (int64_t)nb; ++q) bstart[q] = (uint32_t)n;
+    }
 }
 
 // Decide every request of one bucket (see file header).  res[q] is the packed reply of
 // sorted request q (bit 31 granted, bits 0-30 remaining).
+//
+// A dense bucket (>= R/8 requests) pulls its whole 16*R-byte slice of the table into
+// LDS with coalesced 16-B loads issued together with the first chunk's request loads,
+// and writes the slice back whole (full-line stores); a sparse bucket pulls only the
+// rows its requests touch and writes back only the rows that changed.
 __global__ __launch_bounds__(kBlock) void k_fold(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint32_t *__restrict__ bstart, int r_bits,
-    Slot *__restrict__ table, TbParams P, uint32_t *__restrict__ res,
+    uint64_t n_keys, Slot *__restrict__ table, TbParams P, uint32_t *__restrict__ res,
     const uint32_t *__restrict__ err) {
     __shared__ Slot slot[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];
@@ -230,14 +269,41 @@ __global__ __launch_bounds__(kBlock) void k_fold(
     if (s == e) return;
     const uint32_t R = 1u << r_bits;
     const uint32_t rmask = R - 1;
-    Slot *__restrict__ rows = table + ((uint64_t)b << r_bits);
+    const uint64_t row0 = (uint64_t)b << r_bits;
+    const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
+    Slot *__restrict__ rows = table + row0;
+#ifdef TBE_ABLATE_SKIP_TABLE
+    const bool dense = true;
+#else
+    const bool dense = (e - s) >= (R >> 3);
+#endif
 
+#ifdef TBE_ABLATE_SKIP_TABLE
+    for (uint32_t j = tid; j < R; j += kBlock) slot[j] = Slot{P.cap, kAbsent};
+    if (false) {
+#else
+    if (dense) {
+#endif
+        // Issue all of this thread's row loads before the first LDS store.
+        constexpr int kRowsPerThread = (1 << kMaxRBits) / kBlock;
+        Slot tmp[kRowsPerThread];
+#pragma unroll
+        for (int u = 0; u < kRowsPerThread; ++u) {
+            const uint32_t j = tid + u * kBlock;
+            if (j < nrows) tmp[u] = rows[j];
+        }
+#pragma unroll
+        for (int u = 0; u < kRowsPerThread; ++u) {
+            const uint32_t j = tid + u * kBlock;
+            if (j < nrows) slot[j] = tmp[u];
+        }
+    }
     for (uint32_t j = tid; j < R; j += kBlock) own[j] = kNoOwner;
     for (uint32_t j = tid; j < (R + 31) / 32; j += kBlock) {
-        loaded[j] = 0;
+        loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
-    __syncthreads();
+    if (dense) __syncthreads();
 
     for (uint32_t c = s; c < e; c += kChunk) {
         uint32_t kl[kFoldItems];
@@ -258,16 +324,31 @@ __global__ __launch_bounds__(kBlock) void k_fold(
                 ts[r] = 0;
             }
         }
-        // First touch of a row in this bucket pulls it into LDS.
+        if (!dense) {
+            // First touch of a row in this bucket pulls it into LDS: claim every row
+            // first, then issue all the claimed loads, then store them.
+            uint32_t mine = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldItems; ++r) {
-            if (pend & (1u << r)) {
-                const uint32_t bit = 1u << (kl[r] & 31);
-                const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
-                if (!(old & bit)) slot[kl[r]] = rows[kl[r]];
+            for (int r = 0; r < kFoldItems; ++r) {
+                if (pend & (1u << r)) {
+                    const uint32_t bit = 1u << (kl[r] & 31);
+                    const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
+                    if (!(old & bit)) mine |= 1u << r;
+                }
             }
+            Slot tmp[kFoldItems];
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (mine & (1u << r)) tmp[r] = rows[kl[r]];
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (mine & (1u << r)) slot[kl[r]] = tmp[r];
         }
         __syncthreads();
+#ifdef TBE_ABLATE_SKIP_ROUNDS
+        if (pend) res[c + tid] = (uint32_t)pm[0] + (uint32_t)ts[0] + kl[0];
+        continue;
+#endif
         // Owner rounds: the earliest pending request of each key decides this round.
         for (;;) {
 #pragma unroll
@@ -278,12 +359,12 @@ __global__ __launch_bounds__(kBlock) void k_fold(
 #pragma unroll
             for (int r = 0; r < kFoldItems; ++r) {
                 if ((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kBlock + tid)) {
-                    bool g;
+                    bool modified;
                     Slot st = slot[kl[r]];
-                    res[c + r * kBlock + tid] = tb_acquire(st, pm[r], ts[r], P, g);
-                    if (g) {
+                    res[c + r * kBlock + tid] = tb_acquire(st, pm[r], ts[r], P, modified);
+                    if (modified) {
                         slot[kl[r]] = st;
-                        atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                        if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     }
                     won |= 1u << r;
                 }
@@ -297,48 +378,58 @@ __global__ __launch_bounds__(kBlock) void k_fold(
         }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < R; j += kBlock)
-        if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = slot[j];
+#ifdef TBE_ABLATE_SKIP_TABLE
+    if (slot[tid].v == -1.0) rows[tid] = slot[tid];
+    return;
+#endif
+    if (dense) {
+        for (uint32_t j = tid; j < nrows; j += kBlock) rows[j] = slot[j];
+    } else {
+        for (uint32_t j = tid; j < nrows; j += kBlock)
+            if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = slot[j];
+    }
 }
 
 // Inverse of one k_scatter pass: recompute the tile's local ranks from the pass-input
 // keys, gather the replies from the pass-output positions, store them in pass-input
 // order.  FINAL = pass 0: unpack into granted (u8) / remaining (i32).
 template <typename KeyIn, bool FINAL>
-__global__ __launch_bounds__(kBlock) void k_unscatter(
+__global__ __launch_bounds__(kPartBlock) void k_unscatter(
     const KeyIn *__restrict__ kin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
-    const uint32_t *__restrict__ blockprefix, uint32_t tiles_per_blk,
-    const uint32_t *__restrict__ res_in, uint32_t *__restrict__ res_out,
+    const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
+    uint32_t tiles_per_blk, const uint32_t *__restrict__ res_in, uint32_t *__restrict__ res_out,
     uint8_t *__restrict__ granted, int32_t *__restrict__ remaining) {
-    __shared__ uint16_t cnt[kScatterItems * kWaves * kDigits];
-    __shared__ uint32_t lstart[kDigits];
+    __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
-    __shared__ uint32_t wsum[kWaves];
 
     const int tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * kTile;
     const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    goff[tid] = blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
-                tileprefix[(uint64_t)tile * kDigits + tid];
-    uint32_t dig[kScatterItems], lpos[kScatterItems];
+    uint32_t dig[kPartItems], lpos[kPartItems];
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int e = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
         const uint32_t k = (e < nvalid) ? (uint32_t)kin[base + e] : 0u;
         dig[it] = (k >> shift) & (kDigits - 1);
     }
-    rank_tile<kScatterItems>(dig, nvalid, cnt, lstart, wsum, lpos);
+    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
+    rank_tile<kPartBlock, kPartItems>(dig, nvalid, L, lpos);
+    uint32_t r[kPartItems];
 #pragma unroll
-    for (int it = 0; it < kScatterItems; ++it) {
-        const int e = it * kBlock + tid;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
+        r[it] = (e < nvalid) ? res_in[goff[dig[it]] + lpos[it] - L.lstart[dig[it]]] : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
         if (e < nvalid) {
-            const uint32_t r = res_in[goff[dig[it]] + lpos[it] - lstart[dig[it]]];
             if (FINAL) {
-                granted[base + e] = (uint8_t)(r >> 31);
-                remaining[base + e] = (int32_t)(r & 0x7FFFFFFFu);
+                granted[base + e] = (uint8_t)(r[it] >> 31);
+                remaining[base + e] = (int32_t)(r[it] & 0x7FFFFFFFu);
             } else {
-                res_out[base + e] = r;
+                res_out[base + e] = r[it];
             }
         }
     }
@@ -363,6 +454,7 @@ struct PassBufs {
     int64_t *ts = nullptr;
     uint32_t *tileprefix = nullptr;
     uint32_t *blockprefix = nullptr;
+    uint32_t *digit_total = nullptr;
 };
 
 inline int ceil_log2(uint64_t x) {
@@ -441,6 +533,7 @@ void free_workspace(tbe_engine *e) {
         dfree(pb.ts);
         dfree(pb.tileprefix);
         dfree(pb.blockprefix);
+        dfree(pb.digit_total);
     }
     e->pass.clear();
     dfree(e->blocksum);
@@ -474,6 +567,7 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&pb.digit_total, kDigits * sizeof(uint32_t)));
     }
     HIP_TRY(e, hipMalloc(&e->blocksum, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&e->res[0], cap * sizeof(uint32_t)));
@@ -545,39 +639,42 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                        e->err, 0);
         stage_end(e, ST_HIST, st);
         stage_begin(e, ST_COLSCAN, st);
-        k_colscan<<<1, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix);
+        k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, st);
         stage_begin(e, ST_SCATTER, st);
         if (p == 0)
-            k_scatter<uint64_t><<<ntiles, kBlock, 0, st>>>(
-                keys, permits, ts, n, shift, out.tileprefix, out.blockprefix, tpb, out.keys,
-                out.permits, out.ts, e->err, 1);
+            k_scatter<uint64_t><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, ts, n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb,
+                out.keys, out.permits, out.ts, e->err, 1);
         else
-            k_scatter<uint32_t><<<ntiles, kBlock, 0, st>>>(
+            k_scatter<uint32_t><<<ntiles, kPartBlock, 0, st>>>(
                 e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, n, shift,
-                out.tileprefix, out.blockprefix, tpb, out.keys, out.permits, out.ts, e->err, 0);
+                out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits,
+                out.ts, e->err, 0);
         stage_end(e, ST_SCATTER, st);
     }
     const PassBufs &sorted = e->pass[e->passes - 1];
     stage_begin(e, ST_BOUNDS, st);
-    k_bounds<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+    k_bounds<<<(unsigned)((n + 4 * kBlock - 1) / (4 * kBlock)), kBlock, 0, st>>>(
         sorted.keys, n, e->r_bits, e->nbuckets, e->bstart, e->err);
     stage_end(e, ST_BOUNDS, st);
     stage_begin(e, ST_FOLD, st);
     k_fold<<<e->nbuckets, kBlock, 0, st>>>(sorted.keys, sorted.permits, sorted.ts, e->bstart,
-                                           e->r_bits, e->table, e->params, e->res[0], e->err);
+                                           e->r_bits, e->cfg.n_keys, e->table, e->params,
+                                           e->res[0], e->err);
     stage_end(e, ST_FOLD, st);
     stage_begin(e, ST_UNSCATTER, st);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        k_unscatter<uint32_t, false><<<ntiles, kBlock, 0, st>>>(
-            e->pass[p - 1].keys, n, e->r_bits + kDigitBits * p, e->pass[p].tileprefix,
-            e->pass[p].blockprefix, tpb, e->res[cur], e->res[cur ^ 1], nullptr, nullptr);
+        const PassBufs &pb = e->pass[p];
+        k_unscatter<uint32_t, false><<<ntiles, kPartBlock, 0, st>>>(
+            e->pass[p - 1].keys, n, e->r_bits + kDigitBits * p, pb.tileprefix, pb.blockprefix,
+            pb.digit_total, tpb, e->res[cur], e->res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
-    k_unscatter<uint64_t, true><<<ntiles, kBlock, 0, st>>>(
-        keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix, tpb, e->res[cur],
-        nullptr, granted, remaining);
+    k_unscatter<uint64_t, true><<<ntiles, kPartBlock, 0, st>>>(
+        keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix, e->pass[0].digit_total,
+        tpb, e->res[cur], nullptr, granted, remaining);
     stage_end(e, ST_UNSCATTER, st);
     k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
     HIP_TRY(e, hipGetLastError());

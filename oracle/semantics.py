@@ -185,3 +185,57 @@ class TokenBucketTable:
         if st is None:
             return None
         return st.v, new_t_of(st.t_us)
+
+
+# ---------------------------------------------------------------- approximate: global sync script
+@dataclass
+class ApproxGlobalState:
+    v: float      # decayed consumed count (A:258)
+    p: float      # EWMA of the gap between sync calls (A:262)
+    t_us: int     # injected TIME of the last sync; field t = new_t_of(t_us)
+
+
+class ApproxGlobalTable:
+    """The Redis key space seen by the approximate limiter's sync script (A:221-270)."""
+
+    def __init__(self, decay_rate: float):
+        self.rate = decay_rate
+        self.ttl_ms = APPROX_TTL_S * 1000
+        self.state: Dict[str, ApproxGlobalState] = {}
+
+    def load(self, bucket: str, ts_us: int) -> Optional[ApproxGlobalState]:
+        st = self.state.get(bucket)
+        if st is not None and ts_us // 1000 > st.t_us // 1000 + self.ttl_ms:  # EXPIRE 86400 (A:268)
+            del self.state[bucket]
+            return None
+        return st
+
+    def sync(self, bucket: str, local_count: int, ts_us: int) -> Tuple[int, float, str]:
+        """One ``ScriptEvaluateAsync(_syncScript, {BucketId, LocalCount})`` (A:439) and the
+        reply parse (A:440-442): returns (global score, period, period string)."""
+        new_t = new_t_of(ts_us)                                          # A:241-242
+        prev = self.load(bucket, ts_us)                                  # A:245
+        if prev is None:                                                 # A:250-252
+            pv, pp, pt = 0.0, 0.0, new_t
+        else:                                                            # A:247-249
+            pv, pp, pt = prev.v, prev.p, new_t_of(prev.t_us)
+        count = float(local_count)                                       # A:223 tonumber
+        delta_t = lua_max(0.0, new_t - pt)                               # A:255
+        new_v = lua_max(0.0, pv - (delta_t * self.rate)) + count        # A:258
+        new_p = (pp * 0.8) + (delta_t * 0.2)                             # A:262
+        self.state[bucket] = ApproxGlobalState(new_v, new_p, ts_us)      # A:265 (+ EXPIRE A:268)
+        period_str = lua_tostring(new_p)                                 # A:270 tostring(new_p)
+        return redis_int_reply(new_v), float(period_str), period_str
+
+
+def instance_count_estimate(replenishment_seconds: float, period: float) -> float:
+    """``Math.Max(1, Math.Round(ReplenishmentPeriod.TotalSeconds / period))`` (A:443);
+    period 0 gives +inf (double division), Max(1, inf) = inf."""
+    if period == 0.0:
+        q = math.inf if replenishment_seconds > 0 else math.nan
+    else:
+        q = replenishment_seconds / period
+    r = dotnet_round_half_even(q)
+    if math.isnan(r):
+        return math.nan  # Math.Max(1, NaN) = NaN in .NET
+    return max(1.0, r)

@@ -87,8 +87,14 @@ static inline int tbr_acquire_one(tbr_table *tb, uint64_t key, int32_t p, int64_
     double new_t = tbr_new_t(ts_us);
     int64_t pt_us = tb->t_us[key];
     double pv, pt;
-    if (pt_us == TBR_ABSENT || (ts_us / 1000) > (pt_us / 1000) + tb->ttl_ms) {
-        pv = tb->cap; pt = new_t;                       /* TB:213-215 (absent / expired) */
+    if (pt_us != TBR_ABSENT && (ts_us / 1000) > (pt_us / 1000) + tb->ttl_ms) {
+        /* Passive expiry: HGETALL (TB:210) on a lapsed key deletes it, whatever the
+         * script decides next. */
+        tb->t_us[key] = pt_us = TBR_ABSENT;
+        tb->v[key] = tb->cap;
+    }
+    if (pt_us == TBR_ABSENT) {
+        pv = tb->cap; pt = new_t;                       /* TB:213-215 (absent) */
     } else {
         pv = tb->v[key]; pt = tbr_new_t(pt_us);         /* TB:211-212 */
     }

@@ -178,3 +178,44 @@ def test_device_api_and_generator(engine_lib, gpu):
         assert np.array_equal(dg.cpu().numpy(), g_ref)
         assert np.array_equal(dr.cpu().numpy(), r_ref)
     assert_same_state(eng, ref)
+
+
+GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["tb_testapp_like", "tb_rate_third", "tb_tenth_second", "tb_skewed_clock",
+                                  "tb_mixed_permits", "tb_year_ttl", "tb_fast_refill"])
+@pytest.mark.parametrize("split", [1, 7])
+def test_golden_reference_script(engine_lib, gpu, name, split):
+    """GPU engine vs vectors recorded by executing the reference's Lua script
+    (tests/golden/make_golden.py), one batch or split into `split` batches."""
+    import os
+    from distributedratelimiting.redis_amd import TokenBucketEngine
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    eng = TokenBucketEngine(int(g["n_keys"]), int(g["token_limit"]), int(g["tokens_per_period"]),
+                            int(g["period_ticks"]), device=0)
+    n = g["keys"].size
+    cuts = np.linspace(0, n, split + 1).astype(int)
+    gr, rem = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        x, y = eng.acquire_batch(g["keys"][a:b], g["permits"][a:b], g["ts_us"][a:b])
+        gr.append(x); rem.append(y)
+    assert np.array_equal(np.concatenate(gr), g["granted"])
+    assert np.array_equal(np.concatenate(rem), g["remaining"])
+    for k in range(int(g["n_keys"])):
+        st = eng.query(k)
+        if g["present"][k]:
+            assert st == (g["v"][k], g["t"][k])
+        else:
+            assert st is None
+
+
+def test_expired_key_deleted_even_when_denied(engine_lib, gpu):
+    eng, ref = make_pair(3, 10, 1, 10**14)
+    year = 31_536_000 * 1_000_000
+    keys = np.zeros(3, np.uint64)
+    g, r = run_and_compare(eng, ref, keys, np.array([10, 11, 3], np.int32),
+                           np.array([S_US, S_US + year + 5_000, S_US + year - 5_000], np.int64))
+    assert list(zip(g.tolist(), r.tolist())) == [(1, 0), (0, 10), (1, 7)]
+    assert_same_state(eng, ref)

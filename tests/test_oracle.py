@@ -180,3 +180,19 @@ def test_clock_skew_backwards():
     assert tb.acquire(3, 0, S_US) == (True, 0)
     assert tb.query(3) == (0.0, new_t_of(S_US))
     assert tb.acquire(3, 1, S_US + 1_000_000) == (True, 0)   # refill from the earlier t
+
+
+def test_expired_key_deleted_even_when_denied():
+    # Passive expiry deletes the key at the HGETALL (TB:210) even if the script then
+    # denies (p > cap): a later request with an EARLIER timestamp must see it absent.
+    cfg = TokenBucketConfig(10, 1e-7)
+    year = 31_536_000 * 1_000_000
+    seq = [(0, 10, S_US), (0, 11, S_US + year + 5_000), (0, 3, S_US + year - 5_000)]
+    tb = TokenBucketTable(cfg)
+    out = [tb.acquire(k, p, t) for k, p, t in seq]
+    assert out == [(True, 0), (False, 10), (True, 7)]
+    assert tb.query(0) == (7.0, new_t_of(S_US + year - 5_000))
+    c = cref.CTokenBucket(1, 10, 1e-7)
+    g, r = c.acquire_batch(np.zeros(3, np.uint64), np.array([s[1] for s in seq]),
+                           np.array([s[2] for s in seq]))
+    assert list(zip(g.tolist(), r.tolist())) == [(1, 0), (0, 10), (1, 7)]

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Time ablation builds of the engine in ONE process family on one GPU (bench-shaped
+workload): each variant runs as a child process with TBE_LIB pointing at its build and
+prints per-stage ms.  Variants are built beforehand in this container:
+    python tools/ablate.py --build
+then on the GPU box:
+    python tools/ablate.py --run
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
+VARIANTS = {
+    "base": [],
+    "skip_rounds": ["TBE_ABLATE_SKIP_ROUNDS"],
+    "skip_table": ["TBE_ABLATE_SKIP_TABLE"],
+    "skip_both": ["TBE_ABLATE_SKIP_ROUNDS", "TBE_ABLATE_SKIP_TABLE"],
+}
+
+
+def build():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_b", os.path.join(ROOT, "distributedratelimiting.redis_amd", "build.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    os.makedirs(OUTDIR, exist_ok=True)
+    for name, defs in VARIANTS.items():
+        m.build_engine(force=True, defines=defs, out=os.path.join(OUTDIR, f"libtbe_{name}.so"))
+        print("built", name)
+
+
+def run(rounds: int, steps: int):
+    results = {}
+    for r in range(rounds):
+        for name in VARIANTS:
+            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{name}.so"))
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps),
+                                  "--warmup", "2", "--cpu-seconds", "0"], env=env, capture_output=True,
+                                 text=True, timeout=300)
+            line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+            if not line:
+                print(name, "FAILED", out.stderr[-2000:])
+                continue
+            d = json.loads(line[0])
+            results.setdefault(name, []).append(d["stage_ms_per_step"])
+            print(r, name, d["ms_per_step"], d["stage_ms_per_step"], flush=True)
+    print(json.dumps(results))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--run", action="store_true")
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=5)
+    a = ap.parse_args()
+    if a.build:
+        build()
+    if a.run:
+        run(a.rounds, a.steps)
