@@ -35,12 +35,46 @@ struct __attribute__((aligned(16))) Slot {
 __device__ __forceinline__ double lua_max(double a, double b) { return (b > a) ? b : a; }
 __device__ __forceinline__ double lua_min(double a, double b) { return (b < a) ? b : a; }
 
-// TB:202-203: new_t = now[1] + (now[2] / 1000000) over Redis TIME = (sec, usec).
-// One correctly rounded f64 division (hipcc's default IEEE div sequence), one add.
+// Split an injected timestamp (us, >= 0, < 2^53) into Redis TIME's (sec, usec):
+// an f64 estimate of ts/1e6 is off by at most one, fixed by one integer correction
+// (tests/test_fastdiv.py checks the identity with the same operations).
+__device__ __forceinline__ void split_ts(int64_t ts_us, int64_t &sec, int64_t &usec) {
+    int64_t s = (int64_t)((double)ts_us * 1e-6);
+    int64_t r = ts_us - s * 1000000;
+    if (r < 0) {
+        s -= 1;
+        r += 1000000;
+    } else if (r >= 1000000) {
+        s += 1;
+        r -= 1000000;
+    }
+    sec = s;
+    usec = r;
+}
+
+// TB:202-203: new_t = now[1] + (now[2] / 1000000).  The quotient usec / 1e6 is the
+// IEEE-correctly-rounded one: q0 = u * fl(1e-6), r = fma(-q0, 1e6, u), q = fma(r,
+// fl(1e-6), q0) equals u / 1e6 for EVERY u in [0, 1e6) (checked exhaustively,
+// tests/test_fastdiv.py).  Then one rounded add, as in Lua.
 __device__ __forceinline__ double new_t_of(int64_t ts_us) {
-    const int64_t sec = ts_us / 1000000;
-    const int64_t usec = ts_us - sec * 1000000;
-    return (double)sec + ((double)usec / 1000000.0);
+    int64_t sec, usec;
+    split_ts(ts_us, sec, usec);
+    const double x = (double)usec;
+    const double rcp = 1.0 / 1000000.0;
+    const double q0 = x * rcp;
+    const double r = __builtin_fma(-q0, 1000000.0, x);
+    const double q = __builtin_fma(r, rcp, q0);
+    return (double)sec + q;
+}
+
+// Stored grant time packed for the expiry test: (ts / 1000) << 10 | (ts % 1000).
+// kAbsent (INT64_MIN) marks a key with no Redis hash.
+__device__ __forceinline__ int64_t tpack_of(int64_t ts_us) {
+    const int64_t ms = ts_us / 1000;
+    return (ms << 10) | (ts_us - ms * 1000);
+}
+__device__ __forceinline__ int64_t ts_of_tpack(int64_t tp) {
+    return (tp == kAbsent) ? kAbsent : (tp >> 10) * 1000 + (tp & 1023);
 }
 
 struct TbParams {
@@ -49,35 +83,65 @@ struct TbParams {
     int64_t ttl_ms;   // EXPIRE seconds (TB:234) * 1000
 };
 
-// One evaluation of the acquire script against the state held in `s` (TB:202-238).
-// Returns the packed reply: bit 31 = success (TB:224/238), bits 0-30 = trunc(new_v)
-// (TB:238 -> RESP integer -> TB:73).  `modified` is set when `s` changed: on a grant
-// (HSET, TB:225-236) and when Redis' passive expiry deleted the key on access (the
-// HGETALL at TB:210 finds it lapsed), which happens even if the request is then denied.
-__device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t ts_us,
-                                               const TbParams &P, bool &modified) {
-    const double new_t = new_t_of(ts_us);
-    const bool had = s.t_us != kAbsent;
+// Everything of one request that does not depend on bucket state, computed in
+// parallel before the per-key serial order is resolved.
+struct ReqTime {
+    double new_t;    // TB:203
+    int64_t ms;      // command-time snapshot for passive expiry
+    int64_t tp;      // tpack_of(ts): what a grant stores
+};
+__device__ __forceinline__ ReqTime req_time(int64_t ts_us) {
+    ReqTime r;
+    r.new_t = new_t_of(ts_us);
+    r.ms = ts_us / 1000;
+    r.tp = (r.ms << 10) | (ts_us - r.ms * 1000);
+    return r;
+}
+
+// One evaluation of the acquire script (TB:202-238) on a key's state
+// {v, t = field t as f64, tp = packed grant time}.  Returns the packed reply: bit 31 =
+// success (TB:224/238), bits 0-30 = trunc(new_v) (TB:238 -> RESP integer -> TB:73).
+// `modified` is set when the state changed: on a grant (HSET, TB:225-236) and when
+// Redis' passive expiry deleted the key on access (the HGETALL at TB:210 finds it
+// lapsed), which happens even if the request is then denied.
+__device__ __forceinline__ uint32_t tb_step(double &v, double &t, int64_t &tp, int32_t permits,
+                                            const ReqTime &rq, const TbParams &P, bool &modified) {
+    const bool had = tp != kAbsent;
     // EXPIRE at TB:235 lapses when the command-time snapshot (ms) exceeds grant_ms + ttl.
-    const bool expired = had && ((ts_us / 1000) > (s.t_us / 1000) + P.ttl_ms);
+    const bool expired = had && (rq.ms > (tp >> 10) + P.ttl_ms);
     const bool present = had && !expired;
-    const double pv = present ? s.v : P.cap;              // TB:211-215
-    const double pt = present ? new_t_of(s.t_us) : new_t;
-    const double delta_t = lua_max(0.0, new_t - pt);      // TB:218
+    const double pv = present ? v : P.cap;                // TB:211-215
+    const double pt = present ? t : rq.new_t;
+    const double delta_t = lua_max(0.0, rq.new_t - pt);   // TB:218
     const double fill = delta_t * P.rate;                 // TB:221: mul ...
     double x = lua_max(0.0, lua_min(P.cap, pv + fill));   // ... then add (never fused)
     const double p = (double)permits;
     const bool granted = x >= p;                          // TB:224
     if (granted) {
         x = x - p;                                        // TB:227
-        s.v = x;                                          // TB:230 HSET v, t
-        s.t_us = ts_us;
+        v = x;                                            // TB:230 HSET v, t
+        t = rq.new_t;
+        tp = rq.tp;
     } else if (expired) {
-        s.v = P.cap;                                      // key deleted by passive expiry
-        s.t_us = kAbsent;
+        v = P.cap;                                        // key deleted by passive expiry
+        t = 0.0;
+        tp = kAbsent;
     }
     modified = granted || expired;
     return (granted ? 0x80000000u : 0u) | (uint32_t)(int32_t)x;   // {success, new_v}
+}
+
+// The same on a table row {v, t_us} (drain kernel, queueing fold).
+__device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t ts_us,
+                                               const TbParams &P, bool &modified) {
+    double v = s.v, t = (s.t_us == kAbsent) ? 0.0 : new_t_of(s.t_us);
+    int64_t tp = (s.t_us == kAbsent) ? kAbsent : tpack_of(s.t_us);
+    const uint32_t reply = tb_step(v, t, tp, permits, req_time(ts_us), P, modified);
+    if (modified) {
+        s.v = v;
+        s.t_us = ts_of_tpack(tp);
+    }
+    return reply;
 }
 
 // ----------------------------------------------------------------- wave / block helpers

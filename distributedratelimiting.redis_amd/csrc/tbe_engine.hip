@@ -31,6 +31,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/tbe.h"
@@ -145,13 +146,16 @@ __device__ __forceinline__ void tile_offsets(uint32_t tile, uint32_t tiles_per_b
 // Stable partition of one tile by digit d = (key >> shift) & 255.  Payload travels as
 // SoA {key u32, permits i32, ts i64}; it is staged through LDS in two 8-byte rounds so
 // each digit's run leaves the workgroup as one contiguous, coalesced write.
-template <typename KeyIn>
+// IDX: also carry each request's arrival index (queueing kind: it becomes the request
+// id of a queued entry); pass 0 generates it (iin == nullptr).
+template <typename KeyIn, bool IDX>
 __global__ __launch_bounds__(kPartBlock, 4) void k_scatter(
     const KeyIn *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
-    uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
+    const uint32_t *__restrict__ iin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
     const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
     uint32_t tiles_per_blk, uint32_t *__restrict__ kout, int32_t *__restrict__ pout,
-    int64_t *__restrict__ tout, uint32_t *__restrict__ err, int validate) {
+    int64_t *__restrict__ tout, uint32_t *__restrict__ iout, uint32_t *__restrict__ err,
+    int validate) {
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
@@ -213,6 +217,27 @@ __global__ __launch_bounds__(kPartBlock, 4) void k_scatter(
         const int j = it * kPartBlock + tid;
         if (j < nvalid) tout[gpos[it]] = (int64_t)stage[j];
     }
+    if (IDX) {
+        uint32_t *stage32 = reinterpret_cast<uint32_t *>(stage);
+        uint32_t iv[kPartItems];
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            iv[it] = (e < nvalid) ? (iin ? iin[base + e] : (uint32_t)(base + e)) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            if (e < nvalid) stage32[lpos[it]] = iv[it];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int j = it * kPartBlock + tid;
+            if (j < nvalid) iout[gpos[it]] = stage32[j];
+        }
+    }
     if (validate && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
@@ -248,19 +273,38 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t *__restrict__ 
 // Decide every request of one bucket (see file header).  res[q] is the packed reply of
 // sorted request q (bit 31 granted, bits 0-30 remaining).
 //
-// A dense bucket (>= R/8 requests) pulls its whole 16*R-byte slice of the table into
-// LDS with coalesced 16-B loads issued together with the first chunk's request loads,
-// and writes the slice back whole (full-line stores); a sparse bucket pulls only the
-// rows its requests touch and writes back only the rows that changed.
-__global__ __launch_bounds__(kBlock) void k_fold(
+// State of the bucket's R keys lives in LDS as SoA {v, t (f64 field t), tp (packed
+// grant time)}; a dense bucket (>= R/8 requests) pulls its whole 16*R-byte slice of the
+// table with coalesced loads and writes it back whole, a sparse one pulls and writes
+// back only the rows it touches.  Per chunk of 2048 requests (arrival order), every
+// request first computes its state-independent times (req_time, in parallel); then
+// rounds elect, per key, the earliest pending request (LDS atomicMax on a round-tagged
+// slot), which applies the cheap serial step tb_step.  Replies are staged in LDS and
+// leave as one coalesced store per chunk.
+constexpr int kFoldBlock = 512;
+constexpr int kFoldPer = 4;                                 // requests per thread per chunk
+constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
+constexpr int kMaxRows = 1 << kMaxRBits;
+
+__device__ __forceinline__ void load_row(const Slot &row, double *sv, double *st, int64_t *stp,
+                                         uint32_t j) {
+    sv[j] = row.v;
+    st[j] = (row.t_us == kAbsent) ? 0.0 : new_t_of(row.t_us);
+    stp[j] = (row.t_us == kAbsent) ? kAbsent : tpack_of(row.t_us);
+}
+
+__global__ __launch_bounds__(kFoldBlock, 2) void k_fold(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint32_t *__restrict__ bstart, int r_bits,
     uint64_t n_keys, Slot *__restrict__ table, TbParams P, uint32_t *__restrict__ res,
     const uint32_t *__restrict__ err) {
-    __shared__ Slot slot[1 << kMaxRBits];
-    __shared__ uint32_t own[1 << kMaxRBits];
-    __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
-    __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
+    __shared__ double sv[kMaxRows];
+    __shared__ double st[kMaxRows];
+    __shared__ int64_t stp[kMaxRows];
+    __shared__ uint32_t own[kMaxRows];
+    __shared__ uint32_t rbuf[kFoldChunk];
+    __shared__ uint32_t loaded[kMaxRows / 32];
+    __shared__ uint32_t dirty[kMaxRows / 32];
 
     if (*err) return;
     const int tid = threadIdx.x;
@@ -279,121 +323,131 @@ __global__ __launch_bounds__(kBlock) void k_fold(
 #endif
 
 #ifdef TBE_ABLATE_SKIP_TABLE
-    for (uint32_t j = tid; j < R; j += kBlock) slot[j] = Slot{P.cap, kAbsent};
-    if (false) {
+    for (uint32_t j = tid; j < R; j += kFoldBlock) { sv[j] = P.cap; st[j] = 0.0; stp[j] = kAbsent; }
 #else
     if (dense) {
-#endif
-        // Issue all of this thread's row loads before the first LDS store.
-        constexpr int kRowsPerThread = (1 << kMaxRBits) / kBlock;
+        constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
         Slot tmp[kRowsPerThread];
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kBlock;
+            const uint32_t j = tid + u * kFoldBlock;
             if (j < nrows) tmp[u] = rows[j];
         }
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kBlock;
-            if (j < nrows) slot[j] = tmp[u];
+            const uint32_t j = tid + u * kFoldBlock;
+            if (j < nrows) load_row(tmp[u], sv, st, stp, j);
         }
     }
-    for (uint32_t j = tid; j < R; j += kBlock) own[j] = kNoOwner;
-    for (uint32_t j = tid; j < (R + 31) / 32; j += kBlock) {
-        loaded[j] = dense ? ~0u : 0u;
+#endif
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
+        loaded[j] = 0;
         dirty[j] = 0;
     }
-    if (dense) __syncthreads();
 
-    for (uint32_t c = s; c < e; c += kChunk) {
-        uint32_t kl[kFoldItems];
-        int32_t pm[kFoldItems];
-        int64_t ts[kFoldItems];
+    for (uint32_t c = s; c < e; c += kFoldChunk) {
+        for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
+        uint32_t kl[kFoldPer];
+        int32_t pm[kFoldPer];
+        int64_t tsv[kFoldPer];
         uint32_t pend = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldItems; ++r) {
-            const uint32_t q = c + r * kBlock + tid;
+        for (int r = 0; r < kFoldPer; ++r) {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            kl[r] = 0; pm[r] = 0; tsv[r] = 0;
             if (q < e) {
                 kl[r] = skeys[q] & rmask;
                 pm[r] = sperm[q];
-                ts[r] = sts[q];
+                tsv[r] = sts[q];
                 pend |= 1u << r;
-            } else {
-                kl[r] = 0;
-                pm[r] = 0;
-                ts[r] = 0;
             }
         }
+        __syncthreads();   // own[] reset and (first chunk) dense slice visible
         if (!dense) {
-            // First touch of a row in this bucket pulls it into LDS: claim every row
-            // first, then issue all the claimed loads, then store them.
+            // First touch of a row in this bucket pulls it into LDS: claim, load, store.
             uint32_t mine = 0;
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r) {
+            for (int r = 0; r < kFoldPer; ++r) {
                 if (pend & (1u << r)) {
                     const uint32_t bit = 1u << (kl[r] & 31);
-                    const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
-                    if (!(old & bit)) mine |= 1u << r;
+                    if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
                 }
             }
-            Slot tmp[kFoldItems];
+            Slot tmp[kFoldPer];
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
+            for (int r = 0; r < kFoldPer; ++r)
                 if (mine & (1u << r)) tmp[r] = rows[kl[r]];
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
-                if (mine & (1u << r)) slot[kl[r]] = tmp[r];
+            for (int r = 0; r < kFoldPer; ++r)
+                if (mine & (1u << r)) load_row(tmp[r], sv, st, stp, kl[r]);
         }
-        __syncthreads();
+        ReqTime rq[kFoldPer];
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) rq[r] = req_time(tsv[r]);
+        if (!dense) __syncthreads();
 #ifdef TBE_ABLATE_SKIP_ROUNDS
-        if (pend) res[c + tid] = (uint32_t)pm[0] + (uint32_t)ts[0] + kl[0];
-        continue;
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r)
+            if (pend & (1u << r)) rbuf[r * kFoldBlock + tid] = (uint32_t)rq[r].new_t + (uint32_t)pm[r] + kl[r];
+        pend = 0;
+        if (__syncthreads_or(0))
 #endif
-        // Owner rounds: the earliest pending request of each key decides this round.
-        for (;;) {
+        // Rounds: slot value (round << 12) | (4095 - local id); the max is the earliest
+        // pending request of the key in the newest round, so no reset between rounds.
+        // Workgroup-uniform loop: every thread runs every round (barriers inside) and the
+        // only exit is the __syncthreads_or below.
+        for (uint32_t round = 1;; ++round) {
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
-                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kBlock + tid));
+            for (int r = 0; r < kFoldPer; ++r)
+                if (pend & (1u << r))
+                    atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
             __syncthreads();
-            uint32_t won = 0;
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r) {
-                if ((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kBlock + tid)) {
+            for (int r = 0; r < kFoldPer; ++r) {
+                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid));
+                if ((pend & (1u << r)) && own[kl[r]] == tag) {
+                    double v = sv[kl[r]], t = st[kl[r]];
+                    int64_t tp = stp[kl[r]];
                     bool modified;
-                    Slot st = slot[kl[r]];
-                    res[c + r * kBlock + tid] = tb_acquire(st, pm[r], ts[r], P, modified);
+                    rbuf[r * kFoldBlock + tid] = tb_step(v, t, tp, pm[r], rq[r], P, modified);
                     if (modified) {
-                        slot[kl[r]] = st;
+                        sv[kl[r]] = v;
+                        st[kl[r]] = t;
+                        stp[kl[r]] = tp;
                         if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     }
-                    won |= 1u << r;
+                    pend &= ~(1u << r);
                 }
             }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
-                if (won & (1u << r)) own[kl[r]] = kNoOwner;
-            pend &= ~won;
             if (!__syncthreads_or(pend != 0)) break;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            if (q < e) res[q] = rbuf[r * kFoldBlock + tid];
         }
     }
     __syncthreads();
 #ifdef TBE_ABLATE_SKIP_TABLE
-    if (slot[tid].v == -1.0) rows[tid] = slot[tid];
+    if (sv[tid] == -1.0) rows[tid] = Slot{sv[tid], ts_of_tpack(stp[tid])};
     return;
 #endif
-    if (dense) {
-        for (uint32_t j = tid; j < nrows; j += kBlock) rows[j] = slot[j];
-    } else {
-        for (uint32_t j = tid; j < nrows; j += kBlock)
-            if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = slot[j];
-    }
+    for (uint32_t j = tid; j < nrows; j += kFoldBlock)
+        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) rows[j] = Slot{sv[j], ts_of_tpack(stp[j])};
 }
 
 // Inverse of one k_scatter pass: recompute the tile's local ranks from the pass-input
 // keys, gather the replies from the pass-output positions, store them in pass-input
 // order.  FINAL = pass 0: unpack into granted (u8) / remaining (i32).
-template <typename KeyIn, bool FINAL>
+// Packed replies of the queueing kind: bits 31-30 TBE_WAIT_* status, bits 29-0
+// trunc(new_v), 0x3FFFFFFF when the script was not called.
+constexpr uint32_t kRemNone = 0x3FFFFFFFu;
+__device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, uint32_t rem) {
+    return (status << 30) | (evaluated ? (rem & kRemNone) : kRemNone);
+}
+
+template <typename KeyIn, bool FINAL, bool WAIT>
 __global__ __launch_bounds__(kPartBlock) void k_unscatter(
     const KeyIn *__restrict__ kin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
     const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
@@ -425,13 +479,238 @@ __global__ __launch_bounds__(kPartBlock) void k_unscatter(
     for (int it = 0; it < kPartItems; ++it) {
         const int e = it * kPartBlock + tid;
         if (e < nvalid) {
-            if (FINAL) {
+            if (FINAL && WAIT) {
+                granted[base + e] = (uint8_t)(r[it] >> 30);
+                const uint32_t rem = r[it] & kRemNone;
+                remaining[base + e] = (rem == kRemNone) ? -1 : (int32_t)rem;
+            } else if (FINAL) {
                 granted[base + e] = (uint8_t)(r[it] >> 31);
                 remaining[base + e] = (int32_t)(r[it] & 0x7FFFFFFFu);
             } else {
                 res_out[base + e] = r[it];
             }
         }
+    }
+}
+
+// ----------------------------------------------------------------------------- queueing kind
+// Per-key queue header (u64): bits 0-15 head, 16-31 count, 32-63 qsum (= _queueCount).
+// Ring entry (u64): bits 16-63 request id, 0-15 permits.  Ring of key k: ring[k*C .. k*C+C).
+struct QParams {
+    int32_t token_limit;
+    int32_t queue_limit;
+    int32_t order;       // 0 OldestFirst, 1 NewestFirst
+    uint32_t cap;        // ring entries per key (max(1, QueueLimit))
+    int64_t id_base;     // request id of arrival index 0 of this batch
+};
+__device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t qsum) {
+    return (uint64_t)(head & 0xFFFFu) | ((uint64_t)(cnt & 0xFFFFu) << 16) | ((uint64_t)qsum << 32);
+}
+
+// WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
+// the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
+// LDS and its ring in HBM.  A ring entry written in one round and read (evicted) in a
+// later round of the same workgroup is ordered by the round's __syncthreads
+// (workgroup-scope fence; one CU, one vector L1).
+__global__ __launch_bounds__(kBlock) void k_fold_q(
+    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
+    const int64_t *__restrict__ sts, const uint32_t *__restrict__ sidx,
+    const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
+    uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
+    uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err) {
+    __shared__ Slot slot[1 << kMaxRBits];
+    __shared__ uint64_t qh[1 << kMaxRBits];
+    __shared__ uint32_t own[1 << kMaxRBits];
+    __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
+    __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
+
+    if (*err) return;
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) return;
+    const uint32_t R = 1u << r_bits;
+    const uint32_t rmask = R - 1;
+    const uint64_t row0 = (uint64_t)b << r_bits;
+    const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
+    Slot *__restrict__ rows = table + row0;
+    uint64_t *__restrict__ hrows = qhdr + row0;
+
+    for (uint32_t j = tid; j < R; j += kBlock) own[j] = kNoOwner;
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kBlock) {
+        loaded[j] = 0;
+        dirty[j] = 0;
+    }
+    __syncthreads();
+
+    for (uint32_t c = s; c < e; c += kChunk) {
+        uint32_t kl[kFoldItems], ai[kFoldItems];
+        int32_t pm[kFoldItems];
+        int64_t ts[kFoldItems];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldItems; ++r) {
+            const uint32_t q = c + r * kBlock + tid;
+            if (q < e) {
+                kl[r] = skeys[q] & rmask;
+                pm[r] = sperm[q];
+                ts[r] = sts[q];
+                ai[r] = sidx[q];
+                pend |= 1u << r;
+            } else {
+                kl[r] = 0; pm[r] = 0; ts[r] = 0; ai[r] = 0;
+            }
+        }
+        uint32_t mine = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldItems; ++r) {
+            if (pend & (1u << r)) {
+                const uint32_t bit = 1u << (kl[r] & 31);
+                const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
+                if (!(old & bit)) mine |= 1u << r;
+            }
+        }
+        {
+            Slot tmp[kFoldItems];
+            uint64_t th[kFoldItems];
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (mine & (1u << r)) { tmp[r] = rows[kl[r]]; th[r] = hrows[kl[r]]; }
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (mine & (1u << r)) { slot[kl[r]] = tmp[r]; qh[kl[r]] = th[r]; }
+        }
+        __syncthreads();
+        for (;;) {
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kBlock + tid));
+            __syncthreads();
+            uint32_t won = 0;
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r) {
+                if (!((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kBlock + tid))) continue;
+                won |= 1u << r;
+                Slot st = slot[kl[r]];
+                const uint64_t h0 = qh[kl[r]];
+                uint32_t head = (uint32_t)(h0 & 0xFFFFu), cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
+                int64_t qsum = (int64_t)(h0 >> 32);
+                const int32_t p = pm[r];
+                uint32_t status, rem = 0;
+                bool evaluated = false, smod = false, hmod = false;
+                if (p > Q.token_limit) {                                   // Q:70-73
+                    status = TBE_WAIT_REJECTED;
+                } else {
+                    bool granted = false;
+                    if (p == 0 || !(cnt > 0 && Q.order == 0)) {            // Q:153
+                        bool m;
+                        const uint32_t reply = tb_acquire(st, p, ts[r], P, m);
+                        smod = m;
+                        evaluated = true;
+                        granted = (reply >> 31) != 0;
+                        rem = reply & 0x7FFFFFFFu;
+                    }
+                    if (granted) {
+                        status = TBE_WAIT_GRANTED;
+                    } else {
+                        uint64_t *__restrict__ kr = ring + (row0 + kl[r]) * (uint64_t)Q.cap;
+                        bool fail = false;
+                        if ((int64_t)Q.queue_limit - qsum < p) {           // Q:92
+                            if (Q.order == 1 && p <= Q.queue_limit) {      // Q:94-109
+                                while ((int64_t)Q.queue_limit - qsum < p) {
+                                    const uint64_t ent = kr[head];
+                                    const uint32_t at = atomicAdd(ev_count, 1u);
+                                    if (at < ev_cap) {
+                                        ev_cause[at] = ai[r];
+                                        ev_id[at] = (int64_t)(ent >> 16);
+                                    }
+                                    qsum -= (int64_t)(ent & 0xFFFFu);
+                                    head = (head + 1 == Q.cap) ? 0 : head + 1;
+                                    --cnt;
+                                }
+                            } else {
+                                fail = true;                               // Q:113
+                            }
+                        }
+                        if (fail) {
+                            status = TBE_WAIT_FAILED;
+                        } else {                                           // Q:117-132
+                            uint32_t tail = head + cnt;
+                            if (tail >= Q.cap) tail -= Q.cap;
+                            kr[tail] = ((uint64_t)(Q.id_base + ai[r]) << 16) | (uint32_t)p;
+                            ++cnt;
+                            qsum += p;
+                            hmod = true;
+                            status = TBE_WAIT_QUEUED;
+                        }
+                    }
+                }
+                res[c + r * kBlock + tid] = pack_wait(status, evaluated, rem);
+                if (smod) slot[kl[r]] = st;
+                if (hmod) qh[kl[r]] = qh_pack(head, cnt, qsum);
+                if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kFoldItems; ++r)
+                if (won & (1u << r)) own[kl[r]] = kNoOwner;
+            pend &= ~won;
+            if (!__syncthreads_or(pend != 0)) break;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < nrows; j += kBlock)
+        if (dirty[j >> 5] & (1u << (j & 31))) {
+            rows[j] = slot[j];
+            hrows[j] = qh[j];
+        }
+}
+
+// One replenish tick (Q:237-271) over every key: drain the head (OldestFirst) or tail
+// (NewestFirst) while the acquire script grants.  One thread per key.  Grants are logged
+// as (key, drain position, request id, remaining); the host orders them by key.
+__global__ __launch_bounds__(kBlock) void k_drain(
+    uint64_t n_keys, Slot *__restrict__ table, uint64_t *__restrict__ qhdr,
+    const uint64_t *__restrict__ ring, TbParams P, QParams Q, int64_t ts_us,
+    uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
+    uint32_t *__restrict__ log_count, uint32_t log_cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t key = (uint64_t)blockIdx.x * kBlock + threadIdx.x; key < n_keys; key += stride) {
+        const uint64_t h0 = qhdr[key];
+        uint32_t cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
+        if (cnt == 0) continue;
+        uint32_t head = (uint32_t)(h0 & 0xFFFFu);
+        int64_t qsum = (int64_t)(h0 >> 32);
+        Slot st = table[key];
+        bool smod = false;
+        uint32_t seq = 0;
+        const uint64_t *__restrict__ kr = ring + key * (uint64_t)Q.cap;
+        while (cnt > 0) {
+            uint32_t idx = head;
+            if (Q.order == 1) {
+                idx = head + cnt - 1;
+                if (idx >= Q.cap) idx -= Q.cap;
+            }
+            const uint64_t ent = kr[idx];
+            const int32_t p = (int32_t)(ent & 0xFFFFu);
+            bool m;
+            const uint32_t reply = tb_acquire(st, p, ts_us, P, m);
+            smod |= m;
+            if (!(reply >> 31)) break;
+            const uint32_t at = atomicAdd(log_count, 1u);
+            if (at < log_cap) {
+                log_keyseq[at] = (key << 16) | seq;
+                log_id[at] = (int64_t)(ent >> 16);
+                log_rem[at] = (int32_t)(reply & 0x7FFFFFFFu);
+            }
+            ++seq;
+            qsum -= p;
+            if (Q.order == 0) head = (head + 1 == Q.cap) ? 0 : head + 1;
+            --cnt;
+        }
+        if (smod) table[key] = st;
+        if (seq) qhdr[key] = qh_pack(head, cnt, qsum);
     }
 }
 
@@ -452,6 +731,7 @@ struct PassBufs {
     uint32_t *keys = nullptr;    // pass output (u32 keys)
     int32_t *permits = nullptr;
     int64_t *ts = nullptr;
+    uint32_t *idx = nullptr;     // arrival index (queueing kind only)
     uint32_t *tileprefix = nullptr;
     uint32_t *blockprefix = nullptr;
     uint32_t *digit_total = nullptr;
@@ -475,6 +755,21 @@ struct tbe_engine {
     uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
     int passes = 0;          // 8-bit LSD passes over the bucket id
     Slot *table = nullptr;
+    // queueing kind
+    QParams qp{};
+    uint64_t *qhdr = nullptr;      // per-key queue header
+    uint64_t *ring = nullptr;      // per-key rings of qp.cap entries
+    uint64_t queued_total = 0;     // entries in all queues (host-side count)
+    uint32_t *ev_cause = nullptr;  // eviction log of the last wait batch
+    int64_t *ev_id = nullptr;
+    uint64_t ev_cap = 0;
+    uint64_t *log_keyseq = nullptr;  // refresh grant log
+    int64_t *log_id = nullptr;
+    int32_t *log_rem = nullptr;
+    uint64_t log_cap = 0;
+    uint32_t *counters = nullptr;  // [0] eviction count, [1] refresh log count
+    std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
+    std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
 
     // workspace (sized for `cap_n` requests)
     uint64_t cap_n = 0;
@@ -531,6 +826,7 @@ void free_workspace(tbe_engine *e) {
         dfree(pb.keys);
         dfree(pb.permits);
         dfree(pb.ts);
+        dfree(pb.idx);
         dfree(pb.tileprefix);
         dfree(pb.blockprefix);
         dfree(pb.digit_total);
@@ -565,6 +861,7 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.keys, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
         HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
+        if (e->cfg.kind == TBE_KIND_QUEUEING) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.digit_total, kDigits * sizeof(uint32_t)));
@@ -616,7 +913,8 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 // Enqueue the whole pipeline for one device-resident batch.
 tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                      const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
-                     hipStream_t st) {
+                     hipStream_t st, int64_t id_base = 0) {
+    const bool wait = e->cfg.kind == TBE_KIND_QUEUEING;
     if (n == 0) return TBE_OK;
     if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
                                        (unsigned long long)n);
@@ -642,15 +940,24 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, st);
         stage_begin(e, ST_SCATTER, st);
-        if (p == 0)
-            k_scatter<uint64_t><<<ntiles, kPartBlock, 0, st>>>(
-                keys, permits, ts, n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb,
-                out.keys, out.permits, out.ts, e->err, 1);
-        else
-            k_scatter<uint32_t><<<ntiles, kPartBlock, 0, st>>>(
-                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, n, shift,
+        if (p == 0 && !wait)
+            k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, e->err, 1);
+        else if (p == 0)
+            k_scatter<uint64_t, true><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, e->err, 1);
+        else if (!wait)
+            k_scatter<uint32_t, false><<<ntiles, kPartBlock, 0, st>>>(
+                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, nullptr, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits,
-                out.ts, e->err, 0);
+                out.ts, nullptr, e->err, 0);
+        else
+            k_scatter<uint32_t, true><<<ntiles, kPartBlock, 0, st>>>(
+                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, e->pass[p - 1].idx,
+                n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys,
+                out.permits, out.ts, out.idx, e->err, 0);
         stage_end(e, ST_SCATTER, st);
     }
     const PassBufs &sorted = e->pass[e->passes - 1];
@@ -659,22 +966,36 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         sorted.keys, n, e->r_bits, e->nbuckets, e->bstart, e->err);
     stage_end(e, ST_BOUNDS, st);
     stage_begin(e, ST_FOLD, st);
-    k_fold<<<e->nbuckets, kBlock, 0, st>>>(sorted.keys, sorted.permits, sorted.ts, e->bstart,
-                                           e->r_bits, e->cfg.n_keys, e->table, e->params,
-                                           e->res[0], e->err);
+    if (wait) {
+        QParams q = e->qp;
+        q.id_base = id_base;
+        k_fold_q<<<e->nbuckets, kBlock, 0, st>>>(
+            sorted.keys, sorted.permits, sorted.ts, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys,
+            e->table, e->qhdr, e->ring, e->params, q, e->res[0], e->ev_cause, e->ev_id,
+            e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), e->err);
+    } else {
+        k_fold<<<e->nbuckets, kFoldBlock, 0, st>>>(sorted.keys, sorted.permits, sorted.ts, e->bstart,
+                                               e->r_bits, e->cfg.n_keys, e->table, e->params,
+                                               e->res[0], e->err);
+    }
     stage_end(e, ST_FOLD, st);
     stage_begin(e, ST_UNSCATTER, st);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
         const PassBufs &pb = e->pass[p];
-        k_unscatter<uint32_t, false><<<ntiles, kPartBlock, 0, st>>>(
+        k_unscatter<uint32_t, false, false><<<ntiles, kPartBlock, 0, st>>>(
             e->pass[p - 1].keys, n, e->r_bits + kDigitBits * p, pb.tileprefix, pb.blockprefix,
             pb.digit_total, tpb, e->res[cur], e->res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
-    k_unscatter<uint64_t, true><<<ntiles, kPartBlock, 0, st>>>(
-        keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix, e->pass[0].digit_total,
-        tpb, e->res[cur], nullptr, granted, remaining);
+    if (wait)
+        k_unscatter<uint64_t, true, true><<<ntiles, kPartBlock, 0, st>>>(
+            keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix,
+            e->pass[0].digit_total, tpb, e->res[cur], nullptr, granted, remaining);
+    else
+        k_unscatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
+            keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix,
+            e->pass[0].digit_total, tpb, e->res[cur], nullptr, granted, remaining);
     stage_end(e, ST_UNSCATTER, st);
     k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
     HIP_TRY(e, hipGetLastError());
@@ -696,7 +1017,12 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     *out_engine = nullptr;
     if (!config || config->struct_size < sizeof(tbe_config)) return TBE_EINVAL;
     const tbe_config &c = *config;
-    if (c.kind != TBE_KIND_TOKEN_BUCKET) return TBE_EINVAL;
+    if (c.kind != TBE_KIND_TOKEN_BUCKET && c.kind != TBE_KIND_QUEUEING) return TBE_EINVAL;
+    if (c.kind == TBE_KIND_QUEUEING) {
+        if (c.queue_limit < 0 || c.queue_limit > 0xFFFF) return TBE_EINVAL;        // Q ctor
+        if (c.queue_order != 0 && c.queue_order != 1) return TBE_EINVAL;
+        if (c.token_limit >= (int32_t)kRemNone) return TBE_EINVAL;                 // reply packing
+    }
     if (c.n_keys == 0 || c.n_keys > (1ull << 32)) return TBE_EINVAL;
     if (c.token_limit <= 0 || c.tokens_per_period <= 0) return TBE_EINVAL;   // TB:29-32
     if (c.replenishment_period_ticks <= 0) return TBE_EINVAL;                // TB:34-37 (+ "∞")
@@ -742,6 +1068,18 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     if (hipMemsetAsync(e->err, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess)
         return bail(TBE_EDEVICE);
     k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
+    if (c.kind == TBE_KIND_QUEUEING) {
+        e->qp.token_limit = c.token_limit;
+        e->qp.queue_limit = c.queue_limit;
+        e->qp.order = c.queue_order;
+        e->qp.cap = (uint32_t)std::max(1, c.queue_limit);
+        if (hipMalloc(&e->qhdr, c.n_keys * sizeof(uint64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->ring, c.n_keys * (uint64_t)e->qp.cap * sizeof(uint64_t)) != hipSuccess)
+            return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMemsetAsync(e->qhdr, 0, c.n_keys * sizeof(uint64_t), e->stream) != hipSuccess)
+            return bail(TBE_EDEVICE);
+    }
     if (c.max_batch && ensure_workspace(e, c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(TBE_EDEVICE);
     *out_engine = e;
@@ -753,6 +1091,14 @@ void tbe_destroy(tbe_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_workspace(e);
     dfree(e->table);
+    dfree(e->qhdr);
+    dfree(e->ring);
+    dfree(e->counters);
+    dfree(e->ev_cause);
+    dfree(e->ev_id);
+    dfree(e->log_keyseq);
+    dfree(e->log_id);
+    dfree(e->log_rem);
     dfree(e->bstart);
     dfree(e->err);
     for (auto &ev : e->ev_pool)
@@ -769,6 +1115,7 @@ tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t 
                              const int64_t *ts_us, uint64_t n, uint8_t *granted,
                              int32_t *remaining) {
     if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_TOKEN_BUCKET) return fail(e, TBE_EINVAL, "not a token-bucket engine");
     if (n == 0) return TBE_OK;
     if (!keys || !permits || !ts_us || !granted || !remaining)
         return fail(e, TBE_EINVAL, "null buffer");
@@ -798,6 +1145,7 @@ tbe_status tbe_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys, const
                                     const int64_t *d_ts_us, uint64_t n, uint8_t *d_granted,
                                     int32_t *d_remaining, void *stream) {
     if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_TOKEN_BUCKET) return fail(e, TBE_EINVAL, "not a token-bucket engine");
     if (n == 0) return TBE_OK;
     if (!d_keys || !d_permits || !d_ts_us || !d_granted || !d_remaining)
         return fail(e, TBE_EINVAL, "null buffer");
@@ -853,6 +1201,162 @@ tbe_status tbe_export_state(tbe_engine *e, uint64_t first, uint64_t count, doubl
         v[i] = tmp[i].v;
         t_us[i] = tmp[i].t_us;
     }
+    return TBE_OK;
+}
+
+tbe_status tbe_wait_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                          const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
+                          int32_t *remaining, uint64_t *n_evicted) {
+    if (!e || !n_evicted) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    *n_evicted = 0;
+    e->evicted.clear();
+    if (n == 0) return TBE_OK;
+    if (!keys || !permits || !ts_us || !status || !remaining) return fail(e, TBE_EINVAL, "null buffer");
+    if (id_base < 0 || (uint64_t)id_base + n > (1ull << 47))
+        return fail(e, TBE_EINVAL, "request ids must lie in [0, 2^47)");
+    HIP_TRY(e, hipSetDevice(e->device));
+    tbe_status rc = ensure_host_staging(e, n);
+    if (rc != TBE_OK) return rc;
+    // Evictions in one batch are bounded by the entries queued before it plus n.
+    const uint64_t need_ev = e->queued_total + n;
+    if (need_ev > e->ev_cap) {
+        dfree(e->ev_cause);
+        dfree(e->ev_id);
+        e->ev_cap = 0;
+        HIP_TRY(e, hipMalloc(&e->ev_cause, need_ev * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&e->ev_id, need_ev * sizeof(int64_t)));
+        e->ev_cap = need_ev;
+    }
+    hipStream_t st = e->stream;
+    HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), st));
+    HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    rc = run_batch(e, e->d_keys, e->d_permits, e->d_ts, n, e->d_granted, e->d_remaining, st, id_base);
+    if (rc != TBE_OK) return rc;
+    uint32_t flag = 0, nev = 0;
+    HIP_TRY(e, hipMemcpyAsync(&flag, e->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(&nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(status, e->d_granted, n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipStreamSynchronize(st));
+    if (flag) {
+        HIP_TRY(e, hipMemsetAsync(e->err + 1, 0, sizeof(uint32_t), st));
+        HIP_TRY(e, hipStreamSynchronize(st));
+        return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
+    }
+    if (nev) {
+        std::vector<uint32_t> cause(nev);
+        std::vector<int64_t> id(nev);
+        HIP_TRY(e, hipMemcpy(cause.data(), e->ev_cause, nev * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(e, hipMemcpy(id.data(), e->ev_id, nev * sizeof(int64_t), hipMemcpyDeviceToHost));
+        e->evicted.resize(nev);
+        for (uint32_t i = 0; i < nev; ++i) e->evicted[i] = {cause[i], id[i]};
+        std::sort(e->evicted.begin(), e->evicted.end());
+    }
+    uint64_t queued = 0;
+    for (uint64_t i = 0; i < n; ++i) queued += status[i] == TBE_WAIT_QUEUED;
+    e->queued_total = e->queued_total + queued - nev;
+    *n_evicted = nev;
+    return TBE_OK;
+}
+
+tbe_status tbe_evicted(tbe_engine *e, uint64_t *cause_index, int64_t *request_id, uint64_t capacity,
+                       uint64_t *n_written) {
+    if (!e || !n_written) return TBE_EINVAL;
+    const uint64_t m = std::min<uint64_t>(capacity, e->evicted.size());
+    if (m && (!cause_index || !request_id)) return fail(e, TBE_EINVAL, "null buffer");
+    for (uint64_t i = 0; i < m; ++i) {
+        cause_index[i] = e->evicted[i].first;
+        request_id[i] = e->evicted[i].second;
+    }
+    *n_written = m;
+    return TBE_OK;
+}
+
+tbe_status tbe_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
+    if (!e || !n_granted) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (ts_us < 0) return fail(e, TBE_EINVAL, "ts_us < 0");
+    *n_granted = 0;
+    e->drained.clear();
+    if (e->queued_total == 0) return TBE_OK;
+    HIP_TRY(e, hipSetDevice(e->device));
+    if (e->queued_total > e->log_cap) {
+        dfree(e->log_keyseq);
+        dfree(e->log_id);
+        dfree(e->log_rem);
+        e->log_cap = 0;
+        HIP_TRY(e, hipMalloc(&e->log_keyseq, e->queued_total * sizeof(uint64_t)));
+        HIP_TRY(e, hipMalloc(&e->log_id, e->queued_total * sizeof(int64_t)));
+        HIP_TRY(e, hipMalloc(&e->log_rem, e->queued_total * sizeof(int32_t)));
+        e->log_cap = e->queued_total;
+    }
+    hipStream_t st = e->stream;
+    HIP_TRY(e, hipMemsetAsync(e->counters + 1, 0, sizeof(uint32_t), st));
+    const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+    k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params,
+                                                e->qp, ts_us, e->log_keyseq, e->log_id, e->log_rem,
+                                                e->counters + 1,
+                                                (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu));
+    HIP_TRY(e, hipGetLastError());
+    uint32_t cnt = 0;
+    HIP_TRY(e, hipMemcpyAsync(&cnt, e->counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipStreamSynchronize(st));
+    if (cnt) {
+        std::vector<uint64_t> ks(cnt);
+        std::vector<int64_t> id(cnt);
+        std::vector<int32_t> rem(cnt);
+        HIP_TRY(e, hipMemcpy(ks.data(), e->log_keyseq, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(e, hipMemcpy(id.data(), e->log_id, cnt * sizeof(int64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(e, hipMemcpy(rem.data(), e->log_rem, cnt * sizeof(int32_t), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> order(cnt);
+        for (uint32_t i = 0; i < cnt; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ks[a] < ks[b]; });
+        e->drained.resize(cnt);
+        for (uint32_t i = 0; i < cnt; ++i)
+            e->drained[i] = std::make_tuple(ks[order[i]] >> 16, id[order[i]], rem[order[i]]);
+    }
+    e->queued_total -= cnt;
+    *n_granted = cnt;
+    return TBE_OK;
+}
+
+tbe_status tbe_refresh_log(tbe_engine *e, uint64_t *keys, int64_t *request_id, int32_t *remaining,
+                           uint64_t capacity, uint64_t *n_written) {
+    if (!e || !n_written) return TBE_EINVAL;
+    const uint64_t m = std::min<uint64_t>(capacity, e->drained.size());
+    if (m && (!keys || !request_id || !remaining)) return fail(e, TBE_EINVAL, "null buffer");
+    for (uint64_t i = 0; i < m; ++i) {
+        keys[i] = std::get<0>(e->drained[i]);
+        request_id[i] = std::get<1>(e->drained[i]);
+        remaining[i] = std::get<2>(e->drained[i]);
+    }
+    *n_written = m;
+    return TBE_OK;
+}
+
+tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_t *permits,
+                        uint32_t capacity, uint32_t *count) {
+    if (!e || !count) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (key >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    uint64_t h = 0;
+    std::vector<uint64_t> ent(e->qp.cap);
+    HIP_TRY(e, hipMemcpy(&h, e->qhdr + key, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(ent.data(), e->ring + key * (uint64_t)e->qp.cap, e->qp.cap * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost));
+    const uint32_t head = (uint32_t)(h & 0xFFFFu), cnt = (uint32_t)((h >> 16) & 0xFFFFu);
+    if (cnt && (!request_id || !permits) && capacity) return fail(e, TBE_EINVAL, "null buffer");
+    for (uint32_t j = 0; j < cnt && j < capacity; ++j) {
+        const uint64_t x = ent[(head + j) % e->qp.cap];
+        request_id[j] = (int64_t)(x >> 16);
+        permits[j] = (int32_t)(x & 0xFFFFu);
+    }
+    *count = cnt;
     return TBE_OK;
 }
 

@@ -23,12 +23,17 @@ def fill_rate(tokens_per_period: int, period_ticks: int) -> float:
 
 
 class TokenBucketEngine:
+    KIND = _capi.TBE_KIND_TOKEN_BUCKET
+
     def __init__(self, n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
-                 device: int = -1, stage_timing: bool = False, max_batch: int = 0):
+                 device: int = -1, stage_timing: bool = False, max_batch: int = 0,
+                 queue_limit: int = 0, queue_order: int = 0):
         self._lib = _capi.load()
         flags = _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0
         self.config = _capi.make_config(n_keys, token_limit, tokens_per_period, period_ticks,
-                                        device=device, flags=flags, max_batch=max_batch)
+                                        kind=self.KIND, queue_limit=queue_limit,
+                                        queue_order=queue_order, device=device, flags=flags,
+                                        max_batch=max_batch)
         h = c_void_p()
         st = self._lib.tbe_create(byref(self.config), byref(h))
         if st != _capi.TBE_OK:
@@ -112,3 +117,60 @@ class TokenBucketEngine:
         nw = c_uint32()
         self._check(self._lib.tbe_stage_times(self.handle, out, len(_capi.STAGES), byref(nw)))
         return {name: out[i] for i, name in enumerate(_capi.STAGES[: nw.value])}
+
+
+class QueueingTokenBucketEngine(TokenBucketEngine):
+    """TokenBucketWithQueue (TokenBucketWithQueue/RedisTokenBucketRateLimiter.cs, Q):
+    WaitAsyncCore (Q:67-134) as ``wait_batch``, the timer drain (Q:237-271) as ``refresh``."""
+
+    KIND = _capi.TBE_KIND_QUEUEING
+
+    def __init__(self, n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
+                 queue_limit: int, queue_order: int = 0, **kw):
+        super().__init__(n_keys, token_limit, tokens_per_period, period_ticks,
+                         queue_limit=queue_limit, queue_order=queue_order, **kw)
+        self.queue_limit = queue_limit
+
+    def wait_batch(self, keys, permits, ts_us, id_base: int):
+        """Returns (status u8, remaining i32, evicted (cause index u64, request id i64))."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        permits = np.ascontiguousarray(permits, dtype=np.int32)
+        ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+        n = keys.shape[0]
+        status = np.empty(n, dtype=np.uint8)
+        remaining = np.empty(n, dtype=np.int32)
+        n_ev = ctypes.c_uint64()
+        self._check(self._lib.tbe_wait_batch(self.handle, keys.ctypes.data, permits.ctypes.data,
+                                             ts_us.ctypes.data, n, id_base, status.ctypes.data,
+                                             remaining.ctypes.data, byref(n_ev)))
+        m = n_ev.value
+        cause = np.empty(m, dtype=np.uint64)
+        ids = np.empty(m, dtype=np.int64)
+        nw = ctypes.c_uint64()
+        if m:
+            self._check(self._lib.tbe_evicted(self.handle, cause.ctypes.data, ids.ctypes.data, m, byref(nw)))
+        return status, remaining, (cause, ids)
+
+    def refresh(self, ts_us: int):
+        """One replenish tick; returns (keys u64, request ids i64, remaining i32) in (key, drain) order."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.tbe_refresh(self.handle, ts_us, byref(n)))
+        m = n.value
+        keys = np.empty(m, dtype=np.uint64)
+        ids = np.empty(m, dtype=np.int64)
+        rem = np.empty(m, dtype=np.int32)
+        nw = ctypes.c_uint64()
+        if m:
+            self._check(self._lib.tbe_refresh_log(self.handle, keys.ctypes.data, ids.ctypes.data,
+                                                  rem.ctypes.data, m, byref(nw)))
+        return keys, ids, rem
+
+    def queue_of(self, key: int):
+        cap = max(1, self.queue_limit)
+        ids = np.empty(cap, dtype=np.int64)
+        ps = np.empty(cap, dtype=np.int32)
+        cnt = c_uint32()
+        self._check(self._lib.tbe_queue_of(self.handle, key, ids.ctypes.data, ps.ctypes.data, cap,
+                                           byref(cnt)))
+        c = min(cnt.value, cap)
+        return list(zip(ids[:c].tolist(), ps[:c].tolist()))

@@ -45,7 +45,7 @@ typedef enum tbe_status {
 
 typedef enum tbe_kind {
     TBE_KIND_TOKEN_BUCKET = 0,   /* TokenBucket/ (TB, PTB)                                */
-    TBE_KIND_QUEUEING = 1,       /* TokenBucketWithQueue/ (reserved) */
+    TBE_KIND_QUEUEING = 1,       /* TokenBucketWithQueue/           */
     TBE_KIND_APPROXIMATE = 2     /* ApproximateTokenBucket/ (reserved; §8a a9-a12)        */
 } tbe_kind;
 
@@ -59,7 +59,7 @@ typedef struct tbe_config {
     int32_t token_limit;                  /* TokenLimit (TBO:43), > 0 */
     int32_t tokens_per_period;            /* TokensPerPeriod (TBO:30), > 0 */
     int64_t replenishment_period_ticks;   /* ReplenishmentPeriod in .NET ticks (100 ns), > 0 */
-    int32_t queue_limit;                  /* QueueLimit (queueing kind; ignored otherwise) */
+    int32_t queue_limit;                  /* QueueLimit (queueing kind: 0..65535; ignored otherwise) */
     int32_t queue_order;                  /* 0 = OldestFirst, 1 = NewestFirst */
     int32_t device;                       /* HIP device ordinal; -1 = current device */
     uint32_t flags;                       /* TBE_FLAG_* */
@@ -117,6 +117,46 @@ tbe_status tbe_query(tbe_engine *engine, uint64_t key, int64_t ts_us, double *v,
  * t_us[k] (INT64_MIN when never granted) for keys [first, first + count). */
 tbe_status tbe_export_state(tbe_engine *engine, uint64_t first, uint64_t count, double *v,
                             int64_t *t_us);
+
+/* ---------------------------------------------------------------- TokenBucketWithQueue
+ * Engines created with kind = TBE_KIND_QUEUEING.  The reference limiter
+ * (TokenBucketWithQueue/RedisTokenBucketRateLimiter.cs, "Q") is commented out and does
+ * not compile; its semantics are fixed in DESIGN.md §2b (a lease is one TB script call;
+ * queue order follows System.Collections.Generic/Deque.cs).  Per-key queues hold at most
+ * QueueLimit entries (permits >= 1 each). */
+#define TBE_WAIT_FAILED 0    /* CreateFailedTokenLease (Q:113, Q:383-388) */
+#define TBE_WAIT_GRANTED 1   /* SuccessfulLease (Q:85-88) */
+#define TBE_WAIT_QUEUED 2    /* registration enqueued (Q:117-132); completes via tbe_refresh */
+#define TBE_WAIT_REJECTED 3  /* permits > TokenLimit: ArgumentOutOfRangeException (Q:70-73) */
+
+/* Replaces n WaitAsyncCore calls (Q:67-134).  Request i gets id id_base + i (0 <= id <
+ * 2^47).  status[i] is a TBE_WAIT_* code; remaining[i] = trunc(new_v) of the script call
+ * made for the request, or -1 when no call was made (OldestFirst with a non-empty queue,
+ * or REJECTED).  Queued requests that a NewestFirst admission evicted (Q:94-109) are
+ * retrievable with tbe_evicted until the next batch; *n_evicted gets their number. */
+tbe_status tbe_wait_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
+                          const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
+                          int32_t *remaining, uint64_t *n_evicted);
+
+/* Evictions of the last tbe_wait_batch, sorted by (causing request index, request id):
+ * cause_index[j] is the batch index of the request whose admission evicted request_id[j]. */
+tbe_status tbe_evicted(tbe_engine *engine, uint64_t *cause_index, int64_t *request_id,
+                       uint64_t capacity, uint64_t *n_written);
+
+/* One replenish tick at ts_us (the timer-driven drain, Q:237-271): for every key with a
+ * non-empty queue, grant the head (OldestFirst) or tail (NewestFirst) while the script
+ * grants.  *n_granted gets the number of queued requests completed; fetch them with
+ * tbe_refresh_log. */
+tbe_status tbe_refresh(tbe_engine *engine, int64_t ts_us, uint64_t *n_granted);
+
+/* Grants of the last tbe_refresh in (key, drain order): key, request id and
+ * trunc(new_v) after the grant. */
+tbe_status tbe_refresh_log(tbe_engine *engine, uint64_t *keys, int64_t *request_id,
+                           int32_t *remaining, uint64_t capacity, uint64_t *n_written);
+
+/* Queue of one key, oldest first (Deque enumeration order, DQ:116-125). */
+tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, int32_t *permits,
+                        uint32_t capacity, uint32_t *count);
 
 /* Per-stage device time (ms) accumulated since the last call, when
  * TBE_FLAG_STAGE_TIMING is set: out[0..n_out) = {hist, colscan, scatter, bounds,

@@ -105,3 +105,81 @@ def gen_batch(seed: int, n_keys: int, batch: int, n: int, interval_us: int, p_lo
     lib.tbr_gen_permits(seed, g0, n, p_lo, p_hi, permits.ctypes.data)
     lib.tbr_gen_timestamps(batch, n, interval_us, t0_us, ts.ctypes.data)
     return keys, permits, ts
+
+
+class CQueueingTokenBucket:
+    """C restatement of the TokenBucketWithQueue spec (oracle/tb_ref.c tbrq_*)."""
+
+    def __init__(self, n_keys: int, token_limit: int, fill_rate: float, queue_limit: int, order: int):
+        lib = load()
+        lib.tbrq_create.restype = c_void_p
+        lib.tbrq_create.argtypes = [c_uint64, c_int32, c_double, c_int32, c_int32]
+        lib.tbrq_destroy.argtypes = [c_void_p]
+        lib.tbrq_acquire_batch.restype = c_int
+        lib.tbrq_acquire_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_int64,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]
+        lib.tbrq_refresh.restype = c_int
+        lib.tbrq_refresh.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]
+        lib.tbrq_queue_of.restype = ctypes.c_uint32
+        lib.tbrq_queue_of.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, ctypes.c_uint32]
+        lib.tbrq_bucket_table.restype = c_void_p
+        lib.tbrq_bucket_table.argtypes = [c_void_p]
+        self._lib = lib
+        self._h = lib.tbrq_create(n_keys, token_limit, fill_rate, queue_limit, order)
+        if not self._h:
+            raise ValueError("tbrq_create rejected the configuration")
+        self.n_keys, self.queue_limit = n_keys, queue_limit
+
+    def close(self):
+        if self._h:
+            self._lib.tbrq_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def acquire_batch(self, keys, permits, ts_us, id_base: int):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        permits = np.ascontiguousarray(permits, dtype=np.int32)
+        ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+        n = keys.shape[0]
+        status = np.empty(n, np.uint8)
+        remaining = np.empty(n, np.int32)
+        max_ev = n * max(1, self.queue_limit) + 1
+        ev_id = np.empty(max_ev, np.int64)
+        ev_cause = np.empty(max_ev, np.uint64)
+        n_ev = ctypes.c_uint64()
+        rc = self._lib.tbrq_acquire_batch(self._h, keys.ctypes.data, permits.ctypes.data,
+                                          ts_us.ctypes.data, n, id_base, status.ctypes.data,
+                                          remaining.ctypes.data, ev_id.ctypes.data,
+                                          ev_cause.ctypes.data, max_ev, ctypes.byref(n_ev))
+        if rc != 0:
+            raise ValueError("invalid request in batch")
+        m = n_ev.value
+        return status, remaining, ev_cause[:m].copy(), ev_id[:m].copy()
+
+    def refresh(self, ts_us: int):
+        cap = int(self.n_keys) * max(1, self.queue_limit)
+        cap = min(cap, 1 << 26)
+        lk = np.empty(cap, np.uint64)
+        lid = np.empty(cap, np.int64)
+        lrem = np.empty(cap, np.int32)
+        nl = ctypes.c_uint64()
+        rc = self._lib.tbrq_refresh(self._h, ts_us, lk.ctypes.data, lid.ctypes.data, lrem.ctypes.data,
+                                    cap, ctypes.byref(nl))
+        if rc != 0:
+            raise ValueError("invalid refresh")
+        m = min(nl.value, cap)
+        return lk[:m].copy(), lid[:m].copy(), lrem[:m].copy()
+
+    def queue_of(self, key: int):
+        ids = np.empty(max(1, self.queue_limit), np.int64)
+        ps = np.empty(max(1, self.queue_limit), np.int32)
+        c = self._lib.tbrq_queue_of(self._h, key, ids.ctypes.data, ps.ctypes.data, ids.size)
+        return list(zip(ids[:c].tolist(), ps[:c].tolist()))
+
+    def bucket_state(self):
+        v = np.empty(self.n_keys, dtype=np.float64)
+        t = np.empty(self.n_keys, dtype=np.int64)
+        self._lib.tbr_export(self._lib.tbrq_bucket_table(self._h), v.ctypes.data, t.ctypes.data)
+        return v, t

@@ -239,3 +239,91 @@ def instance_count_estimate(replenishment_seconds: float, period: float) -> floa
     if math.isnan(r):
         return math.nan  # Math.Max(1, NaN) = NaN in .NET
     return max(1.0, r)
+
+
+# ---------------------------------------------------------------- token bucket with queue
+# TokenBucketWithQueue/RedisTokenBucketRateLimiter.cs ("Q") is commented out and does not
+# compile (it uses members it never declares), so its semantics are
+# fixed here by composing its control flow with the TB acquire script as the only
+# token source:
+#   WaitAsyncCore           Q:67-134   admission (lease, else queue, else fail)
+#   TryLeaseUnsynchronized  Q:136-165  OldestFirst never leases past a non-empty queue
+#   RefreshAsync drain      Q:237-271  head (OldestFirst) / tail (NewestFirst) while granted
+#   Deque order             DQ:19-94   EnqueueTail, DequeueHead, PeekTail/DequeueTail
+# Decisions on undefined behaviour: a lease IS one TB script call
+# (`AvailableTokens >= count` + consume is the script's x >= p + HSET); p == 0 goes
+# straight through the script (never queued: unbounded zero-permit queueing is a
+# reference quirk); p > TokenLimit is rejected per request
+# (ArgumentOutOfRangeException, Q:70-73).
+
+OLDEST_FIRST, NEWEST_FIRST = 0, 1
+ST_FAILED, ST_GRANTED, ST_QUEUED, ST_REJECTED = 0, 1, 2, 3
+REMAINING_NOT_EVALUATED = -1   # the script was not called for this request
+
+
+@dataclass
+class QueueEntry:
+    request_id: int
+    permits: int
+
+
+class QueueingTokenBucketTable:
+    """Per-key bucket (TB script) + per-key deque of waiting requests."""
+
+    def __init__(self, cfg: TokenBucketConfig, queue_limit: int, order: int):
+        if queue_limit < 0:
+            raise ValueError("QueueLimit must be set to a value greater than or equal to 0.")
+        self.tb = TokenBucketTable(cfg)
+        self.queue_limit = queue_limit
+        self.order = order
+        self.queues: Dict[int, List[QueueEntry]] = {}
+        self.qsum: Dict[int, int] = {}
+
+    def acquire(self, key: int, permits: int, ts_us: int, request_id: int):
+        """Returns (status, remaining, evicted_ids)."""
+        if permits < 0:
+            raise ArgumentOutOfRange("permitCount")
+        if permits > self.tb.cfg.token_limit:                       # Q:70-73
+            return ST_REJECTED, REMAINING_NOT_EVALUATED, []
+        q = self.queues.setdefault(key, [])
+        qsum = self.qsum.get(key, 0)
+        remaining = REMAINING_NOT_EVALUATED
+        if permits == 0 or not (q and self.order == OLDEST_FIRST):  # Q:153
+            granted, remaining = self.tb.acquire(key, permits, ts_us)
+            if granted:
+                return ST_GRANTED, remaining, []
+        evicted = []
+        if self.queue_limit - qsum < permits:                        # Q:92
+            if self.order == NEWEST_FIRST and permits <= self.queue_limit:   # Q:94-109
+                while self.queue_limit - qsum < permits:
+                    e = q.pop(0)                                     # DequeueHead
+                    qsum -= e.permits
+                    evicted.append(e.request_id)
+            else:
+                self.qsum[key] = qsum
+                return ST_FAILED, remaining, []                      # Q:113
+        q.append(QueueEntry(request_id, permits))                    # Q:128 EnqueueTail
+        self.qsum[key] = qsum + permits
+        return ST_QUEUED, remaining, evicted
+
+    def refresh(self, ts_us: int):
+        """Drain every non-empty queue at one replenish tick (Q:237-271).  Returns the
+        grant log [(key, request_id, remaining)] in (key, drain order)."""
+        log = []
+        for key in sorted(self.queues):
+            q = self.queues[key]
+            while q:
+                e = q[0] if self.order == OLDEST_FIRST else q[-1]    # PeekHead / PeekTail
+                granted, remaining = self.tb.acquire(key, e.permits, ts_us)
+                if not granted:
+                    break
+                if self.order == OLDEST_FIRST:
+                    q.pop(0)                                          # DequeueHead
+                else:
+                    q.pop()                                           # DequeueTail
+                self.qsum[key] -= e.permits
+                log.append((key, e.request_id, remaining))
+        return log
+
+    def queue_of(self, key: int) -> List[Tuple[int, int]]:
+        return [(e.request_id, e.permits) for e in self.queues.get(key, [])]

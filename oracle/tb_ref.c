@@ -206,3 +206,132 @@ void tbr_gen_timestamps(int64_t batch, uint64_t n, int64_t interval_us, int64_t 
     for (uint64_t i = 0; i < n; ++i)
         out[i] = t0_us + batch * interval_us + (int64_t)(((__int128)i * interval_us) / (__int128)n);
 }
+
+/* ------------------------------------------------------------------ token bucket with queue
+ * C restatement of oracle/semantics.py QueueingTokenBucketTable (the build's spec for the
+ * non-compiling TokenBucketWithQueue limiter, Q:67-165 + Q:237-271 + TB script + DQ order).
+ * Per key: a ring of QueueLimit entries {request id, permits} (permits >= 1, so at most
+ * QueueLimit entries), head, count and qsum (= _queueCount). */
+enum { TBRQ_FAILED = 0, TBRQ_GRANTED = 1, TBRQ_QUEUED = 2, TBRQ_REJECTED = 3 };
+
+typedef struct {
+    tbr_table *tb;
+    int32_t token_limit, queue_limit, order;   /* order: 0 OldestFirst, 1 NewestFirst */
+    uint32_t ring_cap;
+    int64_t *ring_id;
+    int32_t *ring_p;
+    uint32_t *head, *count;
+    int64_t *qsum;
+} tbrq_table;
+
+tbrq_table *tbrq_create(uint64_t n_keys, int32_t token_limit, double fill_rate, int32_t queue_limit,
+                        int32_t order) {
+    if (queue_limit < 0 || (order != 0 && order != 1)) return NULL;
+    tbrq_table *q = (tbrq_table *)calloc(1, sizeof(tbrq_table));
+    if (!q) return NULL;
+    q->tb = tbr_create(n_keys, token_limit, fill_rate);
+    q->token_limit = token_limit;
+    q->queue_limit = queue_limit;
+    q->order = order;
+    q->ring_cap = (uint32_t)(queue_limit > 0 ? queue_limit : 1);
+    q->ring_id = (int64_t *)calloc(n_keys * q->ring_cap, sizeof(int64_t));
+    q->ring_p = (int32_t *)calloc(n_keys * q->ring_cap, sizeof(int32_t));
+    q->head = (uint32_t *)calloc(n_keys, sizeof(uint32_t));
+    q->count = (uint32_t *)calloc(n_keys, sizeof(uint32_t));
+    q->qsum = (int64_t *)calloc(n_keys, sizeof(int64_t));
+    if (!q->tb || !q->ring_id || !q->ring_p || !q->head || !q->count || !q->qsum) {
+        tbr_destroy(q->tb); free(q->ring_id); free(q->ring_p); free(q->head); free(q->count);
+        free(q->qsum); free(q);
+        return NULL;
+    }
+    return q;
+}
+
+void tbrq_destroy(tbrq_table *q) {
+    if (!q) return;
+    tbr_destroy(q->tb);
+    free(q->ring_id); free(q->ring_p); free(q->head); free(q->count); free(q->qsum); free(q);
+}
+
+/* One WaitAsync (Q:67-134).  Evicted ids (NewestFirst) are appended to evicted[] with
+ * the causing request's index; returns the status. */
+static int tbrq_acquire_one(tbrq_table *q, uint64_t key, int32_t p, int64_t ts_us, int64_t id,
+                            uint64_t cause, int32_t *remaining, int64_t *ev_id, uint64_t *ev_cause,
+                            uint64_t *n_ev, uint64_t max_ev) {
+    *remaining = -1;
+    if (p > q->token_limit) return TBRQ_REJECTED;                           /* Q:70-73 */
+    uint32_t cap = q->ring_cap;
+    uint64_t base = key * cap;
+    if (p == 0 || !(q->count[key] > 0 && q->order == 0)) {                  /* Q:153 */
+        if (tbr_acquire_one(q->tb, key, p, ts_us, remaining)) return TBRQ_GRANTED;
+    }
+    if ((int64_t)q->queue_limit - q->qsum[key] < p) {                       /* Q:92 */
+        if (q->order == 1 && p <= q->queue_limit) {                         /* Q:94-109 */
+            while ((int64_t)q->queue_limit - q->qsum[key] < p) {
+                uint32_t h = q->head[key];
+                if (*n_ev < max_ev) { ev_id[*n_ev] = q->ring_id[base + h]; ev_cause[*n_ev] = cause; }
+                (*n_ev)++;
+                q->qsum[key] -= q->ring_p[base + h];
+                q->head[key] = (h + 1) % cap;
+                q->count[key]--;
+            }
+        } else {
+            return TBRQ_FAILED;                                              /* Q:113 */
+        }
+    }
+    uint32_t tail = (q->head[key] + q->count[key]) % cap;                   /* EnqueueTail */
+    q->ring_id[base + tail] = id;
+    q->ring_p[base + tail] = p;
+    q->count[key]++;
+    q->qsum[key] += p;
+    return TBRQ_QUEUED;
+}
+
+int tbrq_acquire_batch(tbrq_table *q, const uint64_t *keys, const int32_t *permits,
+                       const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
+                       int32_t *remaining, int64_t *ev_id, uint64_t *ev_cause, uint64_t max_ev,
+                       uint64_t *n_ev) {
+    if (tbr_validate(q->tb, keys, permits, ts_us, n)) return -1;
+    *n_ev = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        status[i] = (uint8_t)tbrq_acquire_one(q, keys[i], permits[i], ts_us[i], id_base + (int64_t)i,
+                                              i, &remaining[i], ev_id, ev_cause, n_ev, max_ev);
+    return 0;
+}
+
+/* One replenish tick (Q:237-271) over every key, in key order. */
+int tbrq_refresh(tbrq_table *q, int64_t ts_us, uint64_t *log_key, int64_t *log_id,
+                 int32_t *log_remaining, uint64_t max_log, uint64_t *n_log) {
+    if (ts_us < 0) return -1;
+    *n_log = 0;
+    uint32_t cap = q->ring_cap;
+    for (uint64_t k = 0; k < q->tb->n_keys; ++k) {
+        while (q->count[k] > 0) {
+            uint32_t idx = (q->order == 0) ? q->head[k] : (q->head[k] + q->count[k] - 1) % cap;
+            int32_t rem;
+            if (!tbr_acquire_one(q->tb, k, q->ring_p[k * cap + idx], ts_us, &rem)) break;
+            if (*n_log < max_log) {
+                log_key[*n_log] = k; log_id[*n_log] = q->ring_id[k * cap + idx];
+                log_remaining[*n_log] = rem;
+            }
+            (*n_log)++;
+            q->qsum[k] -= q->ring_p[k * cap + idx];
+            if (q->order == 0) q->head[k] = (q->head[k] + 1) % cap;
+            q->count[k]--;
+        }
+    }
+    return 0;
+}
+
+/* Queue contents of one key, oldest first: returns the entry count. */
+uint32_t tbrq_queue_of(const tbrq_table *q, uint64_t key, int64_t *ids, int32_t *permits, uint32_t max) {
+    uint32_t c = q->count[key], cap = q->ring_cap;
+    for (uint32_t j = 0; j < c && j < max; ++j) {
+        uint32_t idx = (q->head[key] + j) % cap;
+        ids[j] = q->ring_id[key * cap + idx];
+        permits[j] = q->ring_p[key * cap + idx];
+    }
+    return c;
+}
+
+tbr_table *tbrq_bucket_table(tbrq_table *q) { return q->tb; }

@@ -1,0 +1,69 @@
+"""GPU parity of the TokenBucketWithQueue path (tbe_wait_batch / tbe_refresh) against the
+C restatement of the spec (oracle/tb_ref.c tbrq_*), which tests/test_queue_oracle.py ties
+to the Python restatement."""
+import numpy as np
+import pytest
+
+from oracle import cref
+
+pytestmark = pytest.mark.gpu
+
+S_US = 1_760_572_800 * 1_000_000
+
+
+def pair(n_keys, token_limit, tokens, ticks, qlimit, order):
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    eng = QueueingTokenBucketEngine(n_keys, token_limit, tokens, ticks, qlimit, order, device=0)
+    ref = cref.CQueueingTokenBucket(n_keys, token_limit, fill_rate(tokens, ticks), qlimit, order)
+    return eng, ref
+
+
+def check_round(eng, ref, keys, permits, ts, id_base):
+    st, rem, (cause, ids) = eng.wait_batch(keys, permits, ts, id_base)
+    st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, id_base)
+    bad = np.flatnonzero((st != st2) | (rem != rem2))
+    assert bad.size == 0, f"{bad.size} mismatches at {bad[:5]}: {st[bad[:5]]} {rem[bad[:5]]} vs {st2[bad[:5]]} {rem2[bad[:5]]}"
+    assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2)
+    return st
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("n_keys,qlimit,n,rounds", [(40, 4, 3000, 5), (5000, 16, 60000, 4),
+                                                    (1 << 20, 16, 200_000, 3), (7, 0, 2000, 3)])
+def test_wait_and_refresh(engine_lib, gpu, order, n_keys, qlimit, n, rounds):
+    rng = np.random.default_rng(n_keys + 31 * qlimit + order)
+    eng, ref = pair(n_keys, 4, 1, 10_000_000, qlimit, order)
+    t, rid = S_US, 0
+    for _ in range(rounds):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 1, 2, 3, 5], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        check_round(eng, ref, keys, permits, ts, rid)
+        rid += n
+        t += 1_000 + int(rng.integers(0, 3_000_000))
+        k1, i1, r1 = eng.refresh(t)
+        k2, i2, r2 = ref.refresh(t)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    for k in list(range(min(n_keys, 50))):
+        assert eng.queue_of(k) == ref.queue_of(k)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+def test_config_d_shape_small(engine_lib, gpu):
+    # Config D shape: QueueLimit 16, OldestFirst, permits 1, TokenLimit 4, 1 ms batches,
+    # demand >> fill so queues saturate; refresh at every batch boundary.
+    from oracle import trace
+    n_keys, n = 1_000_000, 1 << 20
+    eng, ref = pair(n_keys, 4, 1, 10_000_000, 16, 0)
+    for b in range(4):
+        k, p, ts = trace.make_batch(0x5EED000D, n_keys, b, n, 1_000)
+        st = check_round(eng, ref, k, p, ts, b * n)
+        t_ref = trace.T0_US + (b + 1) * 1_000
+        k1, i1, r1 = eng.refresh(t_ref)
+        k2, i2, r2 = ref.refresh(t_ref)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    assert (st == 2).mean() > 0.05  # queues in use

@@ -1,0 +1,64 @@
+"""TokenBucketWithQueue spec: Python and C restatements agree, plus hand-checked cases."""
+import numpy as np
+import pytest
+
+from oracle import cref
+from oracle.semantics import (NEWEST_FIRST, OLDEST_FIRST, ST_FAILED, ST_GRANTED, ST_QUEUED,
+                              ST_REJECTED, QueueingTokenBucketTable, TokenBucketConfig)
+
+S_US = 1_760_572_800 * 1_000_000
+
+
+def test_oldest_first_hand_case():
+    q = QueueingTokenBucketTable(TokenBucketConfig(4, 1.0), 3, OLDEST_FIRST)
+    out = [q.acquire(1, p, S_US + i, i) for i, p in enumerate([2, 2, 1, 1, 1, 1, 5])]
+    assert [o[0] for o in out] == [ST_GRANTED, ST_GRANTED, ST_QUEUED, ST_QUEUED, ST_QUEUED,
+                                   ST_FAILED, ST_REJECTED]
+    assert out[2][1] == 0 and out[3][1] == -1          # script ran / not called
+    assert q.refresh(S_US + 2_000_000) == [(1, 2, 1), (1, 3, 0)]
+    assert q.queue_of(1) == [(4, 1)]
+
+
+def test_newest_first_evicts_oldest():
+    q = QueueingTokenBucketTable(TokenBucketConfig(2, 1.0), 3, NEWEST_FIRST)
+    out = [q.acquire(1, p, S_US, i) for i, p in enumerate([2, 1, 1, 1, 2])]
+    assert [o[0] for o in out] == [ST_GRANTED, ST_QUEUED, ST_QUEUED, ST_QUEUED, ST_QUEUED]
+    assert out[4][2] == [1, 2]                          # evicted ids, oldest first
+    assert q.queue_of(1) == [(3, 1), (4, 2)]
+    # NewestFirst drains from the tail (DQ PeekTail/DequeueTail)
+    assert q.refresh(S_US + 2_000_000) == [(1, 4, 0)]
+    assert q.queue_of(1) == [(3, 1)]
+
+
+def random_ops(seed, n_keys, rounds, n):
+    rng = np.random.default_rng(seed)
+    t = S_US
+    for r in range(rounds):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 1, 2, 3, 9], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 300_000, n))).astype(np.int64)
+        t += 300_000
+        yield keys, permits, ts, t
+        t += int(rng.integers(0, 400_000))
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+@pytest.mark.parametrize("qlimit", [0, 1, 4, 16])
+def test_python_vs_c(oracle_lib, order, qlimit):
+    n_keys = 50
+    cfg = TokenBucketConfig.from_options(5, 2, 10_000_000)
+    py = QueueingTokenBucketTable(cfg, qlimit, order)
+    c = cref.CQueueingTokenBucket(n_keys, cfg.token_limit, cfg.fill_rate, qlimit, order)
+    rid = 0
+    for keys, permits, ts, t_refresh in random_ops(qlimit * 7 + order, n_keys, 6, 2000):
+        exp = [py.acquire(int(k), int(p), int(s), rid + i) for i, (k, p, s) in enumerate(zip(keys, permits, ts))]
+        st, rem, ev_cause, ev_id = c.acquire_batch(keys, permits, ts, rid)
+        assert st.tolist() == [e[0] for e in exp]
+        assert rem.tolist() == [e[1] for e in exp]
+        exp_ev = [(i, x) for i, e in enumerate(exp) for x in e[2]]
+        assert list(zip(ev_cause.tolist(), ev_id.tolist())) == exp_ev
+        rid += len(keys)
+        lk, lid, lrem = c.refresh(t_refresh)
+        assert list(zip(lk.tolist(), lid.tolist(), lrem.tolist())) == py.refresh(t_refresh)
+    for k in range(n_keys):
+        assert c.queue_of(k) == py.queue_of(k)

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs (gpurun_out/pmc_*/run_counter_collection.csv) per kernel:
+average counter value per dispatch, plus HBM bytes per launch with the gfx950 correction
+from MI355X_MICROARCH.md (FETCH_SIZE counts half of a wide coalesced read: x2; both
+counters are in KiB).  Writes profiles/pmc_summary.json when --write is given."""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAGE = {"k_hist": "hist", "k_colscan": "colscan", "k_scatter": "scatter", "k_bounds": "bounds",
+         "k_fold": "fold", "k_fold_q": "fold", "k_unscatter": "unscatter", "k_drain": "drain"}
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "")
+    m = re.search(r"(k_\w+)", n)
+    base = m.group(1) if m else n.split("(")[0]
+    t = re.search(r"k_\w+<([^>]*)>", n)
+    return base + (f"<{t.group(1)}>" if t else "")
+
+
+def main():
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc_*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k in sorted(agg):
+        if not k.startswith("k_"):
+            continue
+        d = {c: sum(v) / len(v) for c, v in agg[k].items()}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+        out[k] = d
+        print(k, " ".join(f"{c}={v:.4g}" for c, v in d.items()))
+    stages = {}
+    for k, d in out.items():
+        st = STAGE.get(k.split("<")[0])
+        if st and "hbm_bytes_per_launch" in d:
+            e = stages.setdefault(st, {"hbm_bytes_per_launch": 0.0, "kernels": []})
+            e["kernels"].append(k)
+            e["hbm_bytes_per_launch"] += d["hbm_bytes_per_launch"]
+    for st, e in stages.items():   # average over the kernels (passes) that make up a stage
+        e["hbm_bytes_per_launch"] /= len(e["kernels"])
+    if "--write" in sys.argv:
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
+            json.dump({"note": "per-launch averages; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
+                               "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section)",
+                       **stages, "kernels": out}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
