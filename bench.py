@@ -127,7 +127,7 @@ def main():
     if stages and sum(stages.values()) > 0:
         passes = eng_passes(keys_local)
         launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                    "unscatter": passes}
+                    "unscatter": passes}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
         alg_bytes = algorithmic_bytes(name, n, keys_local, passes)
@@ -180,20 +180,22 @@ def eng_passes(n_keys: int) -> int:
 
 
 def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int) -> int:
-    """Bytes a launch of `stage` must move at minimum (DESIGN.md "Algorithmic bytes")."""
+    """Bytes one launch of `stage` must move at minimum for its function,
+    averaged over the passes where a stage runs once per pass."""
     if stage == "fold":
         # sorted records (key 4 + permits 4 + ts 8) + packed reply 4 per request, plus the
-        # touched table rows (16 B read + 16 B written per distinct key in the batch).
+        # table rows of the distinct keys in the batch (16 B read + 16 B written each).
         u = n_keys * (1.0 - np.exp(-n / n_keys))
         return int(n * 20 + u * 32)
     if stage == "scatter":
-        return n * (36 if passes == 1 else 34)   # averaged over passes: 20 in/16 out, 16/16
+        # pass 0 reads key 8 + permits 4 + ts 8, later passes key 4 + 4 + 8; every pass
+        # writes key 4 + permits 4 + ts 8 and its permutation 4
+        return int(n * ((20 + 16 * (passes - 1)) / passes + 20))
     if stage == "hist":
-        return n * 6                              # 8 B keys (pass 0), 4 B after
+        return int(n * (8 + 4 * (passes - 1)) / passes)
     if stage == "unscatter":
-        return n * 14                             # 12 B (inner passes) / 17 B (final)
-    if stage == "bounds":
-        return n * 4
+        # perm 4 + gathered reply 4 + written 4 (inner passes) or 5 (final: u8 + i32)
+        return int(n * (12 * (passes - 1) + 13) / passes)
     return n * 4
 
 

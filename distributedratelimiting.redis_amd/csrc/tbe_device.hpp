@@ -145,6 +145,15 @@ __device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t
 }
 
 // ----------------------------------------------------------------- wave / block helpers
+// XCD-aware block -> tile remap (cdna_hip_programming.md T1, the bijective form): blocks
+// b and b+8 share an XCD (round-robin dispatch), so give each XCD a contiguous range of
+// tiles.  Consecutive tiles write adjacent pieces of the same digit runs; on one XCD
+// their partial lines merge in that XCD's L2.  Placement only changes speed.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t nblk) {
+    const uint32_t xcd = b & 7u, q = nblk >> 3, r = nblk & 7u;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const int lane = threadIdx.x & 63;
     return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -176,73 +185,98 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wsum, 
     return pre + v - x;
 }
 
-// LDS needed by rank_tile<BLOCK, ITEMS>.
+// Stable local ranking of a tile of BLOCK*ITEMS elements by an 8-bit digit.
+// Element e = it*BLOCK + threadIdx.x (striped, so global loads coalesce); tile order is
+// e order.
+//   A. every wave ballot-matches the 8 digit bits of each of its ITEMS rounds: in-wave
+//      rank, and the wave's count per digit, written to cnt[it][wave][digit] (u16);
+//   B. the 256 digit columns of cnt (ITEMS*W entries each, in tile order) are scanned
+//      in place to exclusive prefixes -- two threads per column when BLOCK = 512 --
+//      and a block scan of the column totals gives lstart[digit];
+//   C. lpos = lstart[d] + cnt[it][wave][d] + in-wave rank.
+// `cnt` needs ITEMS*W*256*2 bytes of LDS; callers alias it with their staging buffer
+// (it is dead after C).  Four barriers per tile.
 template <int BLOCK>
 struct RankLds {
     static constexpr int W = BLOCK / 64;
-    uint16_t wcnt[2][W][kDigits];   // per-wave digit counts, double-buffered by round
-    uint32_t run[kDigits];          // running per-digit count over the rounds so far
-    uint32_t lstart[kDigits];       // first tile position of each digit
+    static constexpr int PARTS = BLOCK / kDigits;   // threads per digit column
+    uint32_t lstart[kDigits];
+    uint32_t part[PARTS][kDigits];                  // per-segment column sums
     uint32_t wsum[W];
 };
 
-// Stable local ranking of a tile of BLOCK*ITEMS elements by an 8-bit digit.
-// Element e = it*BLOCK + threadIdx.x (striped, so global loads coalesce); tile order is
-// e order, i.e. round `it` by round.  Per round: every wave ballot-matches the 8 digit
-// bits (in-wave rank + count), one thread per digit scans the wave counts on top of the
-// running count, each element reads its prefix.  Afterwards lstart = exclusive scan of
-// the digit totals and lpos = lstart[d] + rank is the element's position in the tile
-// sorted stably by digit.  Two barriers per round (the count buffer alternates).
 template <int BLOCK, int ITEMS>
-__device__ __forceinline__ void rank_tile(const uint32_t (&dig)[ITEMS], int nvalid,
-                                          RankLds<BLOCK> &L, uint32_t (&lpos)[ITEMS]) {
+__device__ __forceinline__ void rank_tile(const uint32_t (&key)[ITEMS], int shift, int nvalid,
+                                          RankLds<BLOCK> &L, uint16_t *cnt,
+                                          uint32_t (&lpos)[ITEMS]) {
+#define TBE_DIG(it) ((key[it] >> shift) & (kDigits - 1))
     constexpr int W = BLOCK / 64;
-    static_assert(BLOCK >= kDigits, "one digit column per thread");
+    constexpr int COL = ITEMS * W;                      // entries per digit column
+    static_assert(BLOCK % kDigits == 0, "whole digit columns per thread group");
     const int tid = threadIdx.x, w = tid >> 6;
-    uint32_t *z = reinterpret_cast<uint32_t *>(&L.wcnt[0][0][0]);
-    for (int i = tid; i < 2 * W * kDigits / 2; i += BLOCK) z[i] = 0;
-    if (tid < kDigits) L.run[tid] = 0;
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(cnt);
+        const uint4 zero = {0u, 0u, 0u, 0u};
+        for (int i = tid; i < COL * kDigits * 2 / 16; i += BLOCK) z[i] = zero;
+    }
     __syncthreads();
     const uint64_t lt = lanemask_lt();
-    uint32_t rank[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-        const int buf = it & 1;
         const int e = it * BLOCK + tid;
         const bool valid = e < nvalid;
+        const uint32_t dg = TBE_DIG(it);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < kDigitBits; ++b) {
-            const bool bit = (dig[it] >> b) & 1u;
+            const bool bit = (dg >> b) & 1u;
             const uint64_t m = __ballot(bit);
             peers &= bit ? m : ~m;
         }
-        const uint32_t r = (uint32_t)__popcll(peers & lt);
-        if (valid && r == 0) L.wcnt[buf][w][dig[it]] = (uint16_t)__popcll(peers);
-        __syncthreads();
-        if (tid < kDigits) {
-            uint32_t s = L.run[tid];
+        lpos[it] = (uint32_t)__popcll(peers & lt);   // in-wave rank for now
+        if (valid && lpos[it] == 0) cnt[(it * W + w) * kDigits + dg] = (uint16_t)__popcll(peers);
+    }
+    __syncthreads();
+    // B: column scans.  Entry j of column d is cnt[j*256 + d], j = it*W + wave; PARTS
+    // threads share a column, each scanning one contiguous segment.
+    constexpr int PARTS = BLOCK / kDigits;
+    static_assert(COL % PARTS == 0, "column splits evenly");
+    constexpr int SEG = COL / PARTS;
+    const int d = tid & (kDigits - 1);
+    const int part = tid / kDigits;
+    uint32_t s = 0;
+#pragma unroll 8
+    for (int j = part * SEG; j < (part + 1) * SEG; ++j) {
+        const uint32_t c = cnt[j * kDigits + d];
+        cnt[j * kDigits + d] = (uint16_t)s;
+        s += c;
+    }
+    L.part[part][d] = s;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
 #pragma unroll
-            for (int ww = 0; ww < W; ++ww) {
-                const uint32_t c = L.wcnt[buf][ww][tid];
-                L.wcnt[buf][ww][tid] = (uint16_t)s;   // exclusive prefix within the tile
-                L.wcnt[buf ^ 1][ww][tid] = 0;         // clear the other buffer for round it+1
-                s += c;
-            }
-            L.run[tid] = s;
-        }
-        __syncthreads();
-        rank[it] = valid ? (uint32_t)L.wcnt[buf][w][dig[it]] + r : 0u;
+    for (int q = 0; q < PARTS; ++q) {
+        const uint32_t v = L.part[q][d];
+        off += (q < part) ? v : 0u;
+        total += v;
+    }
+    if (part > 0) {
+#pragma unroll 8
+        for (int j = part * SEG; j < (part + 1) * SEG; ++j)
+            cnt[j * kDigits + d] = (uint16_t)(cnt[j * kDigits + d] + off);
     }
     {
-        uint32_t total;
-        const uint32_t x = (tid < kDigits) ? L.run[tid] : 0u;
-        const uint32_t ex = block_excl_scan<BLOCK>(x, L.wsum, &total);
-        if (tid < kDigits) L.lstart[tid] = ex;
+        // exclusive scan of the column totals, contributed by the part-0 thread of each
+        // column (threads 0..255, in digit order; everyone else adds 0)
+        uint32_t all;
+        const uint32_t ex = block_excl_scan<BLOCK>(part == 0 ? total : 0u, L.wsum, &all);
+        if (part == 0) L.lstart[d] = ex;
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < ITEMS; ++it) lpos[it] = L.lstart[dig[it]] + rank[it];
+    for (int it = 0; it < ITEMS; ++it)
+        lpos[it] += L.lstart[TBE_DIG(it)] + cnt[(it * W + w) * kDigits + TBE_DIG(it)];
+#undef TBE_DIG
 }
 
 }  // namespace tbe

@@ -43,8 +43,8 @@ using namespace tbe;
 
 namespace {
 
-constexpr int kPartBlock = 512;                        // partition workgroup (8 waves)
-constexpr int kPartItems = 16;                         // elements per thread per tile
+constexpr int kPartBlock = 1024;                       // partition workgroup (16 waves)
+constexpr int kPartItems = 8;                          // elements per thread per tile
 constexpr int kTile = kPartBlock * kPartItems;         // 8192 requests per tile
 constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
 constexpr int kMaxHistBlocks = 1024;
@@ -149,25 +149,27 @@ __device__ __forceinline__ void tile_offsets(uint32_t tile, uint32_t tiles_per_b
 // IDX: also carry each request's arrival index (queueing kind: it becomes the request
 // id of a queued entry); pass 0 generates it (iin == nullptr).
 template <typename KeyIn, bool IDX>
-__global__ __launch_bounds__(kPartBlock, 4) void k_scatter(
+__global__ __launch_bounds__(kPartBlock) void k_scatter(
     const KeyIn *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint32_t *__restrict__ iin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
     const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
     uint32_t tiles_per_blk, uint32_t *__restrict__ kout, int32_t *__restrict__ pout,
-    int64_t *__restrict__ tout, uint32_t *__restrict__ iout, uint32_t *__restrict__ err,
-    int validate) {
+    int64_t *__restrict__ tout, uint32_t *__restrict__ iout, uint32_t *__restrict__ perm,
+    uint32_t *__restrict__ err, int validate) {
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
+    // staging buffer; during ranking it holds the per-(round, wave, digit) counts
     __shared__ uint64_t stage[kTile];
+    static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
     const int tid = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t base = (uint64_t)tile * kTile;
     const int nvalid = (int)min<uint64_t>(kTile, n - base);
 
     // Issue every load of the tile up front; the payload waits in registers while the
     // ranks are computed.
-    uint32_t key[kPartItems], dig[kPartItems], lpos[kPartItems];
+    uint32_t key[kPartItems], lpos[kPartItems];
     int32_t pm[kPartItems];
     int64_t tv[kPartItems];
 #pragma unroll
@@ -177,18 +179,21 @@ __global__ __launch_bounds__(kPartBlock, 4) void k_scatter(
         key[it] = v ? (uint32_t)kin[base + e] : 0u;
         pm[it] = v ? pin[base + e] : 0;
         tv[it] = v ? tin[base + e] : 0;
-        dig[it] = (key[it] >> shift) & (kDigits - 1);
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
-    rank_tile<kPartBlock, kPartItems>(dig, nvalid, L, lpos);
+    rank_tile<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint16_t *>(stage), lpos);
+    __syncthreads();   // the counts in `stage` are dead from here on
 
     bool bad = false;
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int e = it * kPartBlock + tid;
         if (e < nvalid) {
+            const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             bad |= validate && (pm[it] < 0 || tv[it] < 0);
             stage[lpos[it]] = ((uint64_t)key[it] << 32) | (uint32_t)pm[it];
+            // where input element e goes: the inverse pass is a plain gather through it
+            perm[base + e] = goff[d] + lpos[it] - L.lstart[d];
         }
     }
     __syncthreads();
@@ -437,58 +442,52 @@ __global__ __launch_bounds__(kFoldBlock, 2) void k_fold(
         if (dense || (dirty[j >> 5] & (1u << (j & 31)))) rows[j] = Slot{sv[j], ts_of_tpack(stp[j])};
 }
 
-// Inverse of one k_scatter pass: recompute the tile's local ranks from the pass-input
-// keys, gather the replies from the pass-output positions, store them in pass-input
-// order.  FINAL = pass 0: unpack into granted (u8) / remaining (i32).
-// Packed replies of the queueing kind: bits 31-30 TBE_WAIT_* status, bits 29-0
-// trunc(new_v), 0x3FFFFFFF when the script was not called.
+// Inverse of one k_scatter pass: out[i] = in[perm[i]] with perm the positions that pass
+// wrote (runs of ~32 consecutive positions per digit and tile, so the gather coalesces).
+// FINAL: unpack into granted/status (u8) and remaining (i32) in arrival order.
+// WAIT: queueing-kind reply packing (see pack_wait).
 constexpr uint32_t kRemNone = 0x3FFFFFFFu;
 __device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, uint32_t rem) {
     return (status << 30) | (evaluated ? (rem & kRemNone) : kRemNone);
 }
 
-template <typename KeyIn, bool FINAL, bool WAIT>
-__global__ __launch_bounds__(kPartBlock) void k_unscatter(
-    const KeyIn *__restrict__ kin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
-    const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
-    uint32_t tiles_per_blk, const uint32_t *__restrict__ res_in, uint32_t *__restrict__ res_out,
-    uint8_t *__restrict__ granted, int32_t *__restrict__ remaining) {
-    __shared__ RankLds<kPartBlock> L;
-    __shared__ uint32_t goff[kDigits];
-
+template <bool FINAL, bool WAIT>
+__global__ __launch_bounds__(kPartBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
+                                                          const uint32_t *__restrict__ res_in,
+                                                          uint32_t *__restrict__ res_out,
+                                                          uint8_t *__restrict__ granted,
+                                                          int32_t *__restrict__ remaining) {
+    // One workgroup per partition tile (same tiles and XCD mapping as k_scatter): the
+    // tile's 8192 gathers land in its 256 digit runs, which stay in this CU's L1 / XCD L2.
     const int tid = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t base = (uint64_t)tile * kTile;
     const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    uint32_t dig[kPartItems], lpos[kPartItems];
+    uint32_t pv[kPartItems], r[kPartItems];
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int e = it * kPartBlock + tid;
-        const uint32_t k = (e < nvalid) ? (uint32_t)kin[base + e] : 0u;
-        dig[it] = (k >> shift) & (kDigits - 1);
-    }
-    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
-    rank_tile<kPartBlock, kPartItems>(dig, nvalid, L, lpos);
-    uint32_t r[kPartItems];
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
-        r[it] = (e < nvalid) ? res_in[goff[dig[it]] + lpos[it] - L.lstart[dig[it]]] : 0u;
+        pv[it] = (e < nvalid) ? perm[base + e] : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int e = it * kPartBlock + tid;
-        if (e < nvalid) {
-            if (FINAL && WAIT) {
-                granted[base + e] = (uint8_t)(r[it] >> 30);
-                const uint32_t rem = r[it] & kRemNone;
-                remaining[base + e] = (rem == kRemNone) ? -1 : (int32_t)rem;
-            } else if (FINAL) {
-                granted[base + e] = (uint8_t)(r[it] >> 31);
-                remaining[base + e] = (int32_t)(r[it] & 0x7FFFFFFFu);
-            } else {
-                res_out[base + e] = r[it];
-            }
+        r[it] = (e < nvalid) ? res_in[pv[it]] : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
+        if (e >= nvalid) continue;
+        const uint64_t i = base + e;
+        if (FINAL && WAIT) {
+            granted[i] = (uint8_t)(r[it] >> 30);
+            const uint32_t rem = r[it] & kRemNone;
+            remaining[i] = (rem == kRemNone) ? -1 : (int32_t)rem;
+        } else if (FINAL) {
+            granted[i] = (uint8_t)(r[it] >> 31);
+            remaining[i] = (int32_t)(r[it] & 0x7FFFFFFFu);
+        } else {
+            res_out[i] = r[it];
         }
     }
 }
@@ -732,6 +731,7 @@ struct PassBufs {
     int32_t *permits = nullptr;
     int64_t *ts = nullptr;
     uint32_t *idx = nullptr;     // arrival index (queueing kind only)
+    uint32_t *perm = nullptr;    // output position of each input element of the pass
     uint32_t *tileprefix = nullptr;
     uint32_t *blockprefix = nullptr;
     uint32_t *digit_total = nullptr;
@@ -827,6 +827,7 @@ void free_workspace(tbe_engine *e) {
         dfree(pb.permits);
         dfree(pb.ts);
         dfree(pb.idx);
+        dfree(pb.perm);
         dfree(pb.tileprefix);
         dfree(pb.blockprefix);
         dfree(pb.digit_total);
@@ -861,6 +862,7 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.keys, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
         HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
+        HIP_TRY(e, hipMalloc(&pb.perm, cap * sizeof(uint32_t)));
         if (e->cfg.kind == TBE_KIND_QUEUEING) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
@@ -943,21 +945,21 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         if (p == 0 && !wait)
             k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, st>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, e->err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.perm, e->err, 1);
         else if (p == 0)
             k_scatter<uint64_t, true><<<ntiles, kPartBlock, 0, st>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, e->err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, out.perm, e->err, 1);
         else if (!wait)
             k_scatter<uint32_t, false><<<ntiles, kPartBlock, 0, st>>>(
                 e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, nullptr, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits,
-                out.ts, nullptr, e->err, 0);
+                out.ts, nullptr, out.perm, e->err, 0);
         else
             k_scatter<uint32_t, true><<<ntiles, kPartBlock, 0, st>>>(
                 e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, e->pass[p - 1].idx,
                 n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys,
-                out.permits, out.ts, out.idx, e->err, 0);
+                out.permits, out.ts, out.idx, out.perm, e->err, 0);
         stage_end(e, ST_SCATTER, st);
     }
     const PassBufs &sorted = e->pass[e->passes - 1];
@@ -982,20 +984,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     stage_begin(e, ST_UNSCATTER, st);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        const PassBufs &pb = e->pass[p];
-        k_unscatter<uint32_t, false, false><<<ntiles, kPartBlock, 0, st>>>(
-            e->pass[p - 1].keys, n, e->r_bits + kDigitBits * p, pb.tileprefix, pb.blockprefix,
-            pb.digit_total, tpb, e->res[cur], e->res[cur ^ 1], nullptr, nullptr);
+        k_unscatter<false, false><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[p].perm, e->res[cur],
+                                                                e->res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
     if (wait)
-        k_unscatter<uint64_t, true, true><<<ntiles, kPartBlock, 0, st>>>(
-            keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix,
-            e->pass[0].digit_total, tpb, e->res[cur], nullptr, granted, remaining);
+        k_unscatter<true, true><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+                                                              nullptr, granted, remaining);
     else
-        k_unscatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
-            keys, n, e->r_bits, e->pass[0].tileprefix, e->pass[0].blockprefix,
-            e->pass[0].digit_total, tpb, e->res[cur], nullptr, granted, remaining);
+        k_unscatter<true, false><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+                                                               nullptr, granted, remaining);
     stage_end(e, ST_UNSCATTER, st);
     k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
     HIP_TRY(e, hipGetLastError());
