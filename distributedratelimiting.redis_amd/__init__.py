@@ -6,7 +6,8 @@ Python package only binds that ABI (``_capi``) and moves buffers (``engine``).
 Importing it does not load the shared library; the first engine does, and fails
 loudly if ``libtbe.so`` has not been built (see ``build.py``).
 """
-from .engine import QueueingTokenBucketEngine, TokenBucketEngine, fill_rate  # noqa: F401
+from .engine import (ApproximateEngine, QueueingTokenBucketEngine, TokenBucketEngine,  # noqa: F401
+                     fill_rate)
 from ._capi import TbeError  # noqa: F401
 
-__all__ = ["TokenBucketEngine", "QueueingTokenBucketEngine", "TbeError", "fill_rate"]
+__all__ = ["TokenBucketEngine", "QueueingTokenBucketEngine", "ApproximateEngine", "TbeError", "fill_rate"]

@@ -36,6 +36,7 @@
 
 #include "../../include/tbe.h"
 #include "tbe_device.hpp"
+#include "tbe_numfmt.hpp"
 
 #pragma clang fp contract(off)
 
@@ -148,7 +149,7 @@ __device__ __forceinline__ void tile_offsets(uint32_t tile, uint32_t tiles_per_b
 // each digit's run leaves the workgroup as one contiguous, coalesced write.
 // IDX: also carry each request's arrival index (queueing kind: it becomes the request
 // id of a queued entry); pass 0 generates it (iin == nullptr).
-template <typename KeyIn, bool IDX>
+template <typename KeyIn, bool IDX, bool TS = true>
 __global__ __launch_bounds__(kPartBlock) void k_scatter(
     const KeyIn *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint32_t *__restrict__ iin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
         const bool v = e < nvalid;
         key[it] = v ? (uint32_t)kin[base + e] : 0u;
         pm[it] = v ? pin[base + e] : 0;
-        tv[it] = v ? tin[base + e] : 0;
+        tv[it] = (v && TS) ? tin[base + e] : 0;
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
     rank_tile<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint16_t *>(stage), lpos);
@@ -210,17 +211,19 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
             pout[gpos[it]] = (int32_t)(uint32_t)s;
         }
     }
-    __syncthreads();
+    if (TS) {
+        __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
-        if (e < nvalid) stage[lpos[it]] = (uint64_t)tv[it];
-    }
-    __syncthreads();
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            if (e < nvalid) stage[lpos[it]] = (uint64_t)tv[it];
+        }
+        __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int j = it * kPartBlock + tid;
-        if (j < nvalid) tout[gpos[it]] = (int64_t)stage[j];
+        for (int it = 0; it < kPartItems; ++it) {
+            const int j = it * kPartBlock + tid;
+            if (j < nvalid) tout[gpos[it]] = (int64_t)stage[j];
+        }
     }
     if (IDX) {
         uint32_t *stage32 = reinterpret_cast<uint32_t *>(stage);
@@ -713,6 +716,297 @@ __global__ __launch_bounds__(kBlock) void k_drain(
     }
 }
 
+// ----------------------------------------------------------------------------- approximate kind
+// One client's local tier per key (A:36-37, A:84-214), the global tier replica per key
+// (the sync script's Redis hash {v, p, t}, A:241-270) and the per-key queue ring.
+struct ALocal {
+    int32_t cap;     // (int)Math.Ceiling((TokenLimit - _globalThrottleScore) / _instanceCountEstimate)
+    int32_t local;   // _localThrottleScore
+    int32_t qsum;    // _queueCount
+    uint32_t hc;     // ring head (bits 0-15) | count (bits 16-31)
+};
+struct AClient {
+    double est;      // _instanceCountEstimate
+    int32_t global;  // _globalThrottleScore
+    int32_t pad;
+};
+struct AParams {
+    int32_t token_limit;
+    int32_t queue_limit;
+    int32_t order;          // 0 OldestFirst, 1 NewestFirst
+    uint32_t cap;           // ring entries per key
+    int64_t id_base;
+    int32_t wait;           // 1: WaitAsyncCore (A:116-183), 0: AcquireCore (A:84-113)
+    int32_t pad;
+    double decay_rate;      // FillRatePerSecond (A:224 decay_rate)
+    double period_s;        // ReplenishmentPeriod.TotalSeconds (A:443)
+};
+constexpr int64_t kApproxTtlMs = 86400LL * 1000;   // EXPIRE 86400 (A:268)
+
+__device__ __forceinline__ int32_t wrap_sub(int32_t a, int32_t b) {
+    return (int32_t)((uint32_t)a - (uint32_t)b);
+}
+__device__ __forceinline__ int32_t avail_of(const ALocal &a) {       // A:37
+    const int32_t d = wrap_sub(a.cap, a.local);
+    return d > 0 ? d : 0;
+}
+// C# (int)double on x64: truncation; NaN and out-of-range give int.MinValue.
+__device__ __forceinline__ int32_t dotnet_to_int(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int32_t)x;
+}
+
+// WaitAsyncCore / AcquireCore of one client for every request of one bucket, per key in
+// arrival order (same bucket/chunk/round structure as k_fold; no timestamps: the local
+// tier never reads the clock).  Reply: pack_wait(status, true, AvailableTokens after).
+__global__ __launch_bounds__(kFoldBlock) void k_fold_a(
+    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
+    const uint32_t *__restrict__ sidx, const uint32_t *__restrict__ bstart, int r_bits,
+    uint64_t n_keys, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring, AParams A,
+    uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err) {
+    __shared__ ALocal sl[kMaxRows];
+    __shared__ uint32_t own[kMaxRows];
+    __shared__ uint32_t rbuf[kFoldChunk];
+    __shared__ uint32_t loaded[kMaxRows / 32];
+    __shared__ uint32_t dirty[kMaxRows / 32];
+
+    if (*err) return;
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) return;
+    const uint32_t R = 1u << r_bits;
+    const uint32_t rmask = R - 1;
+    const uint64_t row0 = (uint64_t)b << r_bits;
+    const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
+    ALocal *__restrict__ rows = alocal + row0;
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
+        loaded[j] = 0;
+        dirty[j] = 0;
+    }
+    for (uint32_t c = s; c < e; c += kFoldChunk) {
+        for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
+        uint32_t kl[kFoldPer], ai[kFoldPer];
+        int32_t pm[kFoldPer];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            kl[r] = 0; pm[r] = 0; ai[r] = 0;
+            if (q < e) {
+                kl[r] = skeys[q] & rmask;
+                pm[r] = sperm[q];
+                ai[r] = sidx[q];
+                pend |= 1u << r;
+            }
+        }
+        __syncthreads();
+        uint32_t mine = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            if (pend & (1u << r)) {
+                const uint32_t bit = 1u << (kl[r] & 31);
+                if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
+            }
+        }
+        {
+            ALocal tmp[kFoldPer];
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r)
+                if (mine & (1u << r)) tmp[r] = rows[kl[r]];
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r)
+                if (mine & (1u << r)) sl[kl[r]] = tmp[r];
+        }
+        __syncthreads();
+        for (uint32_t round = 1;; ++round) {
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r)
+                if (pend & (1u << r))
+                    atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r) {
+                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid));
+                if (!((pend & (1u << r)) && own[kl[r]] == tag)) continue;
+                pend &= ~(1u << r);
+                ALocal a = sl[kl[r]];
+                const int32_t p = pm[r];
+                uint32_t status;
+                bool modified = false, evaluated = true;
+                const int32_t avail = avail_of(a);
+                if (p > A.token_limit) {                                   // A:87-90 / A:119-122
+                    status = TBE_WAIT_REJECTED;
+                    evaluated = false;
+                } else if (p == 0) {                                       // A:93-102 / A:127-130
+                    status = (avail > 0) ? TBE_WAIT_GRANTED : TBE_WAIT_FAILED;
+                } else if (avail >= p && avail != 0 && (a.qsum == 0 || A.order == 1)) {  // A:191-209
+                    a.local = (int32_t)((uint32_t)a.local + (uint32_t)p);
+                    modified = true;
+                    status = TBE_WAIT_GRANTED;
+                } else if (!A.wait) {
+                    status = TBE_WAIT_FAILED;                              // A:111
+                } else {
+                    uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
+                    uint64_t *__restrict__ kr = ring + (row0 + kl[r]) * (uint64_t)A.cap;
+                    bool fail = false;
+                    if ((int64_t)A.queue_limit - a.qsum < p) {             // A:141
+                        if (A.order == 1 && p <= A.queue_limit) {          // A:143-158
+                            while ((int64_t)A.queue_limit - a.qsum < p) {
+                                const uint64_t ent = kr[head];
+                                const uint32_t at = atomicAdd(ev_count, 1u);
+                                if (at < ev_cap) {
+                                    ev_cause[at] = ai[r];
+                                    ev_id[at] = (int64_t)(ent >> 16);
+                                }
+                                a.qsum -= (int32_t)(ent & 0xFFFFu);
+                                head = (head + 1 == A.cap) ? 0 : head + 1;
+                                --cnt;
+                            }
+                        } else {
+                            fail = true;                                   // A:159-163
+                        }
+                    }
+                    if (fail) {
+                        status = TBE_WAIT_FAILED;
+                    } else {                                               // A:166-181
+                        uint32_t tail = head + cnt;
+                        if (tail >= A.cap) tail -= A.cap;
+                        kr[tail] = ((uint64_t)(A.id_base + ai[r]) << 16) | (uint32_t)p;
+                        ++cnt;
+                        a.qsum += p;
+                        status = TBE_WAIT_QUEUED;
+                    }
+                    a.hc = (head & 0xFFFFu) | (cnt << 16);
+                    modified = true;
+                }
+                rbuf[r * kFoldBlock + tid] = pack_wait(status, evaluated, (uint32_t)avail_of(a));
+                if (modified) {
+                    sl[kl[r]] = a;
+                    atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                }
+            }
+            if (!__syncthreads_or(pend != 0)) break;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            if (q < e) res[q] = rbuf[r * kFoldBlock + tid];
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < nrows; j += kFoldBlock)
+        if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = sl[j];
+}
+
+// A:430-435: count = _localThrottleScore; _localThrottleScore = 0, for every key.
+__global__ __launch_bounds__(kBlock) void k_approx_collect(uint64_t n_keys, ALocal *__restrict__ alocal,
+                                                           int32_t *__restrict__ counts) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride) {
+        counts[k] = alocal[k].local;
+        alocal[k].local = 0;
+    }
+}
+
+// One refresh epoch (A:412-508) for every key: replay the n_clients sync-script calls
+// (A:241-270) in client order, client r at ts + r*stagger with count all[r][k], on this
+// engine's replica of the global tier (every engine replays the same calls, so the
+// replicas stay bit-identical); take client `my`'s reply (A:440-443: (int)v', and the
+// period through Lua "%.14g" and double.Parse); then drain the queue (A:462-501).
+__global__ __launch_bounds__(kBlock) void k_approx_sync(
+    uint64_t n_keys, ALocal *__restrict__ alocal, AClient *__restrict__ aclient,
+    double *__restrict__ gv, double *__restrict__ gp, int64_t *__restrict__ gt,
+    const uint64_t *__restrict__ ring, AParams A, const int32_t *__restrict__ all_counts,
+    uint32_t n_clients, uint32_t my, int64_t ts_us, int64_t stagger_us,
+    uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
+    uint32_t *__restrict__ log_count, uint32_t log_cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride) {
+        double v = gv[k], p = gp[k];
+        int64_t t = gt[k];
+        int32_t my_global = 0;
+        double my_period = 0.0;
+        for (uint32_t r = 0; r < n_clients; ++r) {
+            const int64_t ts = ts_us + (int64_t)r * stagger_us;
+            const ReqTime rq = req_time(ts);                                  // A:241-242
+            const bool present = (t != kAbsent) && !(rq.ms > t / 1000 + kApproxTtlMs);
+            const double pv = present ? v : 0.0;                              // A:247-252
+            const double pp = present ? p : 0.0;
+            const double pt = present ? new_t_of(t) : rq.new_t;
+            const double dt = lua_max(0.0, rq.new_t - pt);                    // A:255
+            const double decay = dt * A.decay_rate;
+            const double nv = lua_max(0.0, pv - decay) + (double)all_counts[(uint64_t)r * n_keys + k];  // A:258
+            const double a8 = pp * 0.8;                                       // A:262
+            const double b2 = dt * 0.2;
+            const double np = a8 + b2;
+            v = nv;                                                           // A:265
+            p = np;
+            t = ts;
+            if (r == my) {
+                my_global = (int32_t)(int64_t)nv;                             // A:270 -> A:441
+                my_period = round_trip_14g(np);                               // A:270 -> A:442
+            }
+        }
+        gv[k] = v;
+        gp[k] = p;
+        gt[k] = t;
+        // A:443: Math.Max(1, Math.Round(P / period)); P / 0 = +inf
+        const double q = A.period_s / my_period;
+        const double rnd = __builtin_rint(q);
+        const double est = (rnd != rnd) ? rnd : (rnd > 1.0 ? rnd : 1.0);
+        AClient ac;
+        ac.est = est;
+        ac.global = my_global;
+        ac.pad = 0;
+        aclient[k] = ac;
+        ALocal a = alocal[k];
+        const double lim = (double)wrap_sub(A.token_limit, my_global) / est;
+        a.cap = dotnet_to_int(__builtin_ceil(lim));
+        // drain (A:467-501)
+        uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16, seq = 0;
+        const uint64_t *__restrict__ kr = ring + k * (uint64_t)A.cap;
+        while (cnt > 0) {
+            uint32_t idx = head;
+            if (A.order == 1) {
+                idx = head + cnt - 1;
+                if (idx >= A.cap) idx -= A.cap;
+            }
+            const uint64_t ent = kr[idx];
+            const int32_t c = (int32_t)(ent & 0xFFFFu);
+            if (avail_of(a) < c) break;
+            a.qsum -= c;
+            a.local = (int32_t)((uint32_t)a.local + (uint32_t)c);
+            if (A.order == 0) head = (head + 1 == A.cap) ? 0 : head + 1;
+            --cnt;
+            const uint32_t at = atomicAdd(log_count, 1u);
+            if (at < log_cap) {
+                log_keyseq[at] = (k << 16) | seq;
+                log_id[at] = (int64_t)(ent >> 16);
+                log_rem[at] = avail_of(a);
+            }
+            ++seq;
+        }
+        a.hc = (head & 0xFFFFu) | (cnt << 16);
+        alocal[k] = a;
+    }
+}
+
+__global__ void k_init_approx(uint64_t n_keys, ALocal *__restrict__ alocal, AClient *__restrict__ aclient,
+                              double *__restrict__ gv, double *__restrict__ gp, int64_t *__restrict__ gt,
+                              int32_t token_limit) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += stride) {
+        alocal[k] = ALocal{token_limit, 0, 0, 0u};     // global 0, est 1 -> cap = TokenLimit
+        aclient[k] = AClient{1.0, 0, 0};
+        gv[k] = 0.0;
+        gp[k] = 0.0;
+        gt[k] = kAbsent;
+    }
+}
+
 __global__ void k_init_table(Slot *__restrict__ table, uint64_t n_keys, double cap) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -768,6 +1062,13 @@ struct tbe_engine {
     int32_t *log_rem = nullptr;
     uint64_t log_cap = 0;
     uint32_t *counters = nullptr;  // [0] eviction count, [1] refresh log count
+    // approximate kind
+    AParams ap{};
+    ALocal *alocal = nullptr;
+    AClient *aclient = nullptr;
+    double *gv = nullptr, *gp = nullptr;
+    int64_t *gt = nullptr;
+    int approx_wait = 1;
     std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
     std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
 
@@ -863,7 +1164,7 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
         HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
         HIP_TRY(e, hipMalloc(&pb.perm, cap * sizeof(uint32_t)));
-        if (e->cfg.kind == TBE_KIND_QUEUEING) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
+        if (e->cfg.kind != TBE_KIND_TOKEN_BUCKET) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.digit_total, kDigits * sizeof(uint32_t)));
@@ -916,7 +1217,8 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                      const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
                      hipStream_t st, int64_t id_base = 0) {
-    const bool wait = e->cfg.kind == TBE_KIND_QUEUEING;
+    const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
+    const bool wait = e->cfg.kind != TBE_KIND_TOKEN_BUCKET;   // status-packed replies
     if (n == 0) return TBE_OK;
     if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
                                        (unsigned long long)n);
@@ -942,7 +1244,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, st);
         stage_begin(e, ST_SCATTER, st);
-        if (p == 0 && !wait)
+        if (approx && p == 0)
+            k_scatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, nullptr, nullptr, n, shift, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.perm, e->err, 1);
+        else if (approx)
+            k_scatter<uint32_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
+                e->pass[p - 1].keys, e->pass[p - 1].permits, nullptr, e->pass[p - 1].idx, n, shift,
+                out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits, nullptr,
+                out.idx, out.perm, e->err, 0);
+        else if (p == 0 && !wait)
             k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, st>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.perm, e->err, 1);
@@ -968,7 +1279,15 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         sorted.keys, n, e->r_bits, e->nbuckets, e->bstart, e->err);
     stage_end(e, ST_BOUNDS, st);
     stage_begin(e, ST_FOLD, st);
-    if (wait) {
+    if (approx) {
+        AParams a = e->ap;
+        a.id_base = id_base;
+        a.wait = e->approx_wait;
+        k_fold_a<<<e->nbuckets, kFoldBlock, 0, st>>>(
+            sorted.keys, sorted.permits, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys, e->alocal,
+            e->ring, a, e->res[0], e->ev_cause, e->ev_id, e->counters,
+            (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), e->err);
+    } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
         k_fold_q<<<e->nbuckets, kBlock, 0, st>>>(
@@ -1015,8 +1334,10 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     *out_engine = nullptr;
     if (!config || config->struct_size < sizeof(tbe_config)) return TBE_EINVAL;
     const tbe_config &c = *config;
-    if (c.kind != TBE_KIND_TOKEN_BUCKET && c.kind != TBE_KIND_QUEUEING) return TBE_EINVAL;
-    if (c.kind == TBE_KIND_QUEUEING) {
+    if (c.kind != TBE_KIND_TOKEN_BUCKET && c.kind != TBE_KIND_QUEUEING &&
+        c.kind != TBE_KIND_APPROXIMATE)
+        return TBE_EINVAL;
+    if (c.kind != TBE_KIND_TOKEN_BUCKET) {
         if (c.queue_limit < 0 || c.queue_limit > 0xFFFF) return TBE_EINVAL;        // Q ctor
         if (c.queue_order != 0 && c.queue_order != 1) return TBE_EINVAL;
         if (c.token_limit >= (int32_t)kRemNone) return TBE_EINVAL;                 // reply packing
@@ -1077,6 +1398,23 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMemsetAsync(e->qhdr, 0, c.n_keys * sizeof(uint64_t), e->stream) != hipSuccess)
             return bail(TBE_EDEVICE);
+    } else if (c.kind == TBE_KIND_APPROXIMATE) {
+        e->ap.token_limit = c.token_limit;
+        e->ap.queue_limit = c.queue_limit;
+        e->ap.order = c.queue_order;
+        e->ap.cap = (uint32_t)std::max(1, c.queue_limit);
+        e->ap.decay_rate = rate;
+        e->ap.period_s = (double)c.replenishment_period_ticks / 10000000.0;
+        if (hipMalloc(&e->alocal, c.n_keys * sizeof(ALocal)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->aclient, c.n_keys * sizeof(AClient)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->gv, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->gp, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->gt, c.n_keys * sizeof(int64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->ring, c.n_keys * (uint64_t)e->ap.cap * sizeof(uint64_t)) != hipSuccess)
+            return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,
+                                                   c.token_limit);
     }
     if (c.max_batch && ensure_workspace(e, c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(TBE_EDEVICE);
@@ -1089,6 +1427,11 @@ void tbe_destroy(tbe_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_workspace(e);
     dfree(e->table);
+    dfree(e->alocal);
+    dfree(e->aclient);
+    dfree(e->gv);
+    dfree(e->gp);
+    dfree(e->gt);
     dfree(e->qhdr);
     dfree(e->ring);
     dfree(e->counters);
@@ -1202,15 +1545,35 @@ tbe_status tbe_export_state(tbe_engine *e, uint64_t first, uint64_t count, doubl
     return TBE_OK;
 }
 
+static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                               const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
+                               int32_t *remaining, uint64_t *n_evicted);
+
 tbe_status tbe_wait_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                           const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                           int32_t *remaining, uint64_t *n_evicted) {
     if (!e || !n_evicted) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (n && !ts_us) return fail(e, TBE_EINVAL, "null buffer");
+    return status_batch(e, keys, permits, ts_us, n, id_base, status, remaining, n_evicted);
+}
+
+tbe_status tbe_approx_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                                    uint64_t n, int32_t wait, int64_t id_base, uint8_t *status,
+                                    int32_t *available, uint64_t *n_evicted) {
+    if (!e || !n_evicted) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    e->approx_wait = wait ? 1 : 0;
+    return status_batch(e, keys, permits, nullptr, n, id_base, status, available, n_evicted);
+}
+
+static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                               const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
+                               int32_t *remaining, uint64_t *n_evicted) {
     *n_evicted = 0;
     e->evicted.clear();
     if (n == 0) return TBE_OK;
-    if (!keys || !permits || !ts_us || !status || !remaining) return fail(e, TBE_EINVAL, "null buffer");
+    if (!keys || !permits || !status || !remaining) return fail(e, TBE_EINVAL, "null buffer");
     if (id_base < 0 || (uint64_t)id_base + n > (1ull << 47))
         return fail(e, TBE_EINVAL, "request ids must lie in [0, 2^47)");
     HIP_TRY(e, hipSetDevice(e->device));
@@ -1230,8 +1593,10 @@ tbe_status tbe_wait_batch(tbe_engine *e, const uint64_t *keys, const int32_t *pe
     HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), st));
     HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    rc = run_batch(e, e->d_keys, e->d_permits, e->d_ts, n, e->d_granted, e->d_remaining, st, id_base);
+    if (ts_us)
+        HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    rc = run_batch(e, e->d_keys, e->d_permits, ts_us ? e->d_ts : nullptr, n, e->d_granted,
+                   e->d_remaining, st, id_base);
     if (rc != TBE_OK) return rc;
     uint32_t flag = 0, nev = 0;
     HIP_TRY(e, hipMemcpyAsync(&flag, e->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1321,6 +1686,88 @@ tbe_status tbe_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
     return TBE_OK;
 }
 
+tbe_status tbe_approx_collect(tbe_engine *e, int32_t *d_counts, void *stream) {
+    if (!e || !d_counts) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    HIP_TRY(e, hipSetDevice(e->device));
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+    k_approx_collect<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->alocal, d_counts);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(st));
+    return TBE_OK;
+}
+
+tbe_status tbe_approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
+                           uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted) {
+    if (!e || !d_all_counts || !n_granted) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    if (n_clients == 0 || my_client >= n_clients || ts_us < 0 || stagger_us < 0)
+        return fail(e, TBE_EINVAL, "bad sync arguments");
+    *n_granted = 0;
+    e->drained.clear();
+    HIP_TRY(e, hipSetDevice(e->device));
+    const uint64_t need = std::max<uint64_t>(e->queued_total, 1);
+    if (need > e->log_cap) {
+        dfree(e->log_keyseq);
+        dfree(e->log_id);
+        dfree(e->log_rem);
+        e->log_cap = 0;
+        HIP_TRY(e, hipMalloc(&e->log_keyseq, need * sizeof(uint64_t)));
+        HIP_TRY(e, hipMalloc(&e->log_id, need * sizeof(int64_t)));
+        HIP_TRY(e, hipMalloc(&e->log_rem, need * sizeof(int32_t)));
+        e->log_cap = need;
+    }
+    hipStream_t st = e->stream;
+    HIP_TRY(e, hipMemsetAsync(e->counters + 1, 0, sizeof(uint32_t), st));
+    const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+    k_approx_sync<<<(unsigned)blocks, kBlock, 0, st>>>(
+        e->cfg.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt, e->ring, e->ap, d_all_counts,
+        n_clients, my_client, ts_us, stagger_us, e->log_keyseq, e->log_id, e->log_rem, e->counters + 1,
+        (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu));
+    HIP_TRY(e, hipGetLastError());
+    uint32_t cnt = 0;
+    HIP_TRY(e, hipMemcpyAsync(&cnt, e->counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipStreamSynchronize(st));
+    if (cnt) {
+        std::vector<uint64_t> ks(cnt);
+        std::vector<int64_t> id(cnt);
+        std::vector<int32_t> rem(cnt);
+        HIP_TRY(e, hipMemcpy(ks.data(), e->log_keyseq, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(e, hipMemcpy(id.data(), e->log_id, cnt * sizeof(int64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(e, hipMemcpy(rem.data(), e->log_rem, cnt * sizeof(int32_t), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> order(cnt);
+        for (uint32_t i = 0; i < cnt; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ks[a] < ks[b]; });
+        e->drained.resize(cnt);
+        for (uint32_t i = 0; i < cnt; ++i)
+            e->drained[i] = std::make_tuple(ks[order[i]] >> 16, id[order[i]], rem[order[i]]);
+    }
+    e->queued_total -= cnt;
+    *n_granted = cnt;
+    return TBE_OK;
+}
+
+tbe_status tbe_approx_query(tbe_engine *e, uint64_t key, int32_t *local, int32_t *global_score,
+                            double *est, int32_t *available, uint32_t *queued) {
+    if (!e || !local || !global_score || !est || !available || !queued) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    if (key >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    ALocal a;
+    AClient c;
+    HIP_TRY(e, hipMemcpy(&a, e->alocal + key, sizeof a, hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(&c, e->aclient + key, sizeof c, hipMemcpyDeviceToHost));
+    *local = a.local;
+    *global_score = c.global;
+    *est = c.est;
+    const int32_t d = (int32_t)((uint32_t)a.cap - (uint32_t)a.local);
+    *available = d > 0 ? d : 0;
+    *queued = a.hc >> 16;
+    return TBE_OK;
+}
+
 tbe_status tbe_refresh_log(tbe_engine *e, uint64_t *keys, int64_t *request_id, int32_t *remaining,
                            uint64_t capacity, uint64_t *n_written) {
     if (!e || !n_written) return TBE_EINVAL;
@@ -1338,19 +1785,29 @@ tbe_status tbe_refresh_log(tbe_engine *e, uint64_t *keys, int64_t *request_id, i
 tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_t *permits,
                         uint32_t capacity, uint32_t *count) {
     if (!e || !count) return TBE_EINVAL;
-    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (e->cfg.kind == TBE_KIND_TOKEN_BUCKET) return fail(e, TBE_EINVAL, "engine has no queues");
     if (key >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
     HIP_TRY(e, hipSetDevice(e->device));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    uint64_t h = 0;
-    std::vector<uint64_t> ent(e->qp.cap);
-    HIP_TRY(e, hipMemcpy(&h, e->qhdr + key, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    HIP_TRY(e, hipMemcpy(ent.data(), e->ring + key * (uint64_t)e->qp.cap, e->qp.cap * sizeof(uint64_t),
+    const uint32_t rcap = e->cfg.kind == TBE_KIND_QUEUEING ? e->qp.cap : e->ap.cap;
+    uint32_t head = 0, cnt = 0;
+    if (e->cfg.kind == TBE_KIND_QUEUEING) {
+        uint64_t h = 0;
+        HIP_TRY(e, hipMemcpy(&h, e->qhdr + key, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        head = (uint32_t)(h & 0xFFFFu);
+        cnt = (uint32_t)((h >> 16) & 0xFFFFu);
+    } else {
+        ALocal a;
+        HIP_TRY(e, hipMemcpy(&a, e->alocal + key, sizeof a, hipMemcpyDeviceToHost));
+        head = a.hc & 0xFFFFu;
+        cnt = a.hc >> 16;
+    }
+    std::vector<uint64_t> ent(rcap);
+    HIP_TRY(e, hipMemcpy(ent.data(), e->ring + key * (uint64_t)rcap, rcap * sizeof(uint64_t),
                          hipMemcpyDeviceToHost));
-    const uint32_t head = (uint32_t)(h & 0xFFFFu), cnt = (uint32_t)((h >> 16) & 0xFFFFu);
     if (cnt && (!request_id || !permits) && capacity) return fail(e, TBE_EINVAL, "null buffer");
     for (uint32_t j = 0; j < cnt && j < capacity; ++j) {
-        const uint64_t x = ent[(head + j) % e->qp.cap];
+        const uint64_t x = ent[(head + j) % rcap];
         request_id[j] = (int64_t)(x >> 16);
         permits[j] = (int32_t)(x & 0xFFFFu);
     }

@@ -174,3 +174,60 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
                                            byref(cnt)))
         c = min(cnt.value, cap)
         return list(zip(ids[:c].tolist(), ps[:c].tolist()))
+
+
+class ApproximateEngine(QueueingTokenBucketEngine):
+    """ApproximateTokenBucket (ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs, A):
+    one client's local tier for every key plus a replica of the shared global tier.
+    ``acquire_batch`` = AcquireCore / WaitAsyncCore (A:84-183); a refresh epoch =
+    ``collect`` (A:430-435) -> exchange the counts between clients (RCCL all-gather, or
+    all-reduce for one node-wide client) -> ``sync`` (A:439-508)."""
+
+    KIND = _capi.TBE_KIND_APPROXIMATE
+
+    def acquire_batch(self, keys, permits, wait: bool = True, id_base: int = 0):
+        """Returns (status u8, available i32, evicted (cause index, request id))."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        permits = np.ascontiguousarray(permits, dtype=np.int32)
+        n = keys.shape[0]
+        status = np.empty(n, dtype=np.uint8)
+        avail = np.empty(n, dtype=np.int32)
+        n_ev = ctypes.c_uint64()
+        self._check(self._lib.tbe_approx_acquire_batch(self.handle, keys.ctypes.data, permits.ctypes.data,
+                                                       n, 1 if wait else 0, id_base, status.ctypes.data,
+                                                       avail.ctypes.data, byref(n_ev)))
+        m = n_ev.value
+        cause = np.empty(m, dtype=np.uint64)
+        ids = np.empty(m, dtype=np.int64)
+        nw = ctypes.c_uint64()
+        if m:
+            self._check(self._lib.tbe_evicted(self.handle, cause.ctypes.data, ids.ctypes.data, m, byref(nw)))
+        return status, avail, (cause, ids)
+
+    def collect(self, d_counts) -> None:
+        """Local scores of every key into the int32 device tensor `d_counts` [n_keys]."""
+        self._check(self._lib.tbe_approx_collect(self.handle, d_counts.data_ptr(), None))
+
+    def sync(self, d_all_counts, n_clients: int, my_client: int, ts_us: int, stagger_us: int):
+        """Replay the epoch's sync calls; returns the drain log (keys, request ids, available)."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.tbe_approx_sync(self.handle, d_all_counts.data_ptr(), n_clients, my_client,
+                                              ts_us, stagger_us, byref(n)))
+        m = n.value
+        keys = np.empty(m, dtype=np.uint64)
+        ids = np.empty(m, dtype=np.int64)
+        rem = np.empty(m, dtype=np.int32)
+        nw = ctypes.c_uint64()
+        if m:
+            self._check(self._lib.tbe_refresh_log(self.handle, keys.ctypes.data, ids.ctypes.data,
+                                                  rem.ctypes.data, m, byref(nw)))
+        return keys, ids, rem
+
+    def local_state(self, key: int):
+        """(local, global, est, available, queued) of one key."""
+        lo, gl, av = c_int32(), c_int32(), c_int32()
+        est = c_double()
+        q = c_uint32()
+        self._check(self._lib.tbe_approx_query(self.handle, key, byref(lo), byref(gl), byref(est),
+                                               byref(av), byref(q)))
+        return lo.value, gl.value, est.value, av.value, q.value

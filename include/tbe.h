@@ -46,7 +46,7 @@ typedef enum tbe_status {
 typedef enum tbe_kind {
     TBE_KIND_TOKEN_BUCKET = 0,   /* TokenBucket/ (TB, PTB)                                */
     TBE_KIND_QUEUEING = 1,       /* TokenBucketWithQueue/           */
-    TBE_KIND_APPROXIMATE = 2     /* ApproximateTokenBucket/ (reserved; §8a a9-a12)        */
+    TBE_KIND_APPROXIMATE = 2     /* ApproximateTokenBucket/        */
 } tbe_kind;
 
 /* Limiter options (TBO:9-85) plus engine sizing.  The Redis connection options
@@ -157,6 +157,38 @@ tbe_status tbe_refresh_log(tbe_engine *engine, uint64_t *keys, int64_t *request_
 /* Queue of one key, oldest first (Deque enumeration order, DQ:116-125). */
 tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, int32_t *permits,
                         uint32_t capacity, uint32_t *count);
+
+/* ---------------------------------------------------------------- ApproximateTokenBucket
+ * Engines created with kind = TBE_KIND_APPROXIMATE hold ONE client's local tier for every
+ * key (ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs, "A") plus a
+ * replica of the shared global tier (the sync script's Redis hash, A:241-270).  Status
+ * codes are the TBE_WAIT_* values; available[i] is AvailableTokens (A:37) after the
+ * decision (-1 for REJECTED). */
+
+/* wait = 0: AcquireCore (A:84-113, never queues); wait = 1: WaitAsyncCore (A:116-183).
+ * A zero-permit request that cannot lease is FAILED, never queued. */
+tbe_status tbe_approx_acquire_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
+                                    uint64_t n, int32_t wait, int64_t id_base, uint8_t *status,
+                                    int32_t *available, uint64_t *n_evicted);
+
+/* Refresh step 1 (A:430-435): d_counts[k] = _localThrottleScore of key k, then 0.
+ * d_counts is device memory for n_keys int32 (the caller exchanges it between clients,
+ * e.g. an RCCL all-gather over xGMI). */
+tbe_status tbe_approx_collect(tbe_engine *engine, int32_t *d_counts, void *stream);
+
+/* Refresh step 2 (A:439-508): replay the sync script for every key, once per client in
+ * client order, client r at ts_us + r*stagger_us with LocalCount d_all_counts[r*n_keys+k]
+ * (device memory, n_clients * n_keys int32), keep client `my_client`'s reply (global
+ * score, period via "%.14g" -> est), then drain the queues; fetch the completed queued
+ * requests with tbe_refresh_log.  n_clients = 1 with summed counts makes the node one
+ * client (an all-reduce instead of an all-gather). */
+tbe_status tbe_approx_sync(tbe_engine *engine, const int32_t *d_all_counts, uint32_t n_clients,
+                           uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted);
+
+/* Local-tier state of one key: _localThrottleScore, _globalThrottleScore,
+ * _instanceCountEstimate, AvailableTokens (GetAvailablePermits, A:81), queued requests. */
+tbe_status tbe_approx_query(tbe_engine *engine, uint64_t key, int32_t *local, int32_t *global_score,
+                            double *est, int32_t *available, uint32_t *queued);
 
 /* Per-stage device time (ms) accumulated since the last call, when
  * TBE_FLAG_STAGE_TIMING is set: out[0..n_out) = {hist, colscan, scatter, bounds,

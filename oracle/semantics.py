@@ -327,3 +327,170 @@ class QueueingTokenBucketTable:
 
     def queue_of(self, key: int) -> List[Tuple[int, int]]:
         return [(e.request_id, e.permits) for e in self.queues.get(key, [])]
+
+
+# ---------------------------------------------------------------- approximate: local tier
+# ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs ("A") as one client's
+# local tier per key (partitioned: BucketId = InstanceName + key, cf. PTB:42):
+#   AvailableTokens        A:37     max(0, (int)ceil((TokenLimit - global) / est) - local)
+#   AcquireCore            A:84-113 (sync: never queues)
+#   WaitAsyncCore          A:116-183 (async: may queue)
+#   TryLeaseUnsynchronized A:185-214
+#   RefreshAsync           A:412-508 (swap local -> count, sync script, drain)
+# Decision: a zero-permit WaitAsync that cannot lease is FAILED instead
+# of queued (the reference would queue it with no bound).
+AP_FAILED, AP_GRANTED, AP_QUEUED, AP_REJECTED = 0, 1, 2, 3
+INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+def wrap32(x: int) -> int:
+    """C# unchecked int32 arithmetic."""
+    return ((x + 2 ** 31) % 2 ** 32) - 2 ** 31
+
+
+def dotnet_double_to_int(x: float) -> int:
+    """C# ``(int)double`` (unchecked; .NET 7 on x64 saturates NaN/overflow to INT32_MIN,
+    the cvttsd2si result; in-range values truncate toward zero)."""
+    if math.isnan(x) or x >= 2147483648.0 or x <= -2147483649.0:
+        return INT32_MIN
+    return int(x)
+
+
+@dataclass
+class ApproxLocal:
+    local: int = 0            # _localThrottleScore
+    global_: int = 0          # _globalThrottleScore
+    est: float = 1.0          # _instanceCountEstimate
+    queue: List[QueueEntry] = field(default_factory=list)
+    qcount: int = 0           # _queueCount
+
+
+class ApproxClient:
+    """One client process's local tier for every key (A:9-599)."""
+
+    def __init__(self, token_limit: int, tokens_per_period: int, period_ticks: int,
+                 queue_limit: int, order: int):
+        if token_limit <= 0 or tokens_per_period <= 0:
+            raise ValueError("Both TokenLimit and TokensPerPeriod must be set to values greater than 0.")
+        if queue_limit < 0:
+            raise ValueError("QueueLimit must be set to a value greater than or equal to 0.")
+        if period_ticks < 0:
+            raise ValueError("ReplenishmentPeriod must be >= 0")
+        self.token_limit = token_limit
+        self.queue_limit = queue_limit
+        self.order = order
+        self.period_seconds = float(period_ticks) / float(TICKS_PER_SECOND)
+        self.decay_rate = fill_rate_per_second(tokens_per_period, period_ticks)
+        self.keys: Dict[int, ApproxLocal] = {}
+
+    def st(self, key: int) -> ApproxLocal:
+        s = self.keys.get(key)
+        if s is None:
+            s = self.keys[key] = ApproxLocal()
+        return s
+
+    def cap_of(self, s: ApproxLocal) -> int:
+        """(int)Math.Ceiling((TokenLimit - global) / est)  (A:37; int / double division)."""
+        q = float(wrap32(self.token_limit - s.global_)) / s.est
+        return dotnet_double_to_int(float(math.ceil(q)) if math.isfinite(q) else q)
+
+    def available(self, s: ApproxLocal) -> int:
+        """A:37: Math.Max(0, cap - _localThrottleScore) with unchecked int arithmetic."""
+        return max(0, wrap32(self.cap_of(s) - s.local))
+
+    def try_lease(self, s: ApproxLocal, p: int) -> bool:
+        """A:185-214 (returns True on lease)."""
+        avail = self.available(s)
+        if avail >= p and avail != 0:
+            if p == 0:
+                return True
+            if s.qcount == 0 or self.order == NEWEST_FIRST:
+                s.local = wrap32(s.local + p)
+                return True
+        return False
+
+    def acquire(self, key: int, p: int) -> int:
+        """AcquireCore (A:84-113)."""
+        if p < 0:
+            raise ArgumentOutOfRange("permitCount")
+        if p > self.token_limit:
+            return AP_REJECTED
+        s = self.st(key)
+        if p == 0:
+            return AP_GRANTED if self.available(s) > 0 else AP_FAILED
+        return AP_GRANTED if self.try_lease(s, p) else AP_FAILED
+
+    def wait(self, key: int, p: int, request_id: int):
+        """WaitAsyncCore (A:116-183): (status, evicted ids)."""
+        if p < 0:
+            raise ArgumentOutOfRange("permitCount")
+        if p > self.token_limit:
+            return AP_REJECTED, []
+        s = self.st(key)
+        if p == 0 and self.available(s) > 0:
+            return AP_GRANTED, []
+        if self.try_lease(s, p):
+            return AP_GRANTED, []
+        if p == 0:
+            return AP_FAILED, []          # build decision: zero permits never queue
+        evicted = []
+        if self.queue_limit - s.qcount < p:
+            if self.order == NEWEST_FIRST and p <= self.queue_limit:
+                while self.queue_limit - s.qcount < p:
+                    e = s.queue.pop(0)
+                    s.qcount -= e.permits
+                    evicted.append(e.request_id)
+            else:
+                return AP_FAILED, []
+        s.queue.append(QueueEntry(request_id, p))
+        s.qcount += p
+        return AP_QUEUED, evicted
+
+    def collect(self) -> Dict[int, int]:
+        """A:430-435: swap every key's local score to 0; returns the counts."""
+        out = {}
+        for k, s in self.keys.items():
+            out[k] = s.local
+            s.local = 0
+        return out
+
+    def apply_sync(self, key: int, global_score: int, period: float):
+        """A:441-443"""
+        s = self.st(key)
+        s.global_ = global_score
+        s.est = instance_count_estimate(self.period_seconds, period)
+
+    def drain(self):
+        """A:462-501 over every key (in key order): [(key, request_id)] granted."""
+        log = []
+        for k in sorted(self.keys):
+            s = self.keys[k]
+            while s.queue:
+                e = s.queue[0] if self.order == OLDEST_FIRST else s.queue[-1]
+                if self.available(s) >= e.permits:
+                    if self.order == OLDEST_FIRST:
+                        s.queue.pop(0)
+                    else:
+                        s.queue.pop()
+                    s.qcount -= e.permits
+                    s.local = wrap32(s.local + e.permits)
+                    log.append((k, e.request_id))
+                else:
+                    break
+        return log
+
+
+def approx_refresh_all(clients: List[ApproxClient], table: ApproxGlobalTable, ts_us: int,
+                       stagger_us: int, keys):
+    """One refresh epoch of N clients sharing one global tier: client r syncs at
+    ts_us + r*stagger_us, in client order (the sequential Redis script calls of SURVEY.md
+    §8e option 2), then drains its queues.  `keys` are the keys synced this epoch
+    (in the reference every limiter instance syncs every period)."""
+    counts = [c.collect() for c in clients]
+    logs = []
+    for r, c in enumerate(clients):
+        for k in keys:
+            g, period, _ = table.sync(f"approx:{k}", counts[r].get(k, 0), ts_us + r * stagger_us)
+            c.apply_sync(k, g, period)
+        logs.append(c.drain())
+    return logs
