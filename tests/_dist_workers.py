@@ -1,0 +1,130 @@
+"""Rank bodies for tests/test_dist_gloo.py (world_size 2, gloo on CPU).
+
+The engines here are the oracle stand-ins (tests may use oracle/): the point is the
+cluster protocol of distributedratelimiting.redis_amd/cluster.py -- routing and the
+approximate-limiter epoch -- which is the same code that drives the HIP engines over
+RCCL on a GPU node.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _init(rank: int, world: int, port: int):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+# ------------------------------------------------------------------ token bucket routing
+TB = dict(n_keys=1000, token_limit=5, tokens_per_period=1, period_ticks=10_000_000)
+TB_STEPS, TB_N = 4, 3000
+
+
+def tb_batch(rank: int, step: int):
+    rng = np.random.default_rng(1000 * rank + step)
+    keys = rng.integers(0, TB["n_keys"], TB_N, dtype=np.uint64)
+    permits = rng.integers(0, 4, TB_N, dtype=np.int32)
+    ts = 1_760_000_000_000_000 + step * 700_000 + np.sort(rng.integers(0, 700_000, TB_N))
+    return keys, permits, ts.astype(np.int64)
+
+
+def tb_route_worker(rank: int, world: int, port: int, out_dir: str):
+    dist = _init(rank, world, port)
+    from oracle import cref
+    from oracle.semantics import fill_rate_per_second
+    from distributedratelimiting.redis_amd import cluster
+
+    rate = fill_rate_per_second(TB["tokens_per_period"], TB["period_ticks"])
+    ref = cref.CTokenBucket(cluster.keys_per_rank(TB["n_keys"], world), TB["token_limit"], rate)
+    out = {}
+    for s in range(TB_STEPS):
+        k, p, t = tb_batch(rank, s)
+        g, r = cluster.route_batch(lambda lk, lp, lt: ref.acquire_batch(lk, lp, lt), k, p, t)
+        out[f"g{s}"], out[f"r{s}"] = g, r
+    v, tt = ref.export_state()
+    out["v"], out["t"] = v, tt
+    np.savez(os.path.join(out_dir, f"tb_{rank}.npz"), **out)
+    ref.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ approximate epochs
+AP = dict(n_keys=24, token_limit=8, tokens_per_period=4, period_ticks=10_000_000,
+          queue_limit=6, order=0)
+AP_EPOCHS, AP_N, AP_STAGGER = 5, 60, 1500
+
+
+def ap_batch(rank: int, epoch: int):
+    rng = np.random.default_rng(77 + 31 * rank + 1009 * epoch)
+    keys = rng.integers(0, AP["n_keys"], AP_N)
+    permits = rng.integers(0, 5, AP_N)
+    return keys, permits
+
+
+def ap_epoch_ts(epoch: int) -> int:
+    return 1_760_000_000_000_000 + (epoch + 1) * 1_000_000 + epoch * 37_000
+
+
+class OracleApproxEngine:
+    """Stand-in with the ApproximateEngine collect/sync contract: this rank's client plus a
+    replica of the global tier that every rank updates with the same sync calls."""
+
+    def __init__(self):
+        from oracle.semantics import ApproxClient, ApproxGlobalTable
+        self.client = ApproxClient(AP["token_limit"], AP["tokens_per_period"], AP["period_ticks"],
+                                   AP["queue_limit"], AP["order"])
+        for k in range(AP["n_keys"]):
+            self.client.st(k)
+        self.table = ApproxGlobalTable(self.client.decay_rate)
+
+    def collect(self, counts):
+        c = self.client.collect()
+        for k in range(AP["n_keys"]):
+            counts[k] = c.get(k, 0)
+
+    def sync(self, all_counts, n_clients, my_client, ts_us, stagger_us):
+        K = AP["n_keys"]
+        a = all_counts.numpy()
+        for r in range(n_clients):
+            for k in range(K):
+                g, period, _ = self.table.sync(f"approx:{k}", int(a[r * K + k]), ts_us + r * stagger_us)
+                if r == my_client:
+                    self.client.apply_sync(k, g, period)
+        return self.client.drain()
+
+
+def ap_epoch_worker(rank: int, world: int, port: int, out_dir: str, mode: str):
+    import torch
+    dist = _init(rank, world, port)
+    from distributedratelimiting.redis_amd import cluster
+
+    eng = OracleApproxEngine()
+    statuses, logs = [], []
+    rid = 0
+    for e in range(AP_EPOCHS):
+        keys, permits = ap_batch(rank, e)
+        for k, p in zip(keys.tolist(), permits.tolist()):
+            st, _ = eng.client.wait(k, p, rid)
+            statuses.append(st)
+            rid += 1
+        counts = torch.zeros(AP["n_keys"], dtype=torch.int32)
+        logs.append(cluster.approx_epoch(eng, counts, ap_epoch_ts(e), AP_STAGGER, mode=mode))
+    state = np.array([[s.local, s.global_, s.est, s.qcount]
+                      for _, s in sorted(eng.client.keys.items())], dtype=np.float64)
+    np.savez(os.path.join(out_dir, f"ap_{mode}_{rank}.npz"), status=np.array(statuses),
+             log=np.array([(e, k, r) for e, lg in enumerate(logs) for k, r in lg],
+                          dtype=np.int64).reshape(-1, 3),
+             state=state)
+    dist.barrier()
+    dist.destroy_process_group()
