@@ -1068,6 +1068,7 @@ struct tbe_engine {
     AClient *aclient = nullptr;
     double *gv = nullptr, *gp = nullptr;
     int64_t *gt = nullptr;
+    int32_t *acounts = nullptr;   // tbe_approx_refresh's own count buffer (single client)
     int approx_wait = 1;
     std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
     std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
@@ -1432,6 +1433,7 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->gv);
     dfree(e->gp);
     dfree(e->gt);
+    dfree(e->acounts);
     dfree(e->qhdr);
     dfree(e->ring);
     dfree(e->counters);
@@ -1746,6 +1748,17 @@ tbe_status tbe_approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t 
     e->queued_total -= cnt;
     *n_granted = cnt;
     return TBE_OK;
+}
+
+tbe_status tbe_approx_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
+    if (!e || !n_granted) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    if (ts_us < 0) return fail(e, TBE_EINVAL, "ts_us < 0");
+    HIP_TRY(e, hipSetDevice(e->device));
+    if (!e->acounts) HIP_TRY(e, hipMalloc(&e->acounts, e->cfg.n_keys * sizeof(int32_t)));
+    tbe_status rc = tbe_approx_collect(e, e->acounts, nullptr);
+    if (rc != TBE_OK) return rc;
+    return tbe_approx_sync(e, e->acounts, 1, 0, ts_us, 0, n_granted);
 }
 
 tbe_status tbe_approx_query(tbe_engine *e, uint64_t key, int32_t *local, int32_t *global_score,

@@ -213,7 +213,15 @@ class ApproximateEngine(QueueingTokenBucketEngine):
         n = ctypes.c_uint64()
         self._check(self._lib.tbe_approx_sync(self.handle, d_all_counts.data_ptr(), n_clients, my_client,
                                               ts_us, stagger_us, byref(n)))
-        m = n.value
+        return self._drain_log(n.value)
+
+    def refresh(self, ts_us: int):
+        """RefreshAsync as the only client of the global tier (A:412-508)."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.tbe_approx_refresh(self.handle, ts_us, byref(n)))
+        return self._drain_log(n.value)
+
+    def _drain_log(self, m: int):
         keys = np.empty(m, dtype=np.uint64)
         ids = np.empty(m, dtype=np.int64)
         rem = np.empty(m, dtype=np.int32)
