@@ -24,7 +24,7 @@ STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter")
 # Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).
 EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe_acquire_batch",
             "tbe_acquire_batch_device", "tbe_synchronize", "tbe_query", "tbe_export_state",
-            "tbe_wait_batch", "tbe_evicted", "tbe_refresh", "tbe_refresh_log", "tbe_queue_of",
+            "tbe_wait_batch", "tbe_queue_attempt_batch", "tbe_evicted", "tbe_refresh", "tbe_refresh_log", "tbe_queue_of",
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
             "tbe_approx_query", "tbe_stage_times")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
@@ -106,6 +106,9 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_approx_sync.restype = c_int32
     lib.tbe_approx_sync.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_int64, c_int64,
                                     POINTER(c_uint64)]
+    lib.tbe_queue_attempt_batch.restype = c_int32
+    lib.tbe_queue_attempt_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+                                            c_void_p]
     lib.tbe_approx_refresh.restype = c_int32
     lib.tbe_approx_refresh.argtypes = [c_void_p, c_int64, POINTER(c_uint64)]
     lib.tbe_approx_query.restype = c_int32

@@ -503,6 +503,8 @@ struct QParams {
     int32_t queue_limit;
     int32_t order;       // 0 OldestFirst, 1 NewestFirst
     uint32_t cap;        // ring entries per key (max(1, QueueLimit))
+    int32_t wait;        // 1 = WaitAsyncCore (may queue), 0 = AcquireCore (lease or fail)
+    int32_t pad;
     int64_t id_base;     // request id of arrival index 0 of this batch
 };
 __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t qsum) {
@@ -615,6 +617,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
                     }
                     if (granted) {
                         status = TBE_WAIT_GRANTED;
+                    } else if (!Q.wait) {
+                        status = TBE_WAIT_FAILED;                          // TryLease only
                     } else {
                         uint64_t *__restrict__ kr = ring + (row0 + kl[r]) * (uint64_t)Q.cap;
                         bool fail = false;
@@ -1069,7 +1073,7 @@ struct tbe_engine {
     double *gv = nullptr, *gp = nullptr;
     int64_t *gt = nullptr;
     int32_t *acounts = nullptr;   // tbe_approx_refresh's own count buffer (single client)
-    int approx_wait = 1;
+    int wait_mode = 1;
     std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
     std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
 
@@ -1283,7 +1287,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (approx) {
         AParams a = e->ap;
         a.id_base = id_base;
-        a.wait = e->approx_wait;
+        a.wait = e->wait_mode;
         k_fold_a<<<e->nbuckets, kFoldBlock, 0, st>>>(
             sorted.keys, sorted.permits, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys, e->alocal,
             e->ring, a, e->res[0], e->ev_cause, e->ev_id, e->counters,
@@ -1291,6 +1295,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
+        q.wait = e->wait_mode;
         k_fold_q<<<e->nbuckets, kBlock, 0, st>>>(
             sorted.keys, sorted.permits, sorted.ts, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->qhdr, e->ring, e->params, q, e->res[0], e->ev_cause, e->ev_id,
@@ -1557,7 +1562,19 @@ tbe_status tbe_wait_batch(tbe_engine *e, const uint64_t *keys, const int32_t *pe
     if (!e || !n_evicted) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
     if (n && !ts_us) return fail(e, TBE_EINVAL, "null buffer");
+    e->wait_mode = 1;
     return status_batch(e, keys, permits, ts_us, n, id_base, status, remaining, n_evicted);
+}
+
+tbe_status tbe_queue_attempt_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
+                                   const int64_t *ts_us, uint64_t n, uint8_t *status,
+                                   int32_t *remaining) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (n && !ts_us) return fail(e, TBE_EINVAL, "null buffer");
+    uint64_t n_ev = 0;
+    e->wait_mode = 0;
+    return status_batch(e, keys, permits, ts_us, n, 0, status, remaining, &n_ev);
 }
 
 tbe_status tbe_approx_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
@@ -1565,7 +1582,7 @@ tbe_status tbe_approx_acquire_batch(tbe_engine *e, const uint64_t *keys, const i
                                     int32_t *available, uint64_t *n_evicted) {
     if (!e || !n_evicted) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
-    e->approx_wait = wait ? 1 : 0;
+    e->wait_mode = wait ? 1 : 0;
     return status_batch(e, keys, permits, nullptr, n, id_base, status, available, n_evicted);
 }
 

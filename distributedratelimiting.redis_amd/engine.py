@@ -151,6 +151,19 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
             self._check(self._lib.tbe_evicted(self.handle, cause.ctypes.data, ids.ctypes.data, m, byref(nw)))
         return status, remaining, (cause, ids)
 
+    def attempt_batch(self, keys, permits, ts_us):
+        """AttemptAcquire (lease or fail, never queue); returns (status u8, remaining i32)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        permits = np.ascontiguousarray(permits, dtype=np.int32)
+        ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+        n = keys.shape[0]
+        status = np.empty(n, dtype=np.uint8)
+        remaining = np.empty(n, dtype=np.int32)
+        self._check(self._lib.tbe_queue_attempt_batch(self.handle, keys.ctypes.data, permits.ctypes.data,
+                                                      ts_us.ctypes.data, n, status.ctypes.data,
+                                                      remaining.ctypes.data))
+        return status, remaining
+
     def refresh(self, ts_us: int):
         """One replenish tick; returns (keys u64, request ids i64, remaining i32) in (key, drain) order."""
         n = ctypes.c_uint64()

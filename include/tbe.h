@@ -138,6 +138,14 @@ tbe_status tbe_wait_batch(tbe_engine *engine, const uint64_t *keys, const int32_
                           const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                           int32_t *remaining, uint64_t *n_evicted);
 
+/* AttemptAcquire on a queueing limiter (TryLeaseUnsynchronized only, Q:136-165): like
+ * tbe_wait_batch but a request that cannot lease is FAILED instead of queued (nothing is
+ * ever enqueued or evicted).  OldestFirst with a non-empty queue fails without a script
+ * call (remaining -1).  The reference's own AcquireCore is a stub (Q:62-65). */
+tbe_status tbe_queue_attempt_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
+                                   const int64_t *ts_us, uint64_t n, uint8_t *status,
+                                   int32_t *remaining);
+
 /* Evictions of the last tbe_wait_batch, sorted by (causing request index, request id):
  * cause_index[j] is the batch index of the request whose admission evicted request_id[j]. */
 tbe_status tbe_evicted(tbe_engine *engine, uint64_t *cause_index, int64_t *request_id,

@@ -306,6 +306,18 @@ class QueueingTokenBucketTable:
         self.qsum[key] = qsum + permits
         return ST_QUEUED, remaining, evicted
 
+    def attempt(self, key: int, permits: int, ts_us: int):
+        """AttemptAcquire: TryLeaseUnsynchronized only (Q:136-165), never queues.
+        Returns (status, remaining)."""
+        if permits < 0:
+            raise ArgumentOutOfRange("permitCount")
+        if permits > self.tb.cfg.token_limit:
+            return ST_REJECTED, REMAINING_NOT_EVALUATED
+        if permits == 0 or not (self.queues.get(key) and self.order == OLDEST_FIRST):
+            granted, remaining = self.tb.acquire(key, permits, ts_us)
+            return (ST_GRANTED if granted else ST_FAILED), remaining
+        return ST_FAILED, REMAINING_NOT_EVALUATED
+
     def refresh(self, ts_us: int):
         """Drain every non-empty queue at one replenish tick (Q:237-271).  Returns the
         grant log [(key, request_id, remaining)] in (key, drain order)."""

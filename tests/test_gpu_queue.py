@@ -67,3 +67,40 @@ def test_config_d_shape_small(engine_lib, gpu):
         k2, i2, r2 = ref.refresh(t_ref)
         assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
     assert (st == 2).mean() > 0.05  # queues in use
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_attempt_mixed_with_wait(engine_lib, gpu, order):
+    """AttemptAcquire batches (tbe_queue_attempt_batch) interleaved with WaitAsync batches
+    and replenish ticks, against the Python restatement (QueueingTokenBucketTable.attempt)."""
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine
+    from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
+    rng = np.random.default_rng(99 + order)
+    n_keys, qlimit = 30, 5
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, qlimit, order, device=0)
+    ref = QueueingTokenBucketTable(TokenBucketConfig.from_options(4, 1, 10_000_000), qlimit, order)
+    t, rid = S_US, 0
+    for step in range(12):
+        n = 400
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 2, 3, 5], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        if step % 3 == 1:
+            st, rem = eng.attempt_batch(keys, permits, ts)
+            exp = [ref.attempt(int(k), int(p), int(x)) for k, p, x in zip(keys, permits, ts)]
+            assert st.tolist() == [e[0] for e in exp]
+            assert rem.tolist() == [e[1] for e in exp]
+            assert not (st == 2).any()
+        else:
+            st, rem, (cause, ids) = eng.wait_batch(keys, permits, ts, rid)
+            exp = [ref.acquire(int(k), int(p), int(x), rid + i)
+                   for i, (k, p, x) in enumerate(zip(keys, permits, ts))]
+            assert st.tolist() == [e[0] for e in exp]
+            assert rem.tolist() == [e[1] for e in exp]
+            assert sorted(ids.tolist()) == sorted(i for e in exp for i in e[2])
+            rid += n
+        t += 700_000
+        keys_l, ids_l, rem_l = eng.refresh(t)
+        log = ref.refresh(t)
+        assert list(zip(keys_l.tolist(), ids_l.tolist(), rem_l.tolist())) == log
+        t += 1_000
