@@ -50,5 +50,27 @@ def build_engine(force: bool = False, verbose: bool = False, defines=(), out: st
     return out
 
 
+HOST_SRC = os.path.join(HERE, "host", "rate_limiting.cpp")
+HOST_DEPS = [HOST_SRC, os.path.join(HERE, "host", "rate_limiting.hpp"), os.path.join(ROOT, "include", "tbe.h")]
+HOST_LIB = os.path.join(HERE, "libtbe_host.so")
+CXX_FLAGS = ["-O2", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"]
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """libtbe_host.so: the C++ limiter classes (host/) over libtbe.so."""
+    build_engine(verbose=verbose)
+    if not force and up_to_date(HOST_LIB, HOST_DEPS + [LIB]):
+        return HOST_LIB
+    cmd = ["g++"] + CXX_FLAGS + ["-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
+                                 "-o", HOST_LIB + ".tmp", HOST_SRC, "-L", HERE, "-ltbe",
+                                 "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(HOST_LIB + ".tmp", HOST_LIB)
+    return HOST_LIB
+
+
 if __name__ == "__main__":
     print(build_engine(force="--force" in sys.argv, verbose=True))
+    print(build_host(force="--force" in sys.argv, verbose=True))

@@ -1335,27 +1335,41 @@ double tbe_fill_rate(int32_t tokens_per_period, int64_t replenishment_period_tic
     return (double)tokens_per_period / total_seconds;
 }
 
+static thread_local std::string g_create_error = "no error";
+
+static tbe_status create_fail(tbe_status st, const char *msg) {
+    g_create_error = msg;
+    return st;
+}
+
 tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
-    if (!out_engine) return TBE_EINVAL;
+    if (!out_engine) return create_fail(TBE_EINVAL, "out_engine is NULL");
     *out_engine = nullptr;
-    if (!config || config->struct_size < sizeof(tbe_config)) return TBE_EINVAL;
+    if (!config || config->struct_size < sizeof(tbe_config))
+        return create_fail(TBE_EINVAL, "config is NULL or struct_size too small");
     const tbe_config &c = *config;
     if (c.kind != TBE_KIND_TOKEN_BUCKET && c.kind != TBE_KIND_QUEUEING &&
         c.kind != TBE_KIND_APPROXIMATE)
-        return TBE_EINVAL;
+        return create_fail(TBE_EINVAL, "unknown kind");
     if (c.kind != TBE_KIND_TOKEN_BUCKET) {
-        if (c.queue_limit < 0 || c.queue_limit > 0xFFFF) return TBE_EINVAL;        // Q ctor
-        if (c.queue_order != 0 && c.queue_order != 1) return TBE_EINVAL;
-        if (c.token_limit >= (int32_t)kRemNone) return TBE_EINVAL;                 // reply packing
+        if (c.queue_limit < 0 || c.queue_limit > 0xFFFF)                            // Q ctor
+            return create_fail(TBE_EINVAL, "QueueLimit must lie in [0, 65535]");
+        if (c.queue_order != 0 && c.queue_order != 1)
+            return create_fail(TBE_EINVAL, "QueueProcessingOrder must be OldestFirst (0) or NewestFirst (1)");
+        if (c.token_limit >= (int32_t)kRemNone)                                     // reply packing
+            return create_fail(TBE_EINVAL, "TokenLimit must be < 2^30 - 1 for queueing limiters");
     }
-    if (c.n_keys == 0 || c.n_keys > (1ull << 32)) return TBE_EINVAL;
-    if (c.token_limit <= 0 || c.tokens_per_period <= 0) return TBE_EINVAL;   // TB:29-32
-    if (c.replenishment_period_ticks <= 0) return TBE_EINVAL;                // TB:34-37 (+ "∞")
+    if (c.n_keys == 0 || c.n_keys > (1ull << 32))
+        return create_fail(TBE_EINVAL, "n_keys must lie in [1, 2^32]");
+    if (c.token_limit <= 0 || c.tokens_per_period <= 0)                       // TB:29-32
+        return create_fail(TBE_EINVAL, "Both TokenLimit and TokensPerPeriod must be set to values greater than 0.");
+    if (c.replenishment_period_ticks <= 0)                                    // TB:34-37 (+ "inf")
+        return create_fail(TBE_EINVAL, "ReplenishmentPeriod must be greater than TimeSpan.Zero");
     const double rate = tbe_fill_rate(c.tokens_per_period, c.replenishment_period_ticks);
-    if (!std::isfinite(rate) || !(rate > 0.0)) return TBE_EINVAL;
+    if (!std::isfinite(rate) || !(rate > 0.0)) return create_fail(TBE_EINVAL, "fill rate is not finite and positive");
 
     tbe_engine *e = new (std::nothrow) tbe_engine();
-    if (!e) return TBE_ENOMEM;
+    if (!e) return create_fail(TBE_ENOMEM, "host allocation failed");
     e->cfg = c;
     e->params.cap = (double)c.token_limit;
     e->params.rate = rate;
@@ -1375,7 +1389,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
 
     auto bail = [&](tbe_status st) {
         tbe_destroy(e);
-        return st;
+        return create_fail(st, st == TBE_ENOMEM ? "device allocation failed" : "HIP device error");
     };
     if (c.device >= 0) {
         if (hipSetDevice(c.device) != hipSuccess) return bail(TBE_EDEVICE);
@@ -1456,7 +1470,7 @@ void tbe_destroy(tbe_engine *e) {
 }
 
 const char *tbe_last_error(const tbe_engine *e) {
-    return e ? e->last_error.c_str() : "null engine";
+    return e ? e->last_error.c_str() : g_create_error.c_str();
 }
 
 tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,

@@ -82,7 +82,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine);
 /* Replaces Dispose / DisposeAsyncCore (TB:85-109).  NULL is ignored. */
 void tbe_destroy(tbe_engine *engine);
 
-/* Human-readable description of the last non-OK status on this engine (never NULL). */
+/* Human-readable description of the last non-OK status on this engine (never NULL);
+ * with engine == NULL, of the calling thread's last failed tbe_create. */
 const char *tbe_last_error(const tbe_engine *engine);
 
 /* Replaces n sequential IDatabase.ScriptEvaluateAsync(_acquireScript,

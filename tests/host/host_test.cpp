@@ -1,0 +1,328 @@
+// host_test.cpp -- tests of the C++ limiter mirror (distributedratelimiting.redis_amd/host),
+// written like the reference's callers would use the classes.  Run by tests/test_host_cpp.py:
+//   host_test cpu   option validation, value types, registration (no device needed)
+//   host_test gpu   decisions through libtbe.so on the GPU, checked against the C oracle
+//                   (oracle/tb_ref.c; test infrastructure) and hand-derived expectations
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rate_limiting.hpp"
+
+using namespace tbe::rate_limiting;
+
+// ---- the C oracle (oracle/tb_ref.c), declared here: it has no header of its own
+extern "C" {
+typedef struct tbr_table tbr_table;
+tbr_table *tbr_create(uint64_t n_keys, int32_t token_limit, double fill_rate);
+void tbr_destroy(tbr_table *tb);
+int tbr_acquire_batch(tbr_table *tb, const uint64_t *keys, const int32_t *permits, const int64_t *ts_us,
+                      uint64_t n, uint8_t *granted, int32_t *remaining);
+double tbr_fill_rate(int32_t tokens_per_period, int64_t period_ticks);
+}
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond)                                                                   \
+    do {                                                                              \
+        if (!(cond)) {                                                                \
+            std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+            ++g_fail;                                                                 \
+        } else {                                                                      \
+            ++g_pass;                                                                 \
+        }                                                                             \
+    } while (0)
+
+template <class E, class F>
+static bool throws(F &&f, const char *param = nullptr) {
+    try {
+        f();
+    } catch (const E &e) {
+        if constexpr (std::is_base_of_v<ArgumentException, E>)
+            if (param && e.ParamName != param) return false;
+        return true;
+    } catch (...) {
+        return false;
+    }
+    return false;
+}
+
+static const int64_t T0 = 1760000000000000LL;  // injected "Redis TIME" origin, µs
+
+struct FakeClock {
+    std::shared_ptr<std::atomic<int64_t>> now = std::make_shared<std::atomic<int64_t>>(T0);
+    Clock fn() const {
+        auto p = now;
+        return [p] { return p->load(); };
+    }
+    void advance(int64_t us) { now->fetch_add(us); }
+};
+
+static RedisTokenBucketRateLimiterOptions tb_options(int limit, int per_period, double period_s) {
+    RedisTokenBucketRateLimiterOptions o;
+    o.TokenLimit = limit;
+    o.TokensPerPeriod = per_period;
+    o.ReplenishmentPeriod = TimeSpan::FromSeconds(period_s);
+    o.InstanceName = "tb:";
+    o.Device = 0;
+    return o;
+}
+
+// ====================================================================== CPU cases
+static void test_validation() {
+    // TB:29-37 (and A:49-62): ArgumentException naming "options", before any device work.
+    auto o = tb_options(0, 1, 1.0);
+    CHECK(throws<ArgumentException>([&] { RedisTokenBucketRateLimiter l(o); }, "options"));
+    o = tb_options(5, 0, 1.0);
+    CHECK(throws<ArgumentException>([&] { PartitionedRedisTokenBucketRateLimiter l(o); }, "options"));
+    o = tb_options(5, 1, 1.0);
+    o.ReplenishmentPeriod = TimeSpan::FromTicks(-1);
+    CHECK(throws<ArgumentException>([&] { RedisTokenBucketRateLimiter l(o); }, "options"));
+    // A period of zero is accepted by the reference's ctor but makes the script's fill
+    // rate infinite; the engine refuses it as an invalid option.
+    o.ReplenishmentPeriod = TimeSpan::FromTicks(0);
+    CHECK(throws<ArgumentException>([&] { RedisTokenBucketRateLimiter l(o); }, "options"));
+    RedisApproximateTokenBucketRateLimiterOptions a;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(a) = tb_options(5, 1, 1.0);
+    a.QueueLimit = -1;
+    CHECK(throws<ArgumentException>([&] { RedisApproximateTokenBucketRateLimiter l(a); }, "options"));
+    RedisQueueingTokenBucketRateLimiterOptions q;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(q) = tb_options(5, 1, 1.0);
+    q.QueueLimit = 70000;  // beyond the engine's 16-bit queue accounting
+    CHECK(throws<ArgumentException>([&] { RedisQueueingTokenBucketRateLimiter l(q); }, "options"));
+}
+
+static void test_value_types() {
+    CHECK(TimeSpan::FromSeconds(1.5).ticks == 15000000);
+    CHECK(TimeSpan::FromSeconds(-0.25).ticks == -2500000);
+    CHECK(TimeSpan::FromSeconds(1e-8).ticks == 0);  // truncation toward zero (.NET 7)
+    CHECK(throws<std::overflow_error>([] { TimeSpan::FromSeconds(1e300); }));
+    RateLimitLease ok(true), no(false, TimeSpan::FromSeconds(90061.5));
+    CHECK(ok.IsAcquired() && !no.IsAcquired());
+    TimeSpan ra;
+    CHECK(!ok.TryGetRetryAfter(ra));
+    CHECK(no.TryGetRetryAfter(ra) && ra.ticks == 900615000000LL);
+    CHECK(ok.ToString() == "Lease IsAcquired: True");
+    CHECK(no.ToString() == "Lease IsAcquired: False RETRY_AFTER: 1.01:01:01.5000000");
+    CHECK(no.MetadataNames().size() == 1 && no.MetadataNames()[0] == "RETRY_AFTER");
+    // FillRatePerSecond (TBO:82-85) is the same double the oracle computes.
+    auto o = tb_options(10, 3, 7.0);
+    CHECK(o.FillRatePerSecond() == tbr_fill_rate(3, 70000000));
+    o.ReplenishmentPeriod = TimeSpan::FromMilliseconds(100);
+    CHECK(o.FillRatePerSecond() == 30.0);
+}
+
+static void test_registration_empty() {
+    ServiceCollection services;
+    CHECK(throws<std::logic_error>([&] { services.GetRequiredRateLimiter(); }));
+}
+
+// ====================================================================== GPU cases
+static void test_tb_sequence() {
+    // One bucket, a deterministic sequence: every lease and every estimate equals the
+    // C oracle's reply for the same (permits, time) sequence.
+    FakeClock clk;
+    auto o = tb_options(7, 2, 1.0);
+    o.TimeSource = clk.fn();
+    RedisTokenBucketRateLimiter lim(o);
+    tbr_table *ref = tbr_create(1, 7, o.FillRatePerSecond());
+    std::mt19937_64 rng(7);
+    for (int i = 0; i < 300; ++i) {
+        const int p = (int)(rng() % 5);
+        clk.advance((int64_t)(rng() % 400000));
+        const uint64_t key = 0;
+        const int32_t pp = p;
+        const int64_t ts = clk.now->load();
+        uint8_t g;
+        int32_t rem;
+        tbr_acquire_batch(ref, &key, &pp, &ts, 1, &g, &rem);
+        const bool acquired = (i % 2) ? lim.AcquireAsync(p).get().IsAcquired() : lim.AttemptAcquire(p).IsAcquired();
+        CHECK(acquired == (g != 0));
+        CHECK(lim.GetAvailablePermits() == rem);
+    }
+    CHECK(!lim.IdleDuration().has_value());
+    CHECK(throws<ArgumentOutOfRangeException>([&] { lim.AttemptAcquire(-1); }, "permitCount"));
+    lim.Dispose();
+    CHECK(throws<ObjectDisposedException>([&] { lim.AttemptAcquire(1); }));
+    lim.Dispose();  // idempotent (TB:87-90)
+    tbr_destroy(ref);
+}
+
+static void test_partitioned_concurrent() {
+    // 8 threads x 2500 AcquireAsync over 64 resources.  The submitter's batch trace is
+    // the serial order; replaying it through the oracle must reproduce every reply, and
+    // the callers must see exactly the granted count the trace records.
+    FakeClock clk;
+    auto o = tb_options(5, 1, 0.5);
+    o.TimeSource = [c = clk.now] { return c->fetch_add(37); };
+    o.PartitionLimit = 128;
+    o.MaxBatch = 512;
+    std::mutex tmu;
+    std::vector<uint64_t> tk;
+    std::vector<int32_t> tp, trem;
+    std::vector<int64_t> tts;
+    std::vector<uint8_t> tst;
+    size_t batches = 0;
+    o.OnBatch = [&](const BatchTrace &b) {
+        std::lock_guard<std::mutex> g(tmu);
+        ++batches;
+        tk.insert(tk.end(), b.keys, b.keys + b.n);
+        tp.insert(tp.end(), b.permits, b.permits + b.n);
+        tts.insert(tts.end(), b.ts_us, b.ts_us + b.n);
+        tst.insert(tst.end(), b.status, b.status + b.n);
+        trem.insert(trem.end(), b.remaining, b.remaining + b.n);
+    };
+    PartitionedRedisTokenBucketRateLimiter lim(o);
+    std::atomic<long> granted{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t)
+        th.emplace_back([&, t] {
+            std::mt19937_64 rng(100 + t);
+            std::vector<std::future<RateLimitLease>> fs;
+            for (int i = 0; i < 2500; ++i)
+                fs.push_back(lim.AcquireAsync("user-" + std::to_string(rng() % 64), (int)(rng() % 3)));
+            for (auto &f : fs) granted += f.get().IsAcquired();
+        });
+    for (auto &x : th) x.join();
+    CHECK(tk.size() == 20000);
+    tbr_table *ref = tbr_create(128, 5, o.FillRatePerSecond());
+    std::vector<uint8_t> g(tk.size());
+    std::vector<int32_t> rem(tk.size());
+    tbr_acquire_batch(ref, tk.data(), tp.data(), tts.data(), tk.size(), g.data(), rem.data());
+    long exp_granted = 0, bad = 0;
+    for (size_t i = 0; i < tk.size(); ++i) {
+        exp_granted += g[i];
+        bad += (g[i] != tst[i]) || (rem[i] != trem[i]);
+    }
+    CHECK(bad == 0);
+    CHECK(granted.load() == exp_granted);
+    CHECK(batches < tk.size());  // concurrent callers were actually batched
+    std::printf("partitioned: %zu requests in %zu batches, %ld granted\n", tk.size(), batches, exp_granted);
+    // GetAvailablePermits(resource): unseen resource -> TokenLimit; seen -> last reply
+    CHECK(lim.GetAvailablePermits("never-seen") == 5);
+    uint64_t last_key = tk.back();
+    (void)last_key;
+    tbr_destroy(ref);
+}
+
+static void test_queueing_limiter() {
+    // Hand-derived (DESIGN.md §2b semantics): TokenLimit 2, 1 token/s, QueueLimit 3, OldestFirst.
+    FakeClock clk;
+    RedisQueueingTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(2, 1, 1.0);
+    o.TimeSource = clk.fn();
+    o.QueueLimit = 3;
+    o.AutoReplenishment = false;
+    RedisQueueingTokenBucketRateLimiter lim(o);
+    CHECK(lim.AcquireAsync(2).get().IsAcquired());          // fresh bucket: 2 >= 2
+    CHECK(lim.GetAvailablePermits() == 0);
+    clk.advance(1);
+    auto q1 = lim.AcquireAsync(1);                          // denied by the script -> queued
+    clk.advance(1);
+    auto q2 = lim.AcquireAsync(2);                          // OldestFirst: queue non-empty -> queued
+    clk.advance(1);
+    CHECK(!lim.AcquireAsync(1).get().IsAcquired());         // 3 - 3 < 1: queue full -> failed
+    CHECK(!lim.AttemptAcquire(1).IsAcquired());             // never leases past the queue
+    CHECK(throws<ArgumentOutOfRangeException>([&] { lim.AcquireAsync(3); }, "permitCount"));
+    CHECK(q1.wait_for(std::chrono::milliseconds(50)) == std::future_status::timeout);
+    clk.advance(1000000);
+    CHECK(lim.TryReplenish());                              // head (1) granted, then 2 > ~0 stops
+    CHECK(q1.get().IsAcquired());
+    CHECK(q2.wait_for(std::chrono::milliseconds(50)) == std::future_status::timeout);
+    clk.advance(2000000);
+    CHECK(lim.TryReplenish());
+    CHECK(q2.get().IsAcquired());
+    CHECK(lim.GetAvailablePermits() == 0);
+    auto q3 = lim.AcquireAsync(2);                          // queued again
+    lim.Dispose();                                          // fails every queued request
+    CHECK(!q3.get().IsAcquired());
+    CHECK(throws<ObjectDisposedException>([&] { lim.AcquireAsync(1); }));
+}
+
+static void test_approximate_limiter() {
+    // Expected values from oracle/semantics.py (ApproxClient + ApproxGlobalTable):
+    //   lease 3 ok, lease 2 fails, wait 2 queues (available 1);
+    //   refresh 0: global 3, est inf -> available 0; refresh +1 s: global 0, est 5 -> 1;
+    //   refresh +2 s: est 3 -> cap 2 -> the queued 2 is granted, local 2, available 0.
+    FakeClock clk;
+    RedisApproximateTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(4, 4, 1.0);
+    o.TimeSource = clk.fn();
+    o.QueueLimit = 5;
+    o.AutoReplenishment = false;
+    RedisApproximateTokenBucketRateLimiter lim(o);
+    CHECK(!lim.IdleDuration().has_value());
+    CHECK(lim.AttemptAcquire(3).IsAcquired());
+    RateLimitLease f = lim.AttemptAcquire(2);
+    CHECK(!f.IsAcquired());
+    TimeSpan ra;
+    // A:393-394: deficit = max(0, consumed 3 + 2 + queued 0 - 4) = 1; FromSeconds(1 * 4.0)
+    CHECK(f.TryGetRetryAfter(ra) && ra.ticks == 40000000);
+    auto q = lim.AcquireAsync(2);
+    CHECK(lim.GetAvailablePermits() == 1);
+    CHECK(throws<ArgumentOutOfRangeException>([&] { lim.AttemptAcquire(5); }, "permitCount"));
+    CHECK(lim.TryReplenish());
+    CHECK(lim.GetAvailablePermits() == 0);
+    clk.advance(1000000);
+    CHECK(lim.TryReplenish());
+    CHECK(lim.GetAvailablePermits() == 1);
+    CHECK(lim.IdleDuration().has_value());                  // consumed 0 after the sync (A:503-506)
+    CHECK(q.wait_for(std::chrono::milliseconds(20)) == std::future_status::timeout);
+    clk.advance(1000000);
+    CHECK(lim.TryReplenish());
+    CHECK(q.get().IsAcquired());
+    CHECK(lim.GetAvailablePermits() == 0);
+    CHECK(lim.ToString() == "RedisApproximateTokenBucketRateLimiter Consumed: 2 Available: 0 Peer Count (Estimate): 3");
+    lim.Dispose();
+    CHECK(throws<ObjectDisposedException>([&] { lim.AttemptAcquire(1); }));
+}
+
+static void test_auto_replenishment() {
+    // The timer drains the queue without TryReplenish (real clock, short period).
+    RedisQueueingTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(1, 1, 0.05);
+    o.QueueLimit = 4;
+    RedisQueueingTokenBucketRateLimiter lim(o);
+    CHECK(!lim.TryReplenish());
+    CHECK(lim.AttemptAcquire(1).IsAcquired());
+    auto q = lim.AcquireAsync(1);
+    CHECK(q.wait_for(std::chrono::seconds(5)) == std::future_status::ready && q.get().IsAcquired());
+}
+
+static void test_registration() {
+    ServiceCollection services;
+    services.AddRedisTokenBucketRateLimiter([](RedisTokenBucketRateLimiterOptions &o) {
+        o.TokenLimit = 3;
+        o.TokensPerPeriod = 1;
+        o.InstanceName = "svc";
+        o.Device = 0;
+    });
+    auto a = services.GetRequiredRateLimiter();
+    auto b = services.GetRequiredRateLimiter();
+    CHECK(a.get() == b.get());
+    int got = 0;
+    for (int i = 0; i < 5; ++i) got += a->AttemptAcquire(1).IsAcquired();
+    CHECK(got == 3);
+}
+
+int main(int argc, char **argv) {
+    const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+    test_validation();
+    test_value_types();
+    test_registration_empty();
+    if (gpu) {
+        test_tb_sequence();
+        test_partitioned_concurrent();
+        test_queueing_limiter();
+        test_approximate_limiter();
+        test_auto_replenishment();
+        test_registration();
+    }
+    std::printf("host_test %s: %d checks passed, %d failed\n", gpu ? "gpu" : "cpu", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}
