@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate CPU-baseline budget (0 disables)")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--no-pack", action="store_true",
+                    help="wide pass records even where the packed 8-byte form applies (A/B)")
+    ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
     return ap.parse_args()
 
 
@@ -79,7 +82,9 @@ def main():
     n = args.batch
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                             args.period_ticks, device=dev.index,
-                            stage_timing=not args.no_stage_timing, max_batch=n)
+                            stage_timing=not args.no_stage_timing, max_batch=n,
+                            pack=not args.no_pack, hot=not args.no_hot)
+    layout = eng.layout()
     total_steps = args.warmup + args.steps
     seed = SEED_B + 7919 * rank
     bufs = []
@@ -125,12 +130,12 @@ def main():
     # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
     roofline = None
     if stages and sum(stages.values()) > 0:
-        passes = eng_passes(keys_local)
+        passes = layout["passes"]
         launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                    "unscatter": passes}   # per step
+                    "unscatter": passes, "hot": 5}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
-        alg_bytes = algorithmic_bytes(name, n, keys_local, passes)
+        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"])
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -159,7 +164,8 @@ def main():
                        "keys_total": args.keys, "keys_per_gpu": keys_local, "batch_per_gpu": n,
                        "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
                        "period_ticks": args.period_ticks, "interval_us": args.interval_us,
-                       "partitioning": f"key-hash x{world}, no data-path collective"},
+                       "partitioning": f"key-hash x{world}, no data-path collective",
+                       "layout": layout},
             "grant_rate_last_batch": round(grant_rate, 4),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "roofline": roofline,
@@ -171,28 +177,24 @@ def main():
         td.destroy_process_group()
 
 
-def eng_passes(n_keys: int) -> int:
-    kb = max(0, (n_keys - 1).bit_length())
-    r_bits = min(11, max(4, kb - 10))
-    nb = (n_keys + (1 << r_bits) - 1) >> r_bits
-    bb = max(0, (nb - 1).bit_length())
-    return max(1, (bb + 7) // 8)
-
-
-def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int) -> int:
+def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool) -> int:
     """Bytes one launch of `stage` must move at minimum for its function,
-    averaged over the passes where a stage runs once per pass."""
+    averaged over the passes where a stage runs once per pass.  Packed: the passes and
+    the fold move one 8-byte record per request; wide: {key u32, permits i32, ts i64}."""
+    rec = 8 if packed else 16
     if stage == "fold":
-        # sorted records (key 4 + permits 4 + ts 8) + packed reply 4 per request, plus the
-        # table rows of the distinct keys in the batch (16 B read + 16 B written each).
+        # sorted records + packed reply 4 per request, plus the table rows of the distinct
+        # keys in the batch (16 B read + 16 B written each)
         u = n_keys * (1.0 - np.exp(-n / n_keys))
-        return int(n * 20 + u * 32)
+        return int(n * (rec + 4) + u * 32)
     if stage == "scatter":
-        # pass 0 reads key 8 + permits 4 + ts 8, later passes key 4 + 4 + 8; every pass
-        # writes key 4 + permits 4 + ts 8 and its permutation 4
-        return int(n * ((20 + 16 * (passes - 1)) / passes + 20))
+        # pass 0 reads the caller's key 8 + permits 4 + ts 8, later passes one record;
+        # every pass writes a record and its 4-byte permutation entry
+        return int(n * ((20 + (rec if packed else 16) * (passes - 1)) / passes + rec + 4))
     if stage == "hist":
-        return int(n * (8 + 4 * (passes - 1)) / passes)
+        return int(n * (8 + (8 if packed else 4) * (passes - 1)) / passes)
+    if stage == "bounds":
+        return n * (8 if packed else 4)
     if stage == "unscatter":
         # perm 4 + gathered reply 4 + written 4 (inner passes) or 5 (final: u8 + i32)
         return int(n * (12 * (passes - 1) + 13) / passes)

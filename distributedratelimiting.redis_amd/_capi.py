@@ -19,14 +19,16 @@ STATUS_NAMES = {0: "TBE_OK", 1: "TBE_EINVAL", 2: "TBE_ENOMEM", 3: "TBE_EDEVICE",
                 4: "TBE_EDISPOSED", 5: "TBE_ERANGE"}
 TBE_KIND_TOKEN_BUCKET, TBE_KIND_QUEUEING, TBE_KIND_APPROXIMATE = 0, 1, 2
 TBE_FLAG_STAGE_TIMING = 0x1
-STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter")
+TBE_FLAG_NO_PACK = 0x2
+TBE_FLAG_NO_HOT = 0x4
+STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter", "hot")
 
 # Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).
 EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe_acquire_batch",
             "tbe_acquire_batch_device", "tbe_synchronize", "tbe_query", "tbe_export_state",
             "tbe_wait_batch", "tbe_queue_attempt_batch", "tbe_evicted", "tbe_refresh", "tbe_refresh_log", "tbe_queue_of",
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
-            "tbe_approx_query", "tbe_stage_times")
+            "tbe_approx_query", "tbe_layout", "tbe_stage_times")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -114,6 +116,8 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_approx_query.restype = c_int32
     lib.tbe_approx_query.argtypes = [c_void_p, c_uint64, POINTER(c_int32), POINTER(c_int32),
                                      POINTER(c_double), POINTER(c_int32), POINTER(c_uint32)]
+    lib.tbe_layout.restype = c_int32
+    lib.tbe_layout.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     lib.tbe_stage_times.restype = c_int32
     lib.tbe_stage_times.argtypes = [c_void_p, POINTER(c_double), c_uint32, POINTER(c_uint32)]
     _lib = lib

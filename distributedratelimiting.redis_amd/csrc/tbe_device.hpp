@@ -67,16 +67,6 @@ __device__ __forceinline__ double new_t_of(int64_t ts_us) {
     return (double)sec + q;
 }
 
-// Stored grant time packed for the expiry test: (ts / 1000) << 10 | (ts % 1000).
-// kAbsent (INT64_MIN) marks a key with no Redis hash.
-__device__ __forceinline__ int64_t tpack_of(int64_t ts_us) {
-    const int64_t ms = ts_us / 1000;
-    return (ms << 10) | (ts_us - ms * 1000);
-}
-__device__ __forceinline__ int64_t ts_of_tpack(int64_t tp) {
-    return (tp == kAbsent) ? kAbsent : (tp >> 10) * 1000 + (tp & 1023);
-}
-
 struct TbParams {
     double cap;       // Lua `capacity` (TB:184), TokenLimit as f64
     double rate;      // Lua `fill_rate` (TB:185), FillRatePerSecond bits
@@ -88,60 +78,59 @@ struct TbParams {
 struct ReqTime {
     double new_t;    // TB:203
     int64_t ms;      // command-time snapshot for passive expiry
-    int64_t tp;      // tpack_of(ts): what a grant stores
+    int64_t ts;      // the injected TIME itself: what a grant stores
 };
 __device__ __forceinline__ ReqTime req_time(int64_t ts_us) {
     ReqTime r;
     r.new_t = new_t_of(ts_us);
     r.ms = ts_us / 1000;
-    r.tp = (r.ms << 10) | (ts_us - r.ms * 1000);
+    r.ts = ts_us;
     return r;
 }
 
-// One evaluation of the acquire script (TB:202-238) on a key's state
-// {v, t = field t as f64, tp = packed grant time}.  Returns the packed reply: bit 31 =
-// success (TB:224/238), bits 0-30 = trunc(new_v) (TB:238 -> RESP integer -> TB:73).
-// `modified` is set when the state changed: on a grant (HSET, TB:225-236) and when
-// Redis' passive expiry deleted the key on access (the HGETALL at TB:210 finds it
-// lapsed), which happens even if the request is then denied.
-__device__ __forceinline__ uint32_t tb_step(double &v, double &t, int64_t &tp, int32_t permits,
-                                            const ReqTime &rq, const TbParams &P, bool &modified) {
-    const bool had = tp != kAbsent;
+// One evaluation of the acquire script (TB:202-238) on a key's stored row {v, t_us}
+// (the Redis hash {v, t}), with the row's field t supplied by the caller as ft =
+// new_t_of(row.t_us) (ignored while the key is absent).  Returns the packed reply: bit
+// 31 = success (TB:224/238), bits 0-30 = trunc(new_v) (TB:238 -> RESP integer ->
+// TB:73).  `modified` is set when the row changed: on a grant (HSET, TB:225-236) and
+// when Redis' passive expiry deleted the key on access (the HGETALL at TB:210 finds it
+// lapsed), which happens even if the request is then denied.  A call that leaves
+// `modified` false leaves the row exactly as it found it.
+__device__ __forceinline__ uint32_t tb_step_ft(Slot &row, double ft, int32_t permits,
+                                               const ReqTime &rq, const TbParams &P, bool &modified) {
+    const bool had = row.t_us != kAbsent;
     // EXPIRE at TB:235 lapses when the command-time snapshot (ms) exceeds grant_ms + ttl.
-    const bool expired = had && (rq.ms > (tp >> 10) + P.ttl_ms);
+    const bool expired = had && (rq.ms > row.t_us / 1000 + P.ttl_ms);
     const bool present = had && !expired;
-    const double pv = present ? v : P.cap;                // TB:211-215
-    const double pt = present ? t : rq.new_t;
-    const double delta_t = lua_max(0.0, rq.new_t - pt);   // TB:218
-    const double fill = delta_t * P.rate;                 // TB:221: mul ...
-    double x = lua_max(0.0, lua_min(P.cap, pv + fill));   // ... then add (never fused)
+    const double pv = present ? row.v : P.cap;                          // TB:211-215
+    const double pt = present ? ft : rq.new_t;
+    const double delta_t = lua_max(0.0, rq.new_t - pt);                 // TB:218
+    const double fill = delta_t * P.rate;                               // TB:221: mul ...
+    double x = lua_max(0.0, lua_min(P.cap, pv + fill));                 // ... then add (never fused)
     const double p = (double)permits;
-    const bool granted = x >= p;                          // TB:224
+    const bool granted = x >= p;                                        // TB:224
     if (granted) {
-        x = x - p;                                        // TB:227
-        v = x;                                            // TB:230 HSET v, t
-        t = rq.new_t;
-        tp = rq.tp;
+        x = x - p;                                                      // TB:227
+        row.v = x;                                                      // TB:230 HSET v, t
+        row.t_us = rq.ts;
     } else if (expired) {
-        v = P.cap;                                        // key deleted by passive expiry
-        t = 0.0;
-        tp = kAbsent;
+        row.v = P.cap;                                                  // deleted by passive expiry
+        row.t_us = kAbsent;
     }
     modified = granted || expired;
-    return (granted ? 0x80000000u : 0u) | (uint32_t)(int32_t)x;   // {success, new_v}
+    return (granted ? 0x80000000u : 0u) | (uint32_t)(int32_t)x;         // {success, new_v}
 }
 
-// The same on a table row {v, t_us} (drain kernel, queueing fold).
+// The same, deriving field t from the row itself.
+__device__ __forceinline__ uint32_t tb_step(Slot &row, int32_t permits, const ReqTime &rq,
+                                            const TbParams &P, bool &modified) {
+    const double ft = new_t_of(row.t_us == kAbsent ? 0 : row.t_us);
+    return tb_step_ft(row, ft, permits, rq, P, modified);
+}
+
 __device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t ts_us,
                                                const TbParams &P, bool &modified) {
-    double v = s.v, t = (s.t_us == kAbsent) ? 0.0 : new_t_of(s.t_us);
-    int64_t tp = (s.t_us == kAbsent) ? kAbsent : tpack_of(s.t_us);
-    const uint32_t reply = tb_step(v, t, tp, permits, req_time(ts_us), P, modified);
-    if (modified) {
-        s.v = v;
-        s.t_us = ts_of_tpack(tp);
-    }
-    return reply;
+    return tb_step(s, permits, req_time(ts_us), P, modified);
 }
 
 // ----------------------------------------------------------------- wave / block helpers

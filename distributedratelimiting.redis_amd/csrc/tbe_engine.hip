@@ -44,9 +44,20 @@ using namespace tbe;
 
 namespace {
 
-constexpr int kPartBlock = 1024;                       // partition workgroup (16 waves)
-constexpr int kPartItems = 8;                          // elements per thread per tile
-constexpr int kTile = kPartBlock * kPartItems;         // 8192 requests per tile
+#ifndef TBE_PART_BLOCK
+#define TBE_PART_BLOCK 512
+#endif
+#ifndef TBE_PART_ITEMS
+#define TBE_PART_ITEMS 8
+#endif
+constexpr int kPartBlock = TBE_PART_BLOCK;             // partition workgroup
+constexpr int kPartItems = TBE_PART_ITEMS;             // elements per thread per tile
+constexpr int kTile = kPartBlock * kPartItems;         // 4096 requests per partition tile
+// k_unscatter's own tiles (any size is correct; 8192 keeps each workgroup's gathers in
+// the digit runs of two partition tiles)
+constexpr int kUnBlock = 1024;
+constexpr int kUnItems = 8;
+constexpr int kUnTile = kUnBlock * kUnItems;
 constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
 constexpr int kMaxHistBlocks = 1024;
 constexpr int kFoldItems = 8;                          // requests per thread per chunk
@@ -54,20 +65,70 @@ constexpr int kChunk = kBlock * kFoldItems;            // 2048
 constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
 constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
+// Hot keys (see the "hot keys" section below for how their runs are decided).
+constexpr uint32_t kHotKeysMax = 1024;
+constexpr uint32_t kHotSlots = 2048;             // hash slots: power of two >= 2 * kHotKeysMax
+constexpr uint32_t kHotEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kHotMin = 2048;               // requests in one batch that make a key hot
+
+struct HotSet {
+    uint32_t count;                  // hot keys in use this batch (index h -> bucket nb + h)
+    uint32_t n_cand;                 // nominations for the following batch
+    uint32_t key[kHotKeysMax];
+    uint32_t cand[kHotKeysMax];
+    uint32_t slot_key[kHotSlots];    // open-addressing hash table: key -> index
+    uint32_t slot_idx[kHotSlots];
+};
+
+__device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 21; }
+
+// Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns
+// whether any key is hot.
+template <int BLOCK>
+__device__ __forceinline__ bool hot_load(const HotSet *__restrict__ hot, uint32_t *sk, uint32_t *si) {
+    const bool any = hot != nullptr && hot->count != 0;
+    if (any)
+        for (int j = threadIdx.x; j < (int)kHotSlots; j += BLOCK) {
+            sk[j] = hot->slot_key[j];
+            si[j] = hot->slot_idx[j];
+        }
+    __syncthreads();
+    return any;
+}
+
+// Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
+__device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint32_t *sk, const uint32_t *si,
+                                                uint32_t nb, int r_bits) {
+    uint32_t h = hot_hash(key);
+    for (;;) {
+        const uint32_t k = sk[h];
+        if (k == key) return (nb + si[h]) << r_bits;
+        if (k == kHotEmpty) return key;
+        h = (h + 1) & (kHotSlots - 1);
+    }
+}
+
 // ----------------------------------------------------------------------------- kernels
 // Per-tile digit histograms.  Block j walks tiles [j*tpb, (j+1)*tpb) in order and
 // writes for each tile the exclusive running count per digit within its block
 // (tileprefix) and, at the end, the block's totals (blocksum).  Pass 0 also validates
-// keys (key < n_keys).  Digits come from the 32-bit key exactly as k_scatter computes
-// them, so counts stay consistent even for an (invalid) key >= 2^32.
-template <typename KeyT>
+// keys (key < n_keys).  Digits come from the key bits under `kmask` (the low 32 bits, or
+// a packed record's key field) exactly as the scatter computes them, so counts stay
+// consistent even for an (invalid) key >= 2^32.
+// HOT (first pass of a token-bucket batch with hot runs): a hot key's digits come from
+// its run's partition key (hot_sortkey), as in k_scatter_rec<true, true>.
+template <typename KeyT, bool HOT = false>
 __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
                                                  int shift, uint32_t tiles_per_blk,
                                                  uint32_t ntiles, uint32_t *__restrict__ tileprefix,
                                                  uint32_t *__restrict__ blocksum, uint64_t n_keys,
-                                                 uint32_t *__restrict__ err, int validate) {
+                                                 uint32_t *__restrict__ err, int validate,
+                                                 uint64_t kmask, const HotSet *__restrict__ hot = nullptr,
+                                                 uint32_t nb = 0, int r_bits = 0) {
     __shared__ uint32_t h[kDigits];
+    __shared__ uint32_t hk[HOT ? kHotSlots : 1], hi[HOT ? kHotSlots : 1];
     const int tid = threadIdx.x;
+    const bool any_hot = HOT && hot_load<kBlock>(hot, hk, hi);
     const uint32_t t0 = blockIdx.x * tiles_per_blk;
     const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
     uint32_t run = 0;
@@ -87,7 +148,9 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
             const uint64_t i = base + it * kBlock + tid;
             if (i < n) {
                 bad |= validate && ((uint64_t)kv[it] >= n_keys);
-                atomicAdd(&h[((uint32_t)kv[it] >> shift) & (kDigits - 1)], 1u);
+                uint32_t sk = (uint32_t)((uint64_t)kv[it] & kmask);
+                if (HOT && any_hot) sk = hot_sortkey((uint32_t)kv[it], hk, hi, nb, r_bits);
+                atomicAdd(&h[(sk >> shift) & (kDigits - 1)], 1u);
             }
         }
         __syncthreads();
@@ -251,20 +314,38 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
 
 // bstart[b] = first sorted position with bucket >= b, for b in [0, nb]; bstart[nb] = n.
 // Four sorted keys per thread.
-__global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t *__restrict__ skeys, uint64_t n,
-                                                   int r_bits, uint32_t nb,
+// KeyT: u32 sorted keys, or u64 packed records (key under kmask).
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k_bounds(const KeyT *__restrict__ skeys, uint64_t n,
+                                                   int r_bits, uint32_t nb, uint64_t kmask,
                                                    uint32_t *__restrict__ bstart,
                                                    const uint32_t *__restrict__ err) {
     if (*err) return;
     const uint64_t i0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     if (i0 >= n) return;
-    int64_t prev = (i0 == 0) ? -1 : (int64_t)(skeys[i0 - 1] >> r_bits);
+    auto kof = [&](KeyT x) { return (uint32_t)((uint64_t)x & kmask); };
+    int64_t prev = (i0 == 0) ? -1 : (int64_t)(kof(skeys[i0 - 1]) >> r_bits);
     uint32_t k4[4];
     if (i0 + 4 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(skeys + i0);
-        k4[0] = v.x; k4[1] = v.y; k4[2] = v.z; k4[3] = v.w;
+        // 16-byte vector loads: one for four u32 keys, two for four packed records
+        constexpr int V = sizeof(KeyT) * 4 / 16;
+        uint4 v[V];
+#pragma unroll
+        for (int w = 0; w < V; ++w) v[w] = reinterpret_cast<const uint4 *>(skeys + i0)[w];
+        if (sizeof(KeyT) == 4) {
+            k4[0] = v[0].x; k4[1] = v[0].y; k4[2] = v[0].z; k4[3] = v[0].w;
+        } else {
+            k4[0] = kof((KeyT)(((uint64_t)v[0].y << 32) | v[0].x));
+            k4[1] = kof((KeyT)(((uint64_t)v[0].w << 32) | v[0].z));
+            k4[2] = kof((KeyT)(((uint64_t)v[V - 1].y << 32) | v[V - 1].x));
+            k4[3] = kof((KeyT)(((uint64_t)v[V - 1].w << 32) | v[V - 1].z));
+        }
+        if (sizeof(KeyT) == 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) k4[u] = kof((KeyT)k4[u]);
     } else {
-        for (int u = 0; u < 4; ++u) k4[u] = (i0 + u < n) ? skeys[i0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k4[u] = (i0 + u < n) ? kof(skeys[i0 + u]) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -278,39 +359,160 @@ __global__ __launch_bounds__(kBlock) void k_bounds(const uint32_t *__restrict__ 
     }
 }
 
+// Packed request records (token-bucket kind).  When the key, a permit code and a
+// 32-bit time offset fit one u64, the partition passes and the fold move one 8-byte
+// record per request instead of {key u32, permits i32, ts i64}:
+//
+//   bits [0, kb)            key (< n_keys <= 2^kb)
+//   bits [kb, kb+pb)        permit code min(permits, TokenLimit + 1): x <= TokenLimit
+//                           always (TB:221), so every larger request is decided, and
+//                           leaves the state, exactly like TokenLimit + 1 (TB:224)
+//   bit  kb+pb              escape
+//   bits [kb+pb+1, 64)      ts - base  (base = ts[0] of the batch - 2^(wb-1)), or, with
+//                           the escape bit, the arrival index: the fold then reads the
+//                           request's timestamp from the caller's array
+//
+// wb = 64 - kb - pb - 1 >= 32, so a batch whose timestamps lie within +-35 minutes of
+// its first one never escapes.
+struct PackFmt {
+    uint64_t kmask;     // (1 << kb) - 1
+    int32_t kb;
+    int32_t pb;
+    int32_t pc_max;     // TokenLimit + 1
+    int32_t wb;
+};
+__device__ __forceinline__ int64_t pack_base(const int64_t *__restrict__ ts, const PackFmt &F) {
+    return ts[0] - ((int64_t)1 << (F.wb - 1));
+}
+__device__ __forceinline__ uint64_t pack_rec(uint64_t key, int32_t p, int64_t ts, uint64_t idx,
+                                             int64_t tbase, const PackFmt &F) {
+    const uint64_t pc = (uint64_t)(p < 0 ? 0 : (p > F.pc_max ? F.pc_max : p));
+    const uint64_t d = (uint64_t)ts - (uint64_t)tbase;
+    const bool fits = ts >= tbase && (d >> F.wb) == 0;
+    const uint64_t pay = fits ? d : idx;
+    return (key & F.kmask) | (pc << F.kb) | ((uint64_t)!fits << (F.kb + F.pb)) |
+           (pay << (F.kb + F.pb + 1));
+}
+__device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restrict__ ts_orig,
+                                           int64_t tbase, const PackFmt &F, uint32_t &key,
+                                           int32_t &p, int64_t &ts) {
+    key = (uint32_t)(rec & F.kmask);
+    p = (int32_t)((rec >> F.kb) & ((1ull << F.pb) - 1));
+    const uint64_t pay = rec >> (F.kb + F.pb + 1);
+    ts = ((rec >> (F.kb + F.pb)) & 1) ? ts_orig[pay] : (int64_t)((uint64_t)tbase + pay);
+}
+
+// Stable partition pass over packed records (see k_scatter; one 8-byte LDS staging
+// round instead of two).  FIRST: read the caller's arrays, validate permits and
+// timestamps, and pack; otherwise read the previous pass's records.
+// HOT (with FIRST): a hot key's record carries its run's partition key (hot_sortkey)
+// in the key field.
+template <bool FIRST, bool HOT = false>
+__global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
+    const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
+    const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
+    const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
+    const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
+    uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
+    uint32_t nb = 0, int r_bits = 0) {
+    __shared__ RankLds<kPartBlock> L;
+    __shared__ uint32_t goff[kDigits];
+    __shared__ uint64_t stage[kTile];
+    __shared__ uint32_t hk[HOT ? kHotSlots : 1], hi[HOT ? kHotSlots : 1];
+    const bool any_hot = HOT && hot_load<kPartBlock>(hot, hk, hi);
+    static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
+
+    const int tid = threadIdx.x;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kTile;
+    const int nvalid = (int)min<uint64_t>(kTile, n - base);
+
+    uint64_t rec[kPartItems];
+    uint32_t key[kPartItems], lpos[kPartItems];
+    bool bad = false;
+    if (FIRST) {
+        uint64_t kv[kPartItems];
+        int32_t pv[kPartItems];
+        int64_t tv[kPartItems];
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            const bool v = e < nvalid;
+            kv[it] = v ? kin[base + e] : 0ull;
+            pv[it] = v ? pin[base + e] : 0;
+            tv[it] = v ? tin[base + e] : 0;
+        }
+        const int64_t tbase = pack_base(tin, F);
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            bad |= (e < nvalid) && (pv[it] < 0 || tv[it] < 0);
+            uint64_t sk = kv[it] & F.kmask;
+            if (HOT && any_hot) sk = hot_sortkey((uint32_t)kv[it], hk, hi, nb, r_bits);
+            rec[it] = pack_rec(sk, pv[it], tv[it], base + e, tbase, F);
+            key[it] = (uint32_t)sk;
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            rec[it] = (e < nvalid) ? rin[base + e] : 0ull;
+            key[it] = (uint32_t)(rec[it] & F.kmask);
+        }
+    }
+    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
+    rank_tile<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint16_t *>(stage), lpos);
+    __syncthreads();   // the counts in `stage` are dead from here on
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = it * kPartBlock + tid;
+        if (e < nvalid) {
+            const uint32_t d = (key[it] >> shift) & (kDigits - 1);
+            stage[lpos[it]] = rec[it];
+            perm[base + e] = goff[d] + lpos[it] - L.lstart[d];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int j = it * kPartBlock + tid;
+        if (j < nvalid) {
+            const uint64_t s = stage[j];
+            const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
+            rout[goff[d] + (uint32_t)j - L.lstart[d]] = s;
+        }
+    }
+    if (FIRST && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
+}
+
 // Decide every request of one bucket (see file header).  res[q] is the packed reply of
 // sorted request q (bit 31 granted, bits 0-30 remaining).
 //
-// State of the bucket's R keys lives in LDS as SoA {v, t (f64 field t), tp (packed
-// grant time)}; a dense bucket (>= R/8 requests) pulls its whole 16*R-byte slice of the
-// table with coalesced loads and writes it back whole, a sparse one pulls and writes
-// back only the rows it touches.  Per chunk of 2048 requests (arrival order), every
-// request first computes its state-independent times (req_time, in parallel); then
-// rounds elect, per key, the earliest pending request (LDS atomicMax on a round-tagged
-// slot), which applies the cheap serial step tb_step.  Replies are staged in LDS and
-// leave as one coalesced store per chunk.
+// The bucket's R table rows live in LDS as stored ({v, t_us}, 16 B) plus the row's
+// field t as f64 (ft, TB:203 applied to t_us), derived once when a request first
+// touches the row and replaced by the request's own new_t on a grant.  A dense bucket
+// (>= R/8 requests) pulls its whole 16*R-byte slice with coalesced loads, issued
+// together with its first chunk of requests, and writes it back whole; a sparse one
+// pulls and writes back only the rows it touches.  Requests go in chunks of 2048
+// (arrival order): each computes its state-independent times in parallel, then
+// speculative rounds (below) decide them.  Replies stay in registers and leave as one
+// coalesced store per chunk.
 constexpr int kFoldBlock = 512;
 constexpr int kFoldPer = 4;                                 // requests per thread per chunk
 constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
 constexpr int kMaxRows = 1 << kMaxRBits;
 
-__device__ __forceinline__ void load_row(const Slot &row, double *sv, double *st, int64_t *stp,
-                                         uint32_t j) {
-    sv[j] = row.v;
-    st[j] = (row.t_us == kAbsent) ? 0.0 : new_t_of(row.t_us);
-    stp[j] = (row.t_us == kAbsent) ? kAbsent : tpack_of(row.t_us);
-}
-
-__global__ __launch_bounds__(kFoldBlock, 2) void k_fold(
+template <bool PACKED>
+__global__ __launch_bounds__(kFoldBlock) void k_fold(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
-    const int64_t *__restrict__ sts, const uint32_t *__restrict__ bstart, int r_bits,
-    uint64_t n_keys, Slot *__restrict__ table, TbParams P, uint32_t *__restrict__ res,
-    const uint32_t *__restrict__ err) {
-    __shared__ double sv[kMaxRows];
-    __shared__ double st[kMaxRows];
-    __shared__ int64_t stp[kMaxRows];
+    const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
+    const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
+    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
+    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next) {
+    __shared__ Slot row[kMaxRows];
+    __shared__ uint32_t hcnt[kMaxRows];   // requests per row, in buckets that may hold a hot key
+    __shared__ double ft[kMaxRows];
     __shared__ uint32_t own[kMaxRows];
-    __shared__ uint32_t rbuf[kFoldChunk];
     __shared__ uint32_t loaded[kMaxRows / 32];
     __shared__ uint32_t dirty[kMaxRows / 32];
 
@@ -324,55 +526,70 @@ __global__ __launch_bounds__(kFoldBlock, 2) void k_fold(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-#ifdef TBE_ABLATE_SKIP_TABLE
-    const bool dense = true;
-#else
     const bool dense = (e - s) >= (R >> 3);
-#endif
+    const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
 
-#ifdef TBE_ABLATE_SKIP_TABLE
-    for (uint32_t j = tid; j < R; j += kFoldBlock) { sv[j] = P.cap; st[j] = 0.0; stp[j] = kAbsent; }
-#else
+    uint32_t kl[kFoldPer];
+    int32_t pm[kFoldPer];
+    int64_t tsv[kFoldPer];
+    uint32_t pend = 0;
+    auto load_chunk = [&](uint32_t c) {
+        pend = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            kl[r] = 0;
+            pm[r] = 0;
+            tsv[r] = 0;
+            if (q < e) {
+                if (PACKED) {
+                    uint32_t k;
+                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], tsv[r]);
+                    kl[r] = k & rmask;
+                } else {
+                    kl[r] = skeys[q] & rmask;
+                    pm[r] = sperm[q];
+                    tsv[r] = sts[q];
+                }
+                pend |= 1u << r;
+            }
+        }
+    };
+    load_chunk(s);   // in flight together with the dense slice
     if (dense) {
         constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
         Slot tmp[kRowsPerThread];
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
             const uint32_t j = tid + u * kFoldBlock;
-            if (j < nrows) tmp[u] = rows[j];
+            tmp[u] = rows[j < nrows ? j : nrows - 1];   // unconditional: keeps tmp in VGPRs
         }
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
             const uint32_t j = tid + u * kFoldBlock;
-            if (j < nrows) load_row(tmp[u], sv, st, stp, j);
+            if (j < nrows) row[j] = tmp[u];
         }
     }
-#endif
     for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
         loaded[j] = 0;
         dirty[j] = 0;
     }
 
     for (uint32_t c = s; c < e; c += kFoldChunk) {
+        if (c != s) load_chunk(c);
         for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
-        uint32_t kl[kFoldPer];
-        int32_t pm[kFoldPer];
-        int64_t tsv[kFoldPer];
-        uint32_t pend = 0;
+        if (count_hot && c == s)
+            for (uint32_t j = tid; j < R; j += kFoldBlock) hcnt[j] = 0;
+        __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
+        if (count_hot) {
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
-            const uint32_t q = c + r * kFoldBlock + tid;
-            kl[r] = 0; pm[r] = 0; tsv[r] = 0;
-            if (q < e) {
-                kl[r] = skeys[q] & rmask;
-                pm[r] = sperm[q];
-                tsv[r] = sts[q];
-                pend |= 1u << r;
-            }
+            for (int r = 0; r < kFoldPer; ++r)
+                if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
         }
-        __syncthreads();   // own[] reset and (first chunk) dense slice visible
-        if (!dense) {
-            // First touch of a row in this bucket pulls it into LDS: claim, load, store.
+        {
+            // First touch of a row in this bucket: claim it, pull it into LDS (sparse
+            // buckets) and derive its field t.
             uint32_t mine = 0;
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
@@ -383,66 +600,81 @@ __global__ __launch_bounds__(kFoldBlock, 2) void k_fold(
             }
             Slot tmp[kFoldPer];
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
-                if (mine & (1u << r)) tmp[r] = rows[kl[r]];
+            for (int r = 0; r < kFoldPer; ++r) {
+                tmp[r] = Slot{0.0, 0};                   // fully initialised: stays in VGPRs
+                if (mine & (1u << r)) tmp[r] = dense ? row[kl[r]] : rows[kl[r]];
+            }
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
-                if (mine & (1u << r)) load_row(tmp[r], sv, st, stp, kl[r]);
+            for (int r = 0; r < kFoldPer; ++r) {
+                if (mine & (1u << r)) {
+                    if (!dense) row[kl[r]] = tmp[r];
+                    ft[kl[r]] = new_t_of(tmp[r].t_us == kAbsent ? 0 : tmp[r].t_us);
+                }
+            }
         }
         ReqTime rq[kFoldPer];
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) rq[r] = req_time(tsv[r]);
-        if (!dense) __syncthreads();
-#ifdef TBE_ABLATE_SKIP_ROUNDS
+        __syncthreads();   // claimed rows and their field t visible
+        uint32_t rep[kFoldPer];
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r)
-            if (pend & (1u << r)) rbuf[r * kFoldBlock + tid] = (uint32_t)rq[r].new_t + (uint32_t)pm[r] + kl[r];
-        pend = 0;
-        if (__syncthreads_or(0))
-#endif
-        // Rounds: slot value (round << 12) | (4095 - local id); the max is the earliest
-        // pending request of the key in the newest round, so no reset between rounds.
-        // Workgroup-uniform loop: every thread runs every round (barriers inside) and the
-        // only exit is the __syncthreads_or below.
+        for (int r = 0; r < kFoldPer; ++r) rep[r] = 0;
+        // Speculative rounds.  Every pending request evaluates the script
+        // against its key's current row.  An evaluation that does not modify the row (a
+        // deny without expiry) leaves it as it found it, so the key's pending requests up
+        // to its earliest modifying one are decided by this round's evaluations; that
+        // earliest one commits the row it computed and later ones wait for the next
+        // round.  A key whose requests in the chunk all deny settles in one round.
+        // Election slot: (round << 12) | (4095 - local id); the max is the key's earliest
+        // modifier of the newest round, so no reset between rounds.  Workgroup-uniform
+        // loop: every thread runs every round and the only exit is the __syncthreads_or.
         for (uint32_t round = 1;; ++round) {
+            Slot nrow[kFoldPer];
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
-                if (pend & (1u << r))
-                    atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
+            for (int r = 0; r < kFoldPer; ++r) {
+                nrow[r] = Slot{0.0, 0};
+                if (pend & (1u << r)) {
+                    nrow[r] = row[kl[r]];
+                    bool m;
+                    rep[r] = tb_step_ft(nrow[r], ft[kl[r]], pm[r], rq[r], P, m);
+                    if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
+                }
+            }
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
+                if (!(pend & (1u << r))) continue;
                 const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid));
-                if ((pend & (1u << r)) && own[kl[r]] == tag) {
-                    double v = sv[kl[r]], t = st[kl[r]];
-                    int64_t tp = stp[kl[r]];
-                    bool modified;
-                    rbuf[r * kFoldBlock + tid] = tb_step(v, t, tp, pm[r], rq[r], P, modified);
-                    if (modified) {
-                        sv[kl[r]] = v;
-                        st[kl[r]] = t;
-                        stp[kl[r]] = tp;
-                        if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
-                    }
+                const uint32_t o = own[kl[r]];
+                if ((o >> 12) != round || o < tag) {
+                    pend &= ~(1u << r);             // before the key's first modifier: decided
+                } else if (o == tag) {
+                    row[kl[r]] = nrow[r];           // the row this round's evaluation produced
+                    ft[kl[r]] = rq[r].new_t;        // its field t (unused while absent)
+                    if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     pend &= ~(1u << r);
                 }
             }
             if (!__syncthreads_or(pend != 0)) break;
         }
-        __syncthreads();
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            if (q < e) res[q] = rbuf[r * kFoldBlock + tid];
+            if (q < e) res[q] = rep[r];
         }
     }
     __syncthreads();
-#ifdef TBE_ABLATE_SKIP_TABLE
-    if (sv[tid] == -1.0) rows[tid] = Slot{sv[tid], ts_of_tpack(stp[tid])};
-    return;
-#endif
     for (uint32_t j = tid; j < nrows; j += kFoldBlock)
-        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) rows[j] = Slot{sv[j], ts_of_tpack(stp[j])};
+        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) rows[j] = row[j];
+    if (count_hot) {
+        // nominate this bucket's hot keys for their own runs in the next batch
+        for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
+            if (hcnt[j] >= kHotMin) {
+                const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
+                if (at < kHotKeysMax) hot_next->cand[at] = (uint32_t)(row0 + j);
+            }
+        }
+    }
 }
 
 // Inverse of one k_scatter pass: out[i] = in[perm[i]] with perm the positions that pass
@@ -455,31 +687,31 @@ __device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, u
 }
 
 template <bool FINAL, bool WAIT>
-__global__ __launch_bounds__(kPartBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
+__global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
                                                           const uint32_t *__restrict__ res_in,
                                                           uint32_t *__restrict__ res_out,
                                                           uint8_t *__restrict__ granted,
                                                           int32_t *__restrict__ remaining) {
-    // One workgroup per partition tile (same tiles and XCD mapping as k_scatter): the
-    // tile's 8192 gathers land in its 256 digit runs, which stay in this CU's L1 / XCD L2.
+    // One workgroup per 8192 positions, XCD-aware like k_scatter: the tile's gathers land
+    // in the digit runs of the partition tiles it covers, which stay in this XCD's L2.
     const int tid = threadIdx.x;
     const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kTile;
-    const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    uint32_t pv[kPartItems], r[kPartItems];
+    const uint64_t base = (uint64_t)tile * kUnTile;
+    const int nvalid = (int)min<uint64_t>(kUnTile, n - base);
+    uint32_t pv[kUnItems], r[kUnItems];
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
         pv[it] = (e < nvalid) ? perm[base + e] : 0u;
     }
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
         r[it] = (e < nvalid) ? res_in[pv[it]] : 0u;
     }
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
         if (FINAL && WAIT) {
@@ -493,6 +725,288 @@ __global__ __launch_bounds__(kPartBlock) void k_unscatter(uint64_t n, const uint
             res_out[i] = r[it];
         }
     }
+}
+
+// ----------------------------------------------------------------------------- hot keys
+// Skewed traffic (SURVEY.md §8d config C, §7 hard part iii).  A key that takes at least
+// kHotMin requests of one batch becomes "hot" for the next batch: the first partition
+// pass gives its requests a bucket of their own (id nb + h, past the nb ordinary
+// buckets), so after the partition they form one run, in arrival order, instead of
+// filling one ordinary bucket's serial rounds.  A run is cut into segments of kSeg
+// requests:
+//   k_hot_summary  (parallel)  per segment: the latest timestamp and the smallest permit
+//                              code in it;
+//   k_hot_chain    (one workgroup per run) walks the segments in order carrying the
+//                  key's row S.  The script's decision is monotone in the request time
+//                  and in the permits: x never decreases with a later TIME (TB:218-221),
+//                  a request grants whenever a larger one does (TB:224), and passive
+//                  expiry only starts at a later time.  So if a segment's extreme request
+//                  (latest time, fewest permits) would leave S unmodified, every request
+//                  of the segment does: the segment passes S through.  Segments that may
+//                  modify S are decided here, serially, with the fold's speculative
+//                  rounds;
+//   k_hot_replies  (parallel)  decides every request of a pass-through segment against
+//                              the S it saw.
+// Which keys are hot only changes speed, never a decision.
+constexpr int kSegBlock = kFoldBlock;
+constexpr int kSegItems = 16;
+constexpr uint32_t kSeg = kSegBlock * kSegItems;  // 8192 requests per run segment
+
+struct SegSummary {
+    int64_t max_ts;
+    int32_t min_p;
+    uint32_t pad;
+};
+struct SegState {
+    Slot s;          // the run's row when the segment starts
+    double ft;       // its field t
+    uint32_t pass;   // 1: no request of the segment modifies s (k_hot_replies decides it)
+    uint32_t pad;
+};
+
+
+// segbase[h] = first segment of run h; segbase[kHotKeysMax] = all segments.  One 1024-
+// thread workgroup.
+__global__ __launch_bounds__(1024) void k_hot_plan(const HotSet *__restrict__ hot,
+                                                   const uint32_t *__restrict__ bstart, uint32_t nb,
+                                                   uint32_t *__restrict__ segbase,
+                                                   const uint32_t *__restrict__ err) {
+    __shared__ uint32_t wsum[16];
+    if (*err) return;
+    const uint32_t h = threadIdx.x;
+    uint32_t ns = 0;
+    if (h < hot->count) ns = (bstart[nb + h + 1] - bstart[nb + h] + kSeg - 1) / kSeg;
+    uint32_t total;
+    const uint32_t pre = block_excl_scan<1024>(ns, wsum, &total);
+    segbase[h] = pre;
+    if (h == 0) segbase[kHotKeysMax] = total;
+}
+
+// Run h of segment j: the last h with segbase[h] <= j.
+__device__ __forceinline__ uint32_t seg_run(const uint32_t *__restrict__ segbase, uint32_t j) {
+    uint32_t lo = 0, hi = kHotKeysMax;   // segbase[lo] <= j < segbase[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segbase[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kSegBlock) void k_hot_summary(
+    const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
+    const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
+    SegSummary *__restrict__ summ, const uint32_t *__restrict__ err) {
+    __shared__ int64_t wts[kSegBlock / 64];
+    __shared__ int32_t wp[kSegBlock / 64];
+    if (*err) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t total = segbase[kHotKeysMax];
+    const int64_t tbase = pack_base(ts_orig, F);
+    for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
+        const uint32_t h = seg_run(segbase, j);
+        const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
+        const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
+        int64_t mx = INT64_MIN;
+        int32_t mn = INT32_MAX;
+        for (uint32_t q = a + tid; q < b; q += kSegBlock) {
+            uint32_t k;
+            int32_t p;
+            int64_t ts;
+            unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
+            mx = max(mx, ts);
+            mn = min(mn, p);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
+            mn = min(mn, __shfl_xor(mn, o, 64));
+        }
+        if (lane == 0) {
+            wts[w] = mx;
+            wp[w] = mn;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int u = 1; u < kSegBlock / 64; ++u) {
+                mx = max(mx, wts[u]);
+                mn = min(mn, wp[u]);
+            }
+            summ[j] = SegSummary{mx, mn, 0u};
+        }
+        __syncthreads();
+    }
+}
+
+// One workgroup per run (see the section comment).
+__global__ __launch_bounds__(kSegBlock) void k_hot_chain(
+    const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
+    const uint32_t *__restrict__ bstart, uint32_t nb, const HotSet *__restrict__ hot,
+    HotSet *__restrict__ hot_next, const uint32_t *__restrict__ segbase,
+    const SegSummary *__restrict__ summ, SegState *__restrict__ sst, Slot *__restrict__ table,
+    TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err) {
+    __shared__ Slot S;
+    __shared__ double ftS;
+    __shared__ uint32_t first, own;
+    if (*err) return;
+    const uint32_t h = blockIdx.x;
+    if (h >= hot->count) return;
+    const int tid = threadIdx.x;
+    const uint32_t key = hot->key[h];
+    const uint32_t s0 = bstart[nb + h], e0 = bstart[nb + h + 1];
+    if (s0 == e0) return;
+    const uint32_t j0 = segbase[h], nseg = segbase[h + 1] - j0;
+    const int64_t tbase = pack_base(ts_orig, F);
+    if (tid == 0) {
+        S = table[key];
+        ftS = new_t_of(S.t_us == kAbsent ? 0 : S.t_us);
+    }
+    __syncthreads();
+    bool touched = false;
+    uint32_t cur = 0;
+    while (cur < nseg) {
+        // the first segment at or after `cur` that may modify S
+        const Slot s = S;
+        const double ft = ftS;
+        uint32_t f = nseg;
+        for (uint32_t u = cur + tid; u < nseg; u += kSegBlock) {
+            const SegSummary sm = summ[j0 + u];
+            Slot c = s;
+            bool m;
+            (void)tb_step_ft(c, ft, sm.min_p, req_time(sm.max_ts), P, m);
+            if (m) {
+                f = u;
+                break;
+            }
+        }
+        if (tid == 0) first = nseg;
+        __syncthreads();
+        atomicMin(&first, f);
+        __syncthreads();
+        f = first;
+        for (uint32_t u = cur + tid; u < f; u += kSegBlock) sst[j0 + u] = SegState{s, ft, 1u, 0u};
+        if (f == nseg) break;
+        if (tid == 0) sst[j0 + f].pass = 0u;
+        touched = true;
+        // decide segment f here, 2048 requests at a time, in speculative rounds
+        const uint32_t a = s0 + f * kSeg, b = min(a + kSeg, e0);
+        for (uint32_t c = a; c < b; c += kFoldChunk) {
+            int32_t pm[kFoldPer];
+            ReqTime rq[kFoldPer];
+            uint32_t rep[kFoldPer], pend = 0;
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r) {
+                const uint32_t q = c + r * kSegBlock + tid;
+                int64_t ts = 0;
+                pm[r] = 0;
+                rep[r] = 0;
+                if (q < b) {
+                    uint32_t k;
+                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts);
+                    pend |= 1u << r;
+                }
+                rq[r] = req_time(ts);
+            }
+            if (tid == 0) own = 0;
+            __syncthreads();
+            for (uint32_t round = 1;; ++round) {
+                const Slot sc = S;
+                const double fc = ftS;
+                Slot nrow[kFoldPer];
+#pragma unroll
+                for (int r = 0; r < kFoldPer; ++r) {
+                    nrow[r] = sc;
+                    if (pend & (1u << r)) {
+                        bool m;
+                        rep[r] = tb_step_ft(nrow[r], fc, pm[r], rq[r], P, m);
+                        if (m) atomicMax(&own, (round << 12) | (4095u - (uint32_t)(r * kSegBlock + tid)));
+                    }
+                }
+                __syncthreads();
+                const uint32_t o = own;
+#pragma unroll
+                for (int r = 0; r < kFoldPer; ++r) {
+                    if (!(pend & (1u << r))) continue;
+                    const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kSegBlock + tid));
+                    if ((o >> 12) != round || o < tag) {
+                        pend &= ~(1u << r);
+                    } else if (o == tag) {
+                        S = nrow[r];
+                        ftS = rq[r].new_t;
+                        pend &= ~(1u << r);
+                    }
+                }
+                if (!__syncthreads_or(pend != 0)) break;
+            }
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r) {
+                const uint32_t q = c + r * kSegBlock + tid;
+                if (q < b) res[q] = rep[r];
+            }
+        }
+        __syncthreads();
+        cur = f + 1;
+    }
+    if (tid == 0) {
+        if (touched) table[key] = S;
+        if (e0 - s0 >= kHotMin / 2) {                 // still hot: nominate again
+            const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
+            if (at < kHotKeysMax) hot_next->cand[at] = key;
+        }
+    }
+}
+
+// Replies of the pass-through segments: each request against the row its segment saw.
+__global__ __launch_bounds__(kSegBlock) void k_hot_replies(
+    const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
+    const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
+    const SegState *__restrict__ sst, TbParams P, uint32_t *__restrict__ res,
+    const uint32_t *__restrict__ err) {
+    if (*err) return;
+    const int tid = threadIdx.x;
+    const uint32_t total = segbase[kHotKeysMax];
+    const int64_t tbase = pack_base(ts_orig, F);
+    for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
+        const SegState st = sst[j];
+        if (!st.pass) continue;
+        const uint32_t h = seg_run(segbase, j);
+        const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
+        const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
+        for (uint32_t q = a + tid; q < b; q += kSegBlock) {
+            uint32_t k;
+            int32_t p;
+            int64_t ts;
+            unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
+            Slot c = st.s;
+            bool m;
+            res[q] = tb_step_ft(c, st.ft, p, req_time(ts), P, m);
+        }
+    }
+}
+
+// The next batch's hot set from this batch's nominations (one 1024-thread workgroup).
+__global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, uint32_t cap,
+                                                     const uint32_t *__restrict__ err) {
+    if (*err) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nc = min(next->n_cand, cap);
+    const uint32_t k = (t < nc) ? next->cand[t] : kHotEmpty;
+    for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot_key[j] = kHotEmpty;
+    __syncthreads();
+    if (t < nc) {
+        next->key[t] = k;
+        uint32_t h = hot_hash(k);
+        for (;;) {
+            const uint32_t old = atomicCAS(&next->slot_key[h], kHotEmpty, k);
+            if (old == kHotEmpty) {
+                next->slot_idx[h] = t;
+                break;
+            }
+            if (old == k) break;                    // nominated twice: one run is enough
+            h = (h + 1) & (kHotSlots - 1);
+        }
+    }
+    if (t == 0) next->count = nc;
 }
 
 // ----------------------------------------------------------------------------- queueing kind
@@ -579,8 +1093,11 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
             Slot tmp[kFoldItems];
             uint64_t th[kFoldItems];
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
+            for (int r = 0; r < kFoldItems; ++r) {
+                tmp[r] = Slot{0.0, 0};
+                th[r] = 0;
                 if (mine & (1u << r)) { tmp[r] = rows[kl[r]]; th[r] = hrows[kl[r]]; }
+            }
 #pragma unroll
             for (int r = 0; r < kFoldItems; ++r)
                 if (mine & (1u << r)) { slot[kl[r]] = tmp[r]; qh[kl[r]] = th[r]; }
@@ -817,8 +1334,10 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
         {
             ALocal tmp[kFoldPer];
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
+            for (int r = 0; r < kFoldPer; ++r) {
+                tmp[r] = ALocal{0, 0, 0, 0u};
                 if (mine & (1u << r)) tmp[r] = rows[kl[r]];
+            }
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r)
                 if (mine & (1u << r)) sl[kl[r]] = tmp[r];
@@ -1022,9 +1541,10 @@ __global__ void k_sticky(const uint32_t *__restrict__ err, uint32_t *__restrict_
 }
 
 // ----------------------------------------------------------------------------- host side
-enum Stage { ST_HIST = 0, ST_COLSCAN, ST_SCATTER, ST_BOUNDS, ST_FOLD, ST_UNSCATTER, ST_COUNT };
+enum Stage { ST_HIST = 0, ST_COLSCAN, ST_SCATTER, ST_BOUNDS, ST_FOLD, ST_UNSCATTER, ST_HOT, ST_COUNT };
 
 struct PassBufs {
+    uint64_t *rec = nullptr;     // pass output, packed records (token bucket, PackFmt)
     uint32_t *keys = nullptr;    // pass output (u32 keys)
     int32_t *permits = nullptr;
     int64_t *ts = nullptr;
@@ -1052,6 +1572,16 @@ struct tbe_engine {
     int r_bits = 0;          // bucket = key >> r_bits
     uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
     int passes = 0;          // 8-bit LSD passes over the bucket id
+    bool packed = false;     // token bucket: passes move packed u64 records (PackFmt)
+    PackFmt pf{};
+    // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys
+    uint32_t hot_cap = 0;
+    uint32_t nb_total = 0;
+    HotSet *hot[2] = {nullptr, nullptr};   // this batch's set / the next batch's, alternating
+    int hot_cur = 0;
+    uint32_t *segbase = nullptr;
+    SegSummary *summ = nullptr;            // per run segment, sized with the workspace
+    SegState *sst = nullptr;
     Slot *table = nullptr;
     // queueing kind
     QParams qp{};
@@ -1129,6 +1659,7 @@ void dfree(T *&p) {
 
 void free_workspace(tbe_engine *e) {
     for (auto &pb : e->pass) {
+        dfree(pb.rec);
         dfree(pb.keys);
         dfree(pb.permits);
         dfree(pb.ts);
@@ -1140,6 +1671,8 @@ void free_workspace(tbe_engine *e) {
     }
     e->pass.clear();
     dfree(e->blocksum);
+    dfree(e->summ);
+    dfree(e->sst);
     dfree(e->res[0]);
     dfree(e->res[1]);
     dfree(e->d_keys);
@@ -1165,9 +1698,13 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
     tiles_for(cap, ntiles, nblk, tpb);
     e->pass.resize(e->passes);
     for (auto &pb : e->pass) {
-        HIP_TRY(e, hipMalloc(&pb.keys, cap * sizeof(uint32_t)));
-        HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
-        HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
+        if (e->packed) {
+            HIP_TRY(e, hipMalloc(&pb.rec, cap * sizeof(uint64_t)));
+        } else {
+            HIP_TRY(e, hipMalloc(&pb.keys, cap * sizeof(uint32_t)));
+            HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
+            HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
+        }
         HIP_TRY(e, hipMalloc(&pb.perm, cap * sizeof(uint32_t)));
         if (e->cfg.kind != TBE_KIND_TOKEN_BUCKET) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
@@ -1175,6 +1712,11 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.digit_total, kDigits * sizeof(uint32_t)));
     }
     HIP_TRY(e, hipMalloc(&e->blocksum, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
+    if (e->hot_cap) {
+        const uint64_t segs = cap / kSeg + kHotKeysMax + 1;
+        HIP_TRY(e, hipMalloc(&e->summ, segs * sizeof(SegSummary)));
+        HIP_TRY(e, hipMalloc(&e->sst, segs * sizeof(SegState)));
+    }
     HIP_TRY(e, hipMalloc(&e->res[0], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&e->res[1], cap * sizeof(uint32_t)));
     e->cap_n = cap;
@@ -1233,23 +1775,48 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     tiles_for(n, ntiles, nblk, tpb);
     HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(uint32_t), st));
 
+    const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
+    // hot runs: this batch partitions by hot[cur] and nominates into hot[cur ^ 1]
+    HotSet *hot = e->hot_cap ? e->hot[e->hot_cur] : nullptr;
+    HotSet *hot_next = e->hot_cap ? e->hot[e->hot_cur ^ 1] : nullptr;
+    if (hot_next) HIP_TRY(e, hipMemsetAsync(&hot_next->n_cand, 0, sizeof(uint32_t), st));
     for (int p = 0; p < e->passes; ++p) {
         const int shift = e->r_bits + kDigitBits * p;
         PassBufs &out = e->pass[p];
         stage_begin(e, ST_HIST, st);
-        if (p == 0)
+        if (p == 0 && hot)
+            k_hist<uint64_t, true><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+                                                             e->blocksum, e->cfg.n_keys, e->err, 1, kmask,
+                                                             hot, e->nbuckets, e->r_bits);
+        else if (p == 0)
             k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
-                                                       e->blocksum, e->cfg.n_keys, e->err, 1);
+                                                       e->blocksum, e->cfg.n_keys, e->err, 1, kmask);
+        else if (e->packed)
+            k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].rec, n, shift, tpb, ntiles,
+                                                       out.tileprefix, e->blocksum, e->cfg.n_keys,
+                                                       e->err, 0, kmask);
         else
             k_hist<uint32_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].keys, n, shift, tpb, ntiles,
                                                        out.tileprefix, e->blocksum, e->cfg.n_keys,
-                                                       e->err, 0);
+                                                       e->err, 0, kmask);
         stage_end(e, ST_HIST, st);
         stage_begin(e, ST_COLSCAN, st);
         k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, st);
         stage_begin(e, ST_SCATTER, st);
-        if (approx && p == 0)
+        if (e->packed && p == 0 && hot)
+            k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.rec, out.perm, e->err, hot, e->nbuckets, e->r_bits);
+        else if (e->packed && p == 0)
+            k_scatter_rec<true><<<ntiles, kPartBlock, 0, st>>>(
+                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.rec, out.perm, e->err);
+        else if (e->packed)
+            k_scatter_rec<false><<<ntiles, kPartBlock, 0, st>>>(
+                nullptr, nullptr, nullptr, e->pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, e->err);
+        else if (approx && p == 0)
             k_scatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
                 keys, permits, nullptr, nullptr, n, shift, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.perm, e->err, 1);
@@ -1280,8 +1847,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     }
     const PassBufs &sorted = e->pass[e->passes - 1];
     stage_begin(e, ST_BOUNDS, st);
-    k_bounds<<<(unsigned)((n + 4 * kBlock - 1) / (4 * kBlock)), kBlock, 0, st>>>(
-        sorted.keys, n, e->r_bits, e->nbuckets, e->bstart, e->err);
+    const unsigned bgrid = (unsigned)((n + 4 * kBlock - 1) / (4 * kBlock));
+    const uint32_t nb_total = e->packed ? e->nb_total : e->nbuckets;
+    if (e->packed)
+        k_bounds<uint64_t><<<bgrid, kBlock, 0, st>>>(sorted.rec, n, e->r_bits, nb_total, kmask,
+                                                     e->bstart, e->err);
+    else
+        k_bounds<uint32_t><<<bgrid, kBlock, 0, st>>>(sorted.keys, n, e->r_bits, nb_total, kmask,
+                                                     e->bstart, e->err);
     stage_end(e, ST_BOUNDS, st);
     stage_begin(e, ST_FOLD, st);
     if (approx) {
@@ -1300,24 +1873,46 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             sorted.keys, sorted.permits, sorted.ts, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->qhdr, e->ring, e->params, q, e->res[0], e->ev_cause, e->ev_id,
             e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), e->err);
+    } else if (e->packed) {
+        k_fold<true><<<e->nbuckets, kFoldBlock, 0, st>>>(
+            nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, e->bstart, e->r_bits, e->cfg.n_keys,
+            e->table, e->params, e->res[0], e->err, hot_next);
     } else {
-        k_fold<<<e->nbuckets, kFoldBlock, 0, st>>>(sorted.keys, sorted.permits, sorted.ts, e->bstart,
-                                               e->r_bits, e->cfg.n_keys, e->table, e->params,
-                                               e->res[0], e->err);
+        k_fold<false><<<e->nbuckets, kFoldBlock, 0, st>>>(
+            sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, e->bstart, e->r_bits,
+            e->cfg.n_keys, e->table, e->params, e->res[0], e->err, nullptr);
     }
     stage_end(e, ST_FOLD, st);
+    if (hot) {
+        // runs of this batch's hot keys, after the fold (which may write back a hot key's
+        // unchanged row as part of its bucket's slice), then the next batch's hot set
+        stage_begin(e, ST_HOT, st);
+        const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
+        k_hot_plan<<<1, 1024, 0, st>>>(hot, e->bstart, e->nbuckets, e->segbase, e->err);
+        k_hot_summary<<<sgrid, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets,
+                                                   e->segbase, e->summ, e->err);
+        k_hot_chain<<<e->hot_cap, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets, hot,
+                                                      hot_next, e->segbase, e->summ, e->sst, e->table,
+                                                      e->params, e->res[0], e->err);
+        k_hot_replies<<<sgrid, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets,
+                                                   e->segbase, e->sst, e->params, e->res[0], e->err);
+        k_hot_update<<<1, 1024, 0, st>>>(hot_next, e->hot_cap, e->err);
+        stage_end(e, ST_HOT, st);
+        e->hot_cur ^= 1;
+    }
     stage_begin(e, ST_UNSCATTER, st);
+    const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        k_unscatter<false, false><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[p].perm, e->res[cur],
+        k_unscatter<false, false><<<untiles, kUnBlock, 0, st>>>(n, e->pass[p].perm, e->res[cur],
                                                                 e->res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
     if (wait)
-        k_unscatter<true, true><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+        k_unscatter<true, true><<<untiles, kUnBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
                                                               nullptr, granted, remaining);
     else
-        k_unscatter<true, false><<<ntiles, kPartBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+        k_unscatter<true, false><<<untiles, kUnBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
                                                                nullptr, granted, remaining);
     stage_end(e, ST_UNSCATTER, st);
     k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
@@ -1386,6 +1981,37 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     const int bbits = ceil_log2(e->nbuckets);
     e->passes = std::max(1, (bbits + kDigitBits - 1) / kDigitBits);
     e->timing = (c.flags & TBE_FLAG_STAGE_TIMING) != 0;
+    {
+        // Packed records need key + permit code + a >= 32-bit time offset + escape bit.
+        // Hot runs (token bucket, packed) take bucket ids past the ordinary ones that the
+        // passes' digits already cover, and widen the key field to those ids.
+        int pbits = 0;
+        while (pbits < 32 && ((int64_t)1 << pbits) <= (int64_t)c.token_limit + 1) ++pbits;
+        auto layout = [&](uint32_t hot_cap) {
+            const uint64_t span = std::max<uint64_t>(c.n_keys, ((uint64_t)e->nbuckets + hot_cap) << e->r_bits);
+            const int kbits = std::max(1, ceil_log2(span));
+            e->pf.kb = kbits;
+            e->pf.pb = pbits;
+            e->pf.kmask = (kbits >= 64) ? ~0ull : ((1ull << kbits) - 1);
+            e->pf.pc_max = (c.token_limit == INT32_MAX) ? INT32_MAX : c.token_limit + 1;
+            e->pf.wb = 64 - kbits - pbits - 1;
+            return c.kind == TBE_KIND_TOKEN_BUCKET && e->pf.wb >= 32 && kbits <= 32 &&
+                   (c.flags & TBE_FLAG_NO_PACK) == 0;
+        };
+        uint32_t hot_cap = 0;
+        if ((c.flags & TBE_FLAG_NO_HOT) == 0) {
+            const uint64_t room = (1ull << (kDigitBits * e->passes)) - e->nbuckets;
+            hot_cap = (uint32_t)std::min<uint64_t>(kHotKeysMax, room);
+            if (hot_cap < 16) hot_cap = 0;
+        }
+        e->packed = hot_cap && layout(hot_cap);
+        if (!e->packed) {
+            hot_cap = 0;
+            e->packed = layout(0);
+        }
+        e->hot_cap = hot_cap;
+        e->nb_total = e->nbuckets + hot_cap;
+    }
 
     auto bail = [&](tbe_status st) {
         tbe_destroy(e);
@@ -1401,8 +2027,15 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         return bail(TBE_EDEVICE);
     e->own_stream = true;
     if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
-    if (hipMalloc(&e->bstart, ((uint64_t)e->nbuckets + 1) * sizeof(uint32_t)) != hipSuccess)
+    if (hipMalloc(&e->bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)) != hipSuccess)
         return bail(TBE_ENOMEM);
+    if (e->hot_cap) {
+        for (auto &hs : e->hot) {
+            if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
+            if (hipMemsetAsync(hs, 0, sizeof(HotSet), e->stream) != hipSuccess) return bail(TBE_EDEVICE);
+        }
+        if (hipMalloc(&e->segbase, (kHotKeysMax + 1) * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
+    }
     if (hipMalloc(&e->err, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     if (hipMemsetAsync(e->err, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess)
         return bail(TBE_EDEVICE);
@@ -1463,6 +2096,9 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->log_rem);
     dfree(e->bstart);
     dfree(e->err);
+    dfree(e->hot[0]);
+    dfree(e->hot[1]);
+    dfree(e->segbase);
     for (auto &ev : e->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
@@ -1856,6 +2492,14 @@ tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_
         permits[j] = (int32_t)(x & 0xFFFFu);
     }
     *count = cnt;
+    return TBE_OK;
+}
+
+tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, uint32_t *packed) {
+    if (!e || !passes || !r_bits || !packed) return TBE_EINVAL;
+    *passes = (uint32_t)e->passes;
+    *r_bits = (uint32_t)e->r_bits;
+    *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u);
     return TBE_OK;
 }
 

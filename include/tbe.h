@@ -67,6 +67,11 @@ typedef struct tbe_config {
 } tbe_config;
 
 #define TBE_FLAG_STAGE_TIMING 0x1u        /* record per-stage HIP events (tbe_stage_times) */
+#define TBE_FLAG_NO_PACK 0x2u             /* token bucket: keep the wide pass records even where
+                                             the packed 8-byte form applies (A/B checks) */
+#define TBE_FLAG_NO_HOT 0x4u              /* token bucket: no hot-key runs (A/B checks); keys
+                                             that take >= 2048 requests of a batch otherwise get
+                                             a run of their own in the next batch */
 
 typedef struct tbe_engine tbe_engine;
 
@@ -203,6 +208,13 @@ tbe_status tbe_approx_refresh(tbe_engine *engine, int64_t ts_us, uint64_t *n_gra
  * _instanceCountEstimate, AvailableTokens (GetAvailablePermits, A:81), queued requests. */
 tbe_status tbe_approx_query(tbe_engine *engine, uint64_t key, int32_t *local, int32_t *global_score,
                             double *est, int32_t *available, uint32_t *queued);
+
+/* How the engine lays a batch out (for reports and tests): *passes = 8-bit partition
+ * passes over the bucket id, *r_bits = log2 of the keys per bucket (one workgroup
+ * each), *packed: bit 0 set when the passes move packed 8-byte request records (token
+ * bucket kind) rather than the wide {key, permits, ts} records, bit 1 set
+ * when hot keys get runs of their own (TBE_FLAG_NO_HOT clears it). */
+tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* Per-stage device time (ms) accumulated since the last call, when
  * TBE_FLAG_STAGE_TIMING is set: out[0..n_out) = {hist, colscan, scatter, bounds,

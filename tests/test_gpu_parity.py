@@ -17,9 +17,9 @@ S_US = 1_760_572_800 * 1_000_000
 ABSENT = np.iinfo(np.int64).min
 
 
-def make_pair(n_keys, token_limit, tokens_per_period, period_ticks):
+def make_pair(n_keys, token_limit, tokens_per_period, period_ticks, pack=True):
     from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
-    eng = TokenBucketEngine(n_keys, token_limit, tokens_per_period, period_ticks, device=0)
+    eng = TokenBucketEngine(n_keys, token_limit, tokens_per_period, period_ticks, device=0, pack=pack)
     ref = cref.CTokenBucket(n_keys, token_limit, fill_rate(tokens_per_period, period_ticks))
     return eng, ref
 
@@ -67,17 +67,22 @@ def test_kat_sequence(engine_lib, gpu):
     (1 << 20, 300_000, 2, 10_000, 3),       # two LSD passes
     (3_000_017, 500_000, 1, 10_000, 2),     # odd table size, partial last bucket
 ])
-def test_random_traces(engine_lib, gpu, n_keys, n, p_hi, interval, batches):
-    eng, ref = make_pair(n_keys, 10, 3, 10_000_000)
+@pytest.mark.parametrize("pack", [True, False], ids=["packed", "wide"])
+def test_random_traces(engine_lib, gpu, n_keys, n, p_hi, interval, batches, pack):
+    eng, ref = make_pair(n_keys, 10, 3, 10_000_000, pack=pack)
+    assert eng.layout()["packed"] == pack
     for b in range(batches):
         k, p, t = trace.make_batch(0x5EED000B + n_keys, n_keys, b, n, interval, 0, p_hi)
         run_and_compare(eng, ref, k, p, t)
     assert_same_state(eng, ref)
 
 
-def test_config_b_shape_small(engine_lib, gpu):
+@pytest.mark.parametrize("pack", [True, False], ids=["packed", "wide"])
+def test_config_b_shape_small(engine_lib, gpu, pack):
     # Config B shape (100M keys, cap 10, 1 token/s, 10 ms batches), at 2^21 requests.
-    eng, ref = make_pair(100_000_000, 10, 1, 10_000_000)
+    eng, ref = make_pair(100_000_000, 10, 1, 10_000_000, pack=pack)
+    lay = eng.layout()
+    assert (lay["passes"], lay["r_bits"], lay["packed"], lay["hot"]) == (2, 11, pack, pack)
     for b in range(2):
         k, p, t = trace.make_batch(0x5EED000B, 100_000_000, b, 1 << 21, 10_000)
         g, _ = run_and_compare(eng, ref, k, p, t)
@@ -218,4 +223,103 @@ def test_expired_key_deleted_even_when_denied(engine_lib, gpu):
     g, r = run_and_compare(eng, ref, keys, np.array([10, 11, 3], np.int32),
                            np.array([S_US, S_US + year + 5_000, S_US + year - 5_000], np.int64))
     assert list(zip(g.tolist(), r.tolist())) == [(1, 0), (0, 10), (1, 7)]
+    assert_same_state(eng, ref)
+
+
+def test_packed_time_escape(engine_lib, gpu):
+    """Packed records carry ts - (ts[0] - 2^(wb-1)) in wb bits; requests outside that
+    window travel as escapes (their timestamp is re-read from the caller's array).
+    TokenLimit 2^20 on 1000 keys leaves wb = 32 (+-35.8 min): spread the batch over +-3 h,
+    with permits beyond TokenLimit (permit code clamped to TokenLimit + 1)."""
+    rng = np.random.default_rng(77)
+    cap = 1 << 20
+    eng, ref = make_pair(1000, cap, 1000, 10_000_000)
+    assert eng.layout()["packed"]
+    hour = 3_600_000_000
+    for b in range(3):
+        n = 60_000
+        k = rng.integers(0, 1000, n, dtype=np.uint64)
+        p = rng.choice(np.array([0, 1, 7, cap - 1, cap, cap + 1, 2**31 - 1], np.int32), n)
+        t = (S_US + b * hour + rng.integers(-3 * hour, 3 * hour, n)).astype(np.int64)
+        run_and_compare(eng, ref, k, p, t)
+    assert_same_state(eng, ref)
+    # a batch whose first timestamp is 0 (window starts below zero), the rest far later
+    t = np.full(5000, S_US + 10 * hour, np.int64)
+    t[0] = 0
+    run_and_compare(eng, ref, rng.integers(0, 1000, 5000, dtype=np.uint64),
+                    np.ones(5000, np.int32), t)
+    assert_same_state(eng, ref)
+
+
+@pytest.mark.parametrize("pack", [True, False], ids=["packed", "wide"])
+def test_hot_keys_speculative_rounds(engine_lib, gpu, pack):
+    """Skewed traffic: a handful of keys take most requests, so chunks hold long same-key
+    runs (mostly denies, settled by speculative rounds) mixed with rare grants and
+    expiry deletions (p > TokenLimit on a lapsed key)."""
+    rng = np.random.default_rng(11)
+    n_keys = 50_000
+    eng, ref = make_pair(n_keys, 5, 2, 10_000_000, pack=pack)
+    for b in range(3):
+        n = 200_000
+        hot = rng.integers(0, n_keys, 8, dtype=np.uint64)
+        k = np.where(rng.random(n) < 0.9, hot[rng.integers(0, 8, n)],
+                     rng.integers(0, n_keys, n, dtype=np.uint64)).astype(np.uint64)
+        p = rng.integers(0, 7, n).astype(np.int32)
+        t = (S_US + b * 4_000_000 + np.sort(rng.integers(0, 4_000_000, n))).astype(np.int64)
+        run_and_compare(eng, ref, k, p, t)
+    assert_same_state(eng, ref)
+
+
+@pytest.mark.parametrize("hot", [True, False], ids=["hot_runs", "no_hot"])
+@pytest.mark.parametrize("cap,tokens,period", [(10, 1, 10_000_000), (100, 5000, 10_000_000)],
+                         ids=["throttled", "fast_refill"])
+def test_zipf_hot_runs(engine_lib, gpu, hot, cap, tokens, period):
+    """Config C shape at test size: Zipf(1.1) keys, so the top keys take thousands of
+    requests per batch and (from the second batch on) get runs of their own.  Throttled:
+    hot runs are mostly denies (pass-through segments); fast refill: hot keys keep
+    granting (segments decided serially in the chain)."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate, workloads
+    n_keys, n = 1_000_000, 1 << 20
+    eng = TokenBucketEngine(n_keys, cap, tokens, period, device=0, hot=hot)
+    assert eng.layout()["hot"] == hot
+    ref = cref.CTokenBucket(n_keys, cap, fill_rate(tokens, period))
+    zs = workloads.ZipfSampler(n_keys, 1.1)
+    rng = np.random.default_rng(3)
+    for b in range(4):
+        k = workloads.zipf_keys(0x5EED000C, n_keys, b * n, n, sampler=zs)
+        p = np.where(rng.random(n) < 0.97, 1, rng.integers(0, cap + 3, n)).astype(np.int32)
+        t = workloads.batch_timestamps(b, n, 10_000, trace.T0_US)
+        run_and_compare(eng, ref, k, p, t)
+    assert_same_state(eng, ref)
+
+
+def test_hot_runs_unsorted_times_and_expiry(engine_lib, gpu):
+    """Hot keys with unsorted timestamps spread over several TTLs (cap 5 at 2 tokens/s:
+    TTL 3 s), permits 0..7 (p = 0 always modifies; p > 5 only ever deletes a lapsed
+    key), and a hot set that changes from batch to batch."""
+    rng = np.random.default_rng(21)
+    n_keys = 4096
+    eng, ref = make_pair(n_keys, 5, 2, 10_000_000)
+    assert eng.layout()["hot"]
+    for b in range(5):
+        n = 120_000
+        hot = rng.integers(0, n_keys, 6, dtype=np.uint64)
+        k = np.where(rng.random(n) < 0.8, hot[rng.integers(0, 6, n)],
+                     rng.integers(0, n_keys, n, dtype=np.uint64)).astype(np.uint64)
+        p = rng.integers(0, 8, n).astype(np.int32)
+        t = (S_US + b * 9_000_000 + rng.integers(0, 9_000_000, n)).astype(np.int64)
+        run_and_compare(eng, ref, k, p, t)
+        assert_same_state(eng, ref)
+
+
+def test_single_hot_key_many_segments(engine_lib, gpu):
+    """One key takes a whole 300k-request batch (37 run segments) twice in a row; the
+    refill lets it grant every ~1000 requests, so some segments pass through and others
+    are decided in the chain."""
+    eng, ref = make_pair(64, 3, 1, 10_000_000)
+    n = 300_000
+    for b in range(3):
+        k = np.full(n, 17, np.uint64)
+        t = (S_US + b * 300_000_000 + np.arange(n, dtype=np.int64) * 1000).astype(np.int64)
+        run_and_compare(eng, ref, k, np.ones(n, np.int32), t)
     assert_same_state(eng, ref)

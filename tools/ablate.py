@@ -15,10 +15,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
-    "base": [],
-    "skip_rounds": ["TBE_ABLATE_SKIP_ROUNDS"],
-    "skip_table": ["TBE_ABLATE_SKIP_TABLE"],
-    "skip_both": ["TBE_ABLATE_SKIP_ROUNDS", "TBE_ABLATE_SKIP_TABLE"],
+    # name: (build defines, extra bench args)
+    "base": ([], []),
+    "wide": ([], ["--no-pack"]),
+    "nohot": ([], ["--no-hot"]),
+    "part1024x8": (["TBE_PART_BLOCK=1024", "TBE_PART_ITEMS=8"], []),
 }
 
 
@@ -29,7 +30,7 @@ def build():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     os.makedirs(OUTDIR, exist_ok=True)
-    for name, defs in VARIANTS.items():
+    for name, (defs, _) in VARIANTS.items():
         m.build_engine(force=True, defines=defs, out=os.path.join(OUTDIR, f"libtbe_{name}.so"))
         print("built", name)
 
@@ -37,10 +38,10 @@ def build():
 def run(rounds: int, steps: int):
     results = {}
     for r in range(rounds):
-        for name in VARIANTS:
+        for name, (_, extra) in VARIANTS.items():
             env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{name}.so"))
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps),
-                                  "--warmup", "2", "--cpu-seconds", "0"], env=env, capture_output=True,
+                                  "--warmup", "2", "--cpu-seconds", "0"] + extra, env=env, capture_output=True,
                                  text=True, timeout=300)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")]
             if not line:
