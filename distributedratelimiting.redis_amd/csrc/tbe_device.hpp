@@ -77,13 +77,17 @@ struct TbParams {
 // parallel before the per-key serial order is resolved.
 struct ReqTime {
     double new_t;    // TB:203
-    int64_t ms;      // command-time snapshot for passive expiry
+    int64_t exp_lt;  // passive expiry: a stored grant time t_us < exp_lt has lapsed
     int64_t ts;      // the injected TIME itself: what a grant stores
 };
-__device__ __forceinline__ ReqTime req_time(int64_t ts_us) {
+// Redis lapses a key when the command's millisecond snapshot ms = ts / 1000 exceeds
+// grant_ms + ttl_ms (EXPIRE at TB:235), grant_ms = t_us / 1000.  For t_us >= 0 and
+// integer X, floor(t_us / 1000) < X iff t_us < 1000 X, so the test is one compare:
+// t_us < 1000 * (ms - ttl_ms).
+__device__ __forceinline__ ReqTime req_time(int64_t ts_us, int64_t ttl_ms) {
     ReqTime r;
     r.new_t = new_t_of(ts_us);
-    r.ms = ts_us / 1000;
+    r.exp_lt = (ts_us / 1000 - ttl_ms) * 1000;
     r.ts = ts_us;
     return r;
 }
@@ -100,7 +104,7 @@ __device__ __forceinline__ uint32_t tb_step_ft(Slot &row, double ft, int32_t per
                                                const ReqTime &rq, const TbParams &P, bool &modified) {
     const bool had = row.t_us != kAbsent;
     // EXPIRE at TB:235 lapses when the command-time snapshot (ms) exceeds grant_ms + ttl.
-    const bool expired = had && (rq.ms > row.t_us / 1000 + P.ttl_ms);
+    const bool expired = had && row.t_us < rq.exp_lt;
     const bool present = had && !expired;
     const double pv = present ? row.v : P.cap;                          // TB:211-215
     const double pt = present ? ft : rq.new_t;
@@ -130,7 +134,7 @@ __device__ __forceinline__ uint32_t tb_step(Slot &row, int32_t permits, const Re
 
 __device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t ts_us,
                                                const TbParams &P, bool &modified) {
-    return tb_step(s, permits, req_time(ts_us), P, modified);
+    return tb_step(s, permits, req_time(ts_us, P.ttl_ms), P, modified);
 }
 
 // ----------------------------------------------------------------- wave / block helpers

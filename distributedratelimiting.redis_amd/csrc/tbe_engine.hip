@@ -501,6 +501,7 @@ constexpr int kFoldBlock = 512;
 constexpr int kFoldPer = 4;                                 // requests per thread per chunk
 constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
 constexpr int kMaxRows = 1 << kMaxRBits;
+constexpr int kFoldTail = kFoldBlock;                       // compact pending list after round 1
 
 template <bool PACKED>
 __global__ __launch_bounds__(kFoldBlock) void k_fold(
@@ -510,7 +511,17 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next) {
     __shared__ Slot row[kMaxRows];
-    __shared__ uint32_t hcnt[kMaxRows];   // requests per row, in buckets that may hold a hot key
+    // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
+    // compact list of requests still pending after round 1 (t_*)
+    __shared__ uint64_t aux[kFoldTail * 4];
+    __shared__ uint32_t wsum[kFoldBlock / 64];
+    uint32_t *hcnt = reinterpret_cast<uint32_t *>(aux);
+    uint32_t *t_kl_lid = reinterpret_cast<uint32_t *>(aux);
+    int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kFoldTail;
+    double *t_newt = reinterpret_cast<double *>(aux) + kFoldTail;
+    int64_t *t_exp = reinterpret_cast<int64_t *>(aux) + 2 * kFoldTail;
+    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + 3 * kFoldTail;
+    static_assert(kFoldTail * 4 * 8 >= kMaxRows * 4, "hcnt fits in aux");
     __shared__ double ft[kMaxRows];
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t loaded[kMaxRows / 32];
@@ -614,7 +625,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         }
         ReqTime rq[kFoldPer];
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) rq[r] = req_time(tsv[r]);
+        for (int r = 0; r < kFoldPer; ++r) rq[r] = req_time(tsv[r], P.ttl_ms);
         __syncthreads();   // claimed rows and their field t visible
         uint32_t rep[kFoldPer];
 #pragma unroll
@@ -627,9 +638,8 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         // round.  A key whose requests in the chunk all deny settles in one round.
         // Election slot: (round << 12) | (4095 - local id); the max is the key's earliest
         // modifier of the newest round, so no reset between rounds.  Workgroup-uniform
-        // loop: every thread runs every round and the only exit is the __syncthreads_or.
-        for (uint32_t round = 1;; ++round) {
-            Slot nrow[kFoldPer];
+        // loops: every thread runs every round and the only exits are __syncthreads_or.
+        auto eval_slots = [&](uint32_t round, Slot (&nrow)[kFoldPer]) {
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
                 nrow[r] = Slot{0.0, 0};
@@ -640,7 +650,8 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
                     if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
                 }
             }
-            __syncthreads();
+        };
+        auto resolve_slots = [&](uint32_t round, const Slot (&nrow)[kFoldPer]) {
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
                 if (!(pend & (1u << r))) continue;
@@ -655,12 +666,82 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
                     pend &= ~(1u << r);
                 }
             }
-            if (!__syncthreads_or(pend != 0)) break;
+        };
+        {
+            Slot nrow[kFoldPer];
+            eval_slots(1u, nrow);
+            __syncthreads();
+            resolve_slots(1u, nrow);
+        }
+        // Round 1 settles every key's first request.  The few left pending move to a
+        // compact list (one per thread) so later rounds evaluate one request per thread
+        // instead of every slot of every lane.
+        uint32_t n_tail;
+        const uint32_t tail_at = block_excl_scan<kFoldBlock>(__popc(pend), wsum, &n_tail);
+        uint32_t keep = ~0u;                     // slots whose reply this thread stores
+        if (n_tail != 0 && n_tail <= kFoldTail && !count_hot) {
+            uint32_t at = tail_at;
+#pragma unroll
+            for (int r = 0; r < kFoldPer; ++r) {
+                if (pend & (1u << r)) {
+                    t_kl_lid[at] = kl[r] | ((uint32_t)(r * kFoldBlock + tid) << 16);
+                    t_pm[at] = pm[r];
+                    t_newt[at] = rq[r].new_t;
+                    t_exp[at] = rq[r].exp_lt;
+                    t_ts[at] = rq[r].ts;
+                    ++at;
+                }
+            }
+            keep = ~pend;
+            pend = 0;
+            __syncthreads();
+            bool tp = (uint32_t)tid < n_tail;
+            uint32_t tkl = 0, tlid = 0, trep = 0;
+            int32_t tpm = 0;
+            ReqTime trq{0.0, 0, 0};
+            if (tp) {
+                tkl = t_kl_lid[tid] & 0xFFFFu;
+                tlid = t_kl_lid[tid] >> 16;
+                tpm = t_pm[tid];
+                trq = ReqTime{t_newt[tid], t_exp[tid], t_ts[tid]};
+            }
+            for (uint32_t round = 2;; ++round) {
+                const uint32_t tag = (round << 12) | (4095u - tlid);
+                Slot nr = Slot{0.0, 0};
+                if (tp) {
+                    nr = row[tkl];
+                    bool m;
+                    trep = tb_step_ft(nr, ft[tkl], tpm, trq, P, m);
+                    if (m) atomicMax(&own[tkl], tag);
+                }
+                __syncthreads();
+                if (tp) {
+                    const uint32_t o = own[tkl];
+                    if ((o >> 12) != round || o < tag) {
+                        tp = false;
+                    } else if (o == tag) {
+                        row[tkl] = nr;
+                        ft[tkl] = trq.new_t;
+                        if (!dense) atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
+                        tp = false;
+                    }
+                    if (!tp) res[c + tlid] = trep;
+                }
+                if (!__syncthreads_or(tp)) break;
+            }
+        } else if (n_tail != 0) {
+            for (uint32_t round = 2;; ++round) {
+                Slot nrow[kFoldPer];
+                eval_slots(round, nrow);
+                __syncthreads();
+                resolve_slots(round, nrow);
+                if (!__syncthreads_or(pend != 0)) break;
+            }
         }
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            if (q < e) res[q] = rep[r];
+            if (q < e && (keep & (1u << r))) res[q] = rep[r];
         }
     }
     __syncthreads();
@@ -873,7 +954,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
             const SegSummary sm = summ[j0 + u];
             Slot c = s;
             bool m;
-            (void)tb_step_ft(c, ft, sm.min_p, req_time(sm.max_ts), P, m);
+            (void)tb_step_ft(c, ft, sm.min_p, req_time(sm.max_ts, P.ttl_ms), P, m);
             if (m) {
                 f = u;
                 break;
@@ -905,7 +986,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
                     unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts);
                     pend |= 1u << r;
                 }
-                rq[r] = req_time(ts);
+                rq[r] = req_time(ts, P.ttl_ms);
             }
             if (tid == 0) own = 0;
             __syncthreads();
@@ -979,7 +1060,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
             unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
             Slot c = st.s;
             bool m;
-            res[q] = tb_step_ft(c, st.ft, p, req_time(ts), P, m);
+            res[q] = tb_step_ft(c, st.ft, p, req_time(ts, P.ttl_ms), P, m);
         }
     }
 }
@@ -1454,8 +1535,8 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
         double my_period = 0.0;
         for (uint32_t r = 0; r < n_clients; ++r) {
             const int64_t ts = ts_us + (int64_t)r * stagger_us;
-            const ReqTime rq = req_time(ts);                                  // A:241-242
-            const bool present = (t != kAbsent) && !(rq.ms > t / 1000 + kApproxTtlMs);
+            const ReqTime rq = req_time(ts, kApproxTtlMs);                    // A:241-242
+            const bool present = (t != kAbsent) && !(t < rq.exp_lt);          // EXPIRE 86400 (A:268)
             const double pv = present ? v : 0.0;                              // A:247-252
             const double pp = present ? p : 0.0;
             const double pt = present ? new_t_of(t) : rq.new_t;

@@ -298,7 +298,7 @@ def test_hot_runs_unsorted_times_and_expiry(engine_lib, gpu):
     TTL 3 s), permits 0..7 (p = 0 always modifies; p > 5 only ever deletes a lapsed
     key), and a hot set that changes from batch to batch."""
     rng = np.random.default_rng(21)
-    n_keys = 4096
+    n_keys = 3000                     # 188 ordinary buckets of 16 keys: room for 68 hot runs
     eng, ref = make_pair(n_keys, 5, 2, 10_000_000)
     assert eng.layout()["hot"]
     for b in range(5):
