@@ -124,19 +124,24 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
                                                  uint32_t *__restrict__ blocksum, uint64_t n_keys,
                                                  uint32_t *__restrict__ err, int validate,
                                                  uint64_t kmask, const HotSet *__restrict__ hot = nullptr,
-                                                 uint32_t nb = 0, int r_bits = 0) {
+                                                 uint32_t nb = 0, int r_bits = 0,
+                                                 uint32_t *__restrict__ bcount = nullptr,
+                                                 int lowbits = 0, uint32_t nbt = 0) {
     __shared__ uint32_t h[kDigits];
+    __shared__ uint32_t tile_lo[2];
     __shared__ uint32_t hk[HOT ? kHotSlots : 1], hi[HOT ? kHotSlots : 1];
     const int tid = threadIdx.x;
     const bool any_hot = HOT && hot_load<kBlock>(hot, hk, hi);
     const uint32_t t0 = blockIdx.x * tiles_per_blk;
     const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
     uint32_t run = 0;
+    uint32_t acc = 0, acc_lo = 0;   // bucket counting (last pass): this thread's digit
     bool bad = false;
     for (uint32_t t = t0; t < t1; ++t) {
         h[tid] = 0;
         __syncthreads();
         const uint64_t base = (uint64_t)t * kTile;
+        const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
         KeyT kv[kHistItems];
 #pragma unroll
         for (int it = 0; it < kHistItems; ++it) {
@@ -151,13 +156,45 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
                 uint32_t sk = (uint32_t)((uint64_t)kv[it] & kmask);
                 if (HOT && any_hot) sk = hot_sortkey((uint32_t)kv[it], hk, hi, nb, r_bits);
                 atomicAdd(&h[(sk >> shift) & (kDigits - 1)], 1u);
+                if (bcount && (i == base || i == last)) {
+                    // the tile's first and last bucket low bits (sorted by earlier passes)
+                    tile_lo[i == last] = lowbits ? (sk >> r_bits) & ((1u << lowbits) - 1u) : 0u;
+                    if (i == base && i == last) tile_lo[0] = tile_lo[1];
+                }
             }
         }
         __syncthreads();
         const uint32_t c = h[tid];
         tileprefix[(uint64_t)t * kDigits + tid] = run;
         run += c;
+        if (bcount) {
+            // Last pass: count requests per bucket for the fold's bucket starts.  The
+            // previous passes left the requests sorted by the bucket's lower bits, so a
+            // tile usually shares them: then its digit histogram is the bucket count,
+            // summed here over the block's consecutive tiles and added once per change.
+            const uint32_t lo0 = tile_lo[0], lo1 = tile_lo[1];
+            if (lo0 == lo1) {
+                if (lo0 != acc_lo) {
+                    const uint32_t bk = ((uint32_t)tid << lowbits) | acc_lo;
+                    if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+                    acc = 0;
+                    acc_lo = lo0;
+                }
+                acc += c;
+            } else {
+#pragma unroll
+                for (int it = 0; it < kHistItems; ++it) {
+                    const uint64_t i = base + it * kBlock + tid;
+                    const uint32_t bk = (uint32_t)((uint64_t)kv[it] & kmask) >> r_bits;
+                    if (i < n && bk < nbt) atomicAdd(&bcount[bk], 1u);
+                }
+            }
+        }
         __syncthreads();
+    }
+    if (bcount) {
+        const uint32_t bk = ((uint32_t)tid << lowbits) | acc_lo;
+        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
     }
     blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
     if (__any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
@@ -312,51 +349,47 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
     if (validate && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
-// bstart[b] = first sorted position with bucket >= b, for b in [0, nb]; bstart[nb] = n.
-// Four sorted keys per thread.
-// KeyT: u32 sorted keys, or u64 packed records (key under kmask).
-template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k_bounds(const KeyT *__restrict__ skeys, uint64_t n,
-                                                   int r_bits, uint32_t nb, uint64_t kmask,
-                                                   uint32_t *__restrict__ bstart,
-                                                   const uint32_t *__restrict__ err) {
-    if (*err) return;
-    const uint64_t i0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
-    if (i0 >= n) return;
-    auto kof = [&](KeyT x) { return (uint32_t)((uint64_t)x & kmask); };
-    int64_t prev = (i0 == 0) ? -1 : (int64_t)(kof(skeys[i0 - 1]) >> r_bits);
-    uint32_t k4[4];
-    if (i0 + 4 <= n) {
-        // 16-byte vector loads: one for four u32 keys, two for four packed records
-        constexpr int V = sizeof(KeyT) * 4 / 16;
-        uint4 v[V];
+// bstart = exclusive scan of the per-bucket counts k_hist's last pass gathered;
+// bstart[nbt] = the batch size.  One 1024-thread workgroup over rows of 16384 buckets:
+// a coalesced load into LDS, each thread scans its 16 consecutive counts, one block
+// scan of the thread sums, and a coalesced store back through LDS.
+constexpr int kScanPer = 16;
+__global__ __launch_bounds__(1024) void k_bscan(const uint32_t *__restrict__ bcount, uint32_t nbt,
+                                                uint32_t *__restrict__ bstart) {
+    __shared__ uint32_t tile[1024 * kScanPer];
+    __shared__ uint32_t wsum[16];
+    const uint32_t t = threadIdx.x;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < nbt; r0 += 1024 * kScanPer) {
 #pragma unroll
-        for (int w = 0; w < V; ++w) v[w] = reinterpret_cast<const uint4 *>(skeys + i0)[w];
-        if (sizeof(KeyT) == 4) {
-            k4[0] = v[0].x; k4[1] = v[0].y; k4[2] = v[0].z; k4[3] = v[0].w;
-        } else {
-            k4[0] = kof((KeyT)(((uint64_t)v[0].y << 32) | v[0].x));
-            k4[1] = kof((KeyT)(((uint64_t)v[0].w << 32) | v[0].z));
-            k4[2] = kof((KeyT)(((uint64_t)v[V - 1].y << 32) | v[V - 1].x));
-            k4[3] = kof((KeyT)(((uint64_t)v[V - 1].w << 32) | v[V - 1].z));
+        for (int k = 0; k < kScanPer; ++k) {
+            const uint32_t j = r0 + k * 1024 + t;
+            tile[k * 1024 + t] = j < nbt ? bcount[j] : 0u;
         }
-        if (sizeof(KeyT) == 4)
+        __syncthreads();
+        uint32_t v[kScanPer], sum = 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) k4[u] = kof((KeyT)k4[u]);
-    } else {
+        for (int k = 0; k < kScanPer; ++k) {
+            v[k] = tile[t * kScanPer + k];
+            sum += v[k];
+        }
+        uint32_t total;
+        uint32_t pre = carry + block_excl_scan<1024>(sum, wsum, &total);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) k4[u] = (i0 + u < n) ? kof(skeys[i0 + u]) : 0u;
+        for (int k = 0; k < kScanPer; ++k) {
+            tile[t * kScanPer + k] = pre;
+            pre += v[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const uint32_t j = r0 + k * 1024 + t;
+            if (j < nbt) bstart[j] = tile[k * 1024 + t];
+        }
+        carry += total;
+        __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const uint64_t i = i0 + u;
-        if (i >= n) break;
-        const int64_t b = (int64_t)(k4[u] >> r_bits);
-        for (int64_t q = prev + 1; q <= b; ++q) bstart[q] = (uint32_t)i;
-        prev = b;
-        if (i == n - 1)
-            for (int64_t q = b + 1; q <= (int64_t)nb; ++q) bstart[q] = (uint32_t)n;
-    }
+    if (t == 0) bstart[nbt] = carry;
 }
 
 // Packed request records (token-bucket kind).  When the key, a permit code and a
@@ -1694,6 +1727,7 @@ struct tbe_engine {
     uint32_t *blocksum = nullptr;
     uint32_t *res[2] = {nullptr, nullptr};
     uint32_t *bstart = nullptr;
+    uint32_t *bcount = nullptr;  // requests per bucket of the current batch
     uint32_t *err = nullptr;     // [0] per-batch flag, [1] sticky flag
     // host-buffer path staging
     uint64_t *d_keys = nullptr;
@@ -1857,6 +1891,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(uint32_t), st));
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
+    HIP_TRY(e, hipMemsetAsync(e->bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), st));
     // hot runs: this batch partitions by hot[cur] and nominates into hot[cur ^ 1]
     HotSet *hot = e->hot_cap ? e->hot[e->hot_cur] : nullptr;
     HotSet *hot_next = e->hot_cap ? e->hot[e->hot_cur ^ 1] : nullptr;
@@ -1865,21 +1900,29 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         const int shift = e->r_bits + kDigitBits * p;
         PassBufs &out = e->pass[p];
         stage_begin(e, ST_HIST, st);
+        // the last pass also counts requests per bucket (k_bscan turns them into bstart)
+        uint32_t *bc = (p == e->passes - 1) ? e->bcount : nullptr;
+        const int lowbits = kDigitBits * p;
         if (p == 0 && hot)
             k_hist<uint64_t, true><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                              e->blocksum, e->cfg.n_keys, e->err, 1, kmask,
-                                                             hot, e->nbuckets, e->r_bits);
+                                                             hot, e->nbuckets, e->r_bits, bc, lowbits,
+                                                             e->nb_total);
         else if (p == 0)
             k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
-                                                       e->blocksum, e->cfg.n_keys, e->err, 1, kmask);
+                                                       e->blocksum, e->cfg.n_keys, e->err, 1, kmask,
+                                                       nullptr, e->nbuckets, e->r_bits, bc, lowbits,
+                                                       e->nb_total);
         else if (e->packed)
             k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].rec, n, shift, tpb, ntiles,
                                                        out.tileprefix, e->blocksum, e->cfg.n_keys,
-                                                       e->err, 0, kmask);
+                                                       e->err, 0, kmask, nullptr, e->nbuckets,
+                                                       e->r_bits, bc, lowbits, e->nb_total);
         else
             k_hist<uint32_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].keys, n, shift, tpb, ntiles,
                                                        out.tileprefix, e->blocksum, e->cfg.n_keys,
-                                                       e->err, 0, kmask);
+                                                       e->err, 0, kmask, nullptr, e->nbuckets,
+                                                       e->r_bits, bc, lowbits, e->nb_total);
         stage_end(e, ST_HIST, st);
         stage_begin(e, ST_COLSCAN, st);
         k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
@@ -1928,14 +1971,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     }
     const PassBufs &sorted = e->pass[e->passes - 1];
     stage_begin(e, ST_BOUNDS, st);
-    const unsigned bgrid = (unsigned)((n + 4 * kBlock - 1) / (4 * kBlock));
-    const uint32_t nb_total = e->packed ? e->nb_total : e->nbuckets;
-    if (e->packed)
-        k_bounds<uint64_t><<<bgrid, kBlock, 0, st>>>(sorted.rec, n, e->r_bits, nb_total, kmask,
-                                                     e->bstart, e->err);
-    else
-        k_bounds<uint32_t><<<bgrid, kBlock, 0, st>>>(sorted.keys, n, e->r_bits, nb_total, kmask,
-                                                     e->bstart, e->err);
+    k_bscan<<<1, 1024, 0, st>>>(e->bcount, e->nb_total, e->bstart);
     stage_end(e, ST_BOUNDS, st);
     stage_begin(e, ST_FOLD, st);
     if (approx) {
@@ -2110,6 +2146,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
     if (hipMalloc(&e->bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)) != hipSuccess)
         return bail(TBE_ENOMEM);
+    if (hipMalloc(&e->bcount, (uint64_t)e->nb_total * sizeof(uint32_t)) != hipSuccess)
+        return bail(TBE_ENOMEM);
     if (e->hot_cap) {
         for (auto &hs : e->hot) {
             if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
@@ -2176,6 +2214,7 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->log_id);
     dfree(e->log_rem);
     dfree(e->bstart);
+    dfree(e->bcount);
     dfree(e->err);
     dfree(e->hot[0]);
     dfree(e->hot[1]);
