@@ -31,6 +31,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED_B = 0x5EED000B
+SEED_C = 0x5EED000C
 T0_US = 1_760_000_000_000_000
 
 
@@ -39,7 +40,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--keys", type=int, default=100_000_000)
+    ap.add_argument("--workload", choices=("uniform", "zipf"), default="uniform",
+                    help="uniform: config B (the headline); zipf: config C's per-GPU slice")
+    ap.add_argument("--keys", type=int, default=None,
+                    help="total keys (uniform, default 1e8) / keys per GPU (zipf, default 1.25e8)")
+    ap.add_argument("--zipf-s", type=float, default=1.1)
+    ap.add_argument("--zipf-batches", type=int, default=2,
+                    help="distinct Zipf key batches drawn on the host, reused in turn")
     ap.add_argument("--batch", type=int, default=1 << 26)
     ap.add_argument("--interval-us", type=int, default=10_000)
     ap.add_argument("--token-limit", type=int, default=10)
@@ -77,8 +84,14 @@ def main():
 
     # Hash partition: this rank owns keys_local = ceil(K / world) dense local ids.  The
     # synthetic stream is generated directly in the rank's local id space (uniform keys
-    # stay uniform under a hash partition); seeds differ per rank.
-    keys_local = (args.keys + world - 1) // world
+    # stay uniform under a hash partition); seeds differ per rank.  Zipf (config C): each
+    # rank owns 1.25e8 keys (1e9 over 8 GPUs) and draws its own Zipf(1.1) stream over them.
+    if args.workload == "zipf":
+        keys_local = args.keys or 125_000_000
+        keys_total = keys_local * world
+    else:
+        keys_total = args.keys or 100_000_000
+        keys_local = (keys_total + world - 1) // world
     n = args.batch
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                             args.period_ticks, device=dev.index,
@@ -86,7 +99,14 @@ def main():
                             pack=not args.no_pack, hot=not args.no_hot)
     layout = eng.layout()
     total_steps = args.warmup + args.steps
-    seed = SEED_B + 7919 * rank
+    seed = (SEED_C if args.workload == "zipf" else SEED_B) + 7919 * rank
+    zkeys = []
+    if args.workload == "zipf":
+        from distributedratelimiting.redis_amd import workloads
+        zs = workloads.ZipfSampler(keys_local, args.zipf_s)
+        for d in range(args.zipf_batches):
+            zk = workloads.zipf_keys(seed, keys_local, d * n, n, sampler=zs)
+            zkeys.append((zk, torch.from_numpy(zk.view(np.int64)).to(dev)))
     bufs = []
     for s in range(total_steps):
         k = torch.empty(n, dtype=torch.int64, device=dev)
@@ -95,6 +115,8 @@ def main():
         rc = lib.tbe_gen_batch_device(seed, keys_local, s * n, n, 1, 1, T0_US + s * args.interval_us,
                                       args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), None)
         assert rc == 0
+        if zkeys:
+            k.copy_(zkeys[s % len(zkeys)][1])
         bufs.append((k, p, t))
     granted = torch.empty(n, dtype=torch.uint8, device=dev)
     remaining = torch.empty(n, dtype=torch.int32, device=dev)
@@ -135,7 +157,10 @@ def main():
                     "unscatter": passes, "hot": 5}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
-        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"])
+        distinct = None
+        if zkeys:   # distinct keys per batch, measured (the uniform estimate does not apply)
+            distinct = float(np.mean([np.unique(zk).size for zk, _ in zkeys]))
+        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct)
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -144,7 +169,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, keys_local)
+        cpu = cpu_baseline(args, keys_local, [zk for zk, _ in zkeys])
 
     if rank == 0:
         line = {
@@ -159,9 +184,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (splitmix64 seeded trace generated in HBM)",
-            "config": {"workload": "TokenBucket 100M keys uniform, 2^26-request batches (config B)",
-                       "keys_total": args.keys, "keys_per_gpu": keys_local, "batch_per_gpu": n,
+            "data": ("synthetic (Zipf keys drawn on the host, copied to HBM before timing; "
+                     "timestamps generated in HBM)" if zkeys else
+                     "synthetic (splitmix64 seeded trace generated in HBM)"),
+            "config": {"workload": workload_name(args, n),
+                       "keys_total": keys_total, "keys_per_gpu": keys_local, "batch_per_gpu": n,
                        "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
                        "period_ticks": args.period_ticks, "interval_us": args.interval_us,
                        "partitioning": f"key-hash x{world}, no data-path collective",
@@ -177,7 +204,8 @@ def main():
         td.destroy_process_group()
 
 
-def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool) -> int:
+def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool,
+                      distinct: float = None) -> int:
     """Bytes one launch of `stage` must move at minimum for its function,
     averaged over the passes where a stage runs once per pass.  Packed: the passes and
     the fold move one 8-byte record per request; wide: {key u32, permits i32, ts i64}."""
@@ -185,7 +213,7 @@ def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool
     if stage == "fold":
         # sorted records + packed reply 4 per request, plus the table rows of the distinct
         # keys in the batch (16 B read + 16 B written each)
-        u = n_keys * (1.0 - np.exp(-n / n_keys))
+        u = distinct if distinct is not None else n_keys * (1.0 - np.exp(-n / n_keys))
         return int(n * (rec + 4) + u * 32)
     if stage == "scatter":
         # pass 0 reads the caller's key 8 + permits 4 + ts 8, later passes one record;
@@ -212,7 +240,14 @@ def pmc_traffic(stage: str):
         return None
 
 
-def cpu_baseline(args, n_keys: int):
+def workload_name(args, n: int) -> str:
+    if args.workload == "zipf":
+        return (f"TokenBucket Zipf({args.zipf_s}) over each GPU's keys, 2^{n.bit_length() - 1}-request "
+                "batches (config C per-GPU slice)")
+    return f"TokenBucket uniform keys, 2^{n.bit_length() - 1}-request batches (config B)"
+
+
+def cpu_baseline(args, n_keys: int, zkeys=()):
     """The C restatement of the reference script (oracle/tb_ref.c, serial like Redis'
     single script thread) timed on the same trace: the first `sample` requests of each
     batch, batches in order, until ~args.cpu_seconds of CPU work."""
@@ -221,9 +256,12 @@ def cpu_baseline(args, n_keys: int):
 
     ref = cref.CTokenBucket(n_keys, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks))
     sample = min(args.batch, 1 << 22)
+    seed = SEED_C if zkeys else SEED_B
     done, spent, b = 0, 0.0, 0
     while spent < args.cpu_seconds and b < 64:
-        k, p, t = cref.gen_batch(SEED_B, n_keys, b, args.batch, args.interval_us)
+        k, p, t = cref.gen_batch(seed, n_keys, b, args.batch, args.interval_us)
+        if zkeys:
+            k = zkeys[b % len(zkeys)]
         k, p, t = k[:sample], p[:sample], t[:sample]
         t0 = time.perf_counter()
         ref.acquire_batch(k, p, t, threads=1)
@@ -231,8 +269,9 @@ def cpu_baseline(args, n_keys: int):
         done += sample
         b += 1
     ref.close()
+    what = "config-C (Zipf)" if zkeys else "config-B"
     return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} requests of each of {b} config-B batches "
+            "sample": f"first {sample} requests of each of {b} {what} batches "
                       f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
             "host_cpus": os.cpu_count()}
 

@@ -67,44 +67,61 @@ constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
 // Hot keys (see the "hot keys" section below for how their runs are decided).
 constexpr uint32_t kHotKeysMax = 1024;
-constexpr uint32_t kHotSlots = 2048;             // hash slots: power of two >= 2 * kHotKeysMax
+constexpr uint32_t kHotSlots = 4096;             // hash slots: power of two, load <= 1/4
 constexpr uint32_t kHotEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kHotMin = 2048;               // requests in one batch that make a key hot
+constexpr uint32_t kHotCandMax = 4096;           // nominations kept per batch (the busiest win)
 
 struct HotSet {
     uint32_t count;                  // hot keys in use this batch (index h -> bucket nb + h)
     uint32_t n_cand;                 // nominations for the following batch
     uint32_t key[kHotKeysMax];
-    uint32_t cand[kHotKeysMax];
-    uint32_t slot_key[kHotSlots];    // open-addressing hash table: key -> index
-    uint32_t slot_idx[kHotSlots];
+    uint64_t cand[kHotCandMax];      // (requests << 32) | key
+    uint64_t slot[kHotSlots];        // open-addressing hash table: (index << 32) | key
 };
 
-__device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 21; }
+__device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 20; }
+constexpr uint64_t kHotSlotEmpty = 0xFFFFFFFFFFFFFFFFull;
 
 // Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns
 // whether any key is hot.
 template <int BLOCK>
-__device__ __forceinline__ bool hot_load(const HotSet *__restrict__ hot, uint32_t *sk, uint32_t *si) {
+__device__ __forceinline__ bool hot_load(const HotSet *__restrict__ hot, uint64_t *slots) {
     const bool any = hot != nullptr && hot->count != 0;
     if (any)
-        for (int j = threadIdx.x; j < (int)kHotSlots; j += BLOCK) {
-            sk[j] = hot->slot_key[j];
-            si[j] = hot->slot_idx[j];
-        }
+        for (int j = threadIdx.x; j < (int)kHotSlots; j += BLOCK) slots[j] = hot->slot[j];
     __syncthreads();
     return any;
 }
 
 // Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
-__device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint32_t *sk, const uint32_t *si,
-                                                uint32_t nb, int r_bits) {
+__device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *slots, uint32_t nb,
+                                                int r_bits) {
     uint32_t h = hot_hash(key);
     for (;;) {
-        const uint32_t k = sk[h];
-        if (k == key) return (nb + si[h]) << r_bits;
+        const uint64_t v = slots[h];
+        const uint32_t k = (uint32_t)v;
+        if (k == key) return (nb + (uint32_t)(v >> 32)) << r_bits;
         if (k == kHotEmpty) return key;
         h = (h + 1) & (kHotSlots - 1);
+    }
+}
+
+// hot_sortkey for N requests at once: the first probes of all N issue together (LDS
+// latency overlaps); the rare collision chains finish one by one.
+template <int N, typename KeyT>
+__device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t *slots, uint32_t nb,
+                                             int r_bits, uint32_t (&sk)[N]) {
+    uint64_t v[N];
+#pragma unroll
+    for (int it = 0; it < N; ++it) v[it] = slots[hot_hash((uint32_t)kv[it])];
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+        const uint32_t key = (uint32_t)kv[it];
+        const uint32_t k = (uint32_t)v[it];
+        if (k == key) sk[it] = (nb + (uint32_t)(v[it] >> 32)) << r_bits;
+        else if (k == kHotEmpty) sk[it] = key;
+        else sk[it] = hot_sortkey(key, slots, nb, r_bits);
     }
 }
 
@@ -127,18 +144,20 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
                                                  uint32_t nb = 0, int r_bits = 0,
                                                  uint32_t *__restrict__ bcount = nullptr,
                                                  int lowbits = 0, uint32_t nbt = 0) {
-    __shared__ uint32_t h[kDigits];
+    __shared__ uint32_t h8[kDigits * 8];
     __shared__ uint32_t tile_lo[2];
-    __shared__ uint32_t hk[HOT ? kHotSlots : 1], hi[HOT ? kHotSlots : 1];
+    static_assert(kBlock == kDigits, "one digit per thread");
+    __shared__ uint64_t hs[HOT ? kHotSlots : 1];
     const int tid = threadIdx.x;
-    const bool any_hot = HOT && hot_load<kBlock>(hot, hk, hi);
+    const bool any_hot = HOT && hot_load<kBlock>(hot, hs);
     const uint32_t t0 = blockIdx.x * tiles_per_blk;
     const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
     uint32_t run = 0;
     uint32_t acc = 0, acc_lo = 0;   // bucket counting (last pass): this thread's digit
     bool bad = false;
     for (uint32_t t = t0; t < t1; ++t) {
-        h[tid] = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) h8[u * kBlock + tid] = 0;
         __syncthreads();
         const uint64_t base = (uint64_t)t * kTile;
         const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
@@ -148,14 +167,42 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
             const uint64_t i = base + it * kBlock + tid;
             kv[it] = (i < n) ? keys[i] : (KeyT)0;
         }
+        uint32_t skv[kHistItems];
+        if (HOT && any_hot) {
+            hot_sortkeys<kHistItems>(kv, hs, nb, r_bits, skv);
+        } else {
+#pragma unroll
+            for (int it = 0; it < kHistItems; ++it) skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
+        }
 #pragma unroll
         for (int it = 0; it < kHistItems; ++it) {
             const uint64_t i = base + it * kBlock + tid;
-            if (i < n) {
+            const bool valid = i < n;
+            const uint32_t sk = skv[it];
+            const uint32_t d = (sk >> shift) & (kDigits - 1);
+            const uint64_t vmask = __ballot(valid);
+            const uint32_t d0 = __shfl(d, vmask ? __ffsll((long long)vmask) - 1 : 0, 64);
+            if (__all(!valid || d == d0)) {
+                // the whole wave on one digit (a hot run's tile): one add
+                if (vmask && (vmask & lanemask_lt()) == 0 && valid) atomicAdd(&h8[d0 * 8], (uint32_t)__popcll(vmask));
+            } else {
+#ifdef TBE_HIST_MATCH
+                uint64_t peers = vmask;
+#pragma unroll
+                for (int b = 0; b < kDigitBits; ++b) {
+                    const bool bit = (d >> b) & 1u;
+                    const uint64_t m = __ballot(bit);
+                    peers &= bit ? m : ~m;
+                }
+                if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h8[d * 8 + (tid & 7)], (uint32_t)__popcll(peers));
+#else
+                // 8 copies of each counter: lanes that share a digit (skewed traffic) mostly
+                // hit different words instead of serialising on one
+                if (valid) atomicAdd(&h8[d * 8 + (tid & 7)], 1u);
+#endif
+            }
+            if (valid) {
                 bad |= validate && ((uint64_t)kv[it] >= n_keys);
-                uint32_t sk = (uint32_t)((uint64_t)kv[it] & kmask);
-                if (HOT && any_hot) sk = hot_sortkey((uint32_t)kv[it], hk, hi, nb, r_bits);
-                atomicAdd(&h[(sk >> shift) & (kDigits - 1)], 1u);
                 if (bcount && (i == base || i == last)) {
                     // the tile's first and last bucket low bits (sorted by earlier passes)
                     tile_lo[i == last] = lowbits ? (sk >> r_bits) & ((1u << lowbits) - 1u) : 0u;
@@ -164,7 +211,9 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
             }
         }
         __syncthreads();
-        const uint32_t c = h[tid];
+        uint32_t c = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c += h8[tid * 8 + ((u + tid) & 7)];
         tileprefix[(uint64_t)t * kDigits + tid] = run;
         run += c;
         if (bcount) {
@@ -181,11 +230,30 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
                     acc_lo = lo0;
                 }
                 acc += c;
+            } else if (lo1 - lo0 < 8) {
+                // the lower bits change inside this tile (at most once per value): count
+                // per (lower bits, digit) in LDS, then add each nonzero count once
+                __syncthreads();                     // everyone has read its digit count
+#pragma unroll
+                for (int u = 0; u < 8; ++u) h8[u * kBlock + tid] = 0;
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < kHistItems; ++it) {
+                    const uint64_t i = base + it * kBlock + tid;
+                    const uint32_t bk = skv[it] >> r_bits;
+                    if (i < n) atomicAdd(&h8[((bk & ((1u << lowbits) - 1u)) - lo0) * kBlock + ((bk >> lowbits) & (kDigits - 1))], 1u);
+                }
+                __syncthreads();
+                for (uint32_t u = 0; u <= lo1 - lo0; ++u) {
+                    const uint32_t cnt = h8[u * kBlock + tid];
+                    const uint32_t bk = ((uint32_t)tid << lowbits) | (lo0 + u);
+                    if (cnt && bk < nbt) atomicAdd(&bcount[bk], cnt);
+                }
             } else {
 #pragma unroll
                 for (int it = 0; it < kHistItems; ++it) {
                     const uint64_t i = base + it * kBlock + tid;
-                    const uint32_t bk = (uint32_t)((uint64_t)kv[it] & kmask) >> r_bits;
+                    const uint32_t bk = skv[it] >> r_bits;
                     if (i < n && bk < nbt) atomicAdd(&bcount[bk], 1u);
                 }
             }
@@ -451,8 +519,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
-    __shared__ uint32_t hk[HOT ? kHotSlots : 1], hi[HOT ? kHotSlots : 1];
-    const bool any_hot = HOT && hot_load<kPartBlock>(hot, hk, hi);
+    __shared__ uint64_t hs[HOT ? kHotSlots : 1];
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
     const int tid = threadIdx.x;
@@ -463,6 +530,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     uint64_t rec[kPartItems];
     uint32_t key[kPartItems], lpos[kPartItems];
     bool bad = false;
+    bool any_hot = false;
     if (FIRST) {
         uint64_t kv[kPartItems];
         int32_t pv[kPartItems];
@@ -475,15 +543,22 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
             pv[it] = v ? pin[base + e] : 0;
             tv[it] = v ? tin[base + e] : 0;
         }
+        // the table fill overlaps the tile loads above
+        any_hot = HOT && hot_load<kPartBlock>(hot, hs);
         const int64_t tbase = pack_base(tin, F);
+        uint32_t skv[kPartItems];
+        if (HOT && any_hot) {
+            hot_sortkeys<kPartItems>(kv, hs, nb, r_bits, skv);
+        } else {
+#pragma unroll
+            for (int it = 0; it < kPartItems; ++it) skv[it] = (uint32_t)(kv[it] & F.kmask);
+        }
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
             const int e = it * kPartBlock + tid;
             bad |= (e < nvalid) && (pv[it] < 0 || tv[it] < 0);
-            uint64_t sk = kv[it] & F.kmask;
-            if (HOT && any_hot) sk = hot_sortkey((uint32_t)kv[it], hk, hi, nb, r_bits);
-            rec[it] = pack_rec(sk, pv[it], tv[it], base + e, tbase, F);
-            key[it] = (uint32_t)sk;
+            rec[it] = pack_rec(skv[it], pv[it], tv[it], base + e, tbase, F);
+            key[it] = skv[it];
         }
     } else {
 #pragma unroll
@@ -785,7 +860,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
             if (hcnt[j] >= kHotMin) {
                 const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
-                if (at < kHotKeysMax) hot_next->cand[at] = (uint32_t)(row0 + j);
+                if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)hcnt[j] << 32) | (uint32_t)(row0 + j);
             }
         }
     }
@@ -1065,7 +1140,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
         if (touched) table[key] = S;
         if (e0 - s0 >= kHotMin / 2) {                 // still hot: nominate again
             const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
-            if (at < kHotKeysMax) hot_next->cand[at] = key;
+            if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)(e0 - s0) << 32) | key;
         }
     }
 }
@@ -1098,29 +1173,49 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     }
 }
 
-// The next batch's hot set from this batch's nominations (one 1024-thread workgroup).
+// The next batch's hot set from this batch's nominations (one 1024-thread workgroup):
+// the `cap` busiest nominated keys (bitonic sort of the nominations, descending by
+// their request counts), then their hash table.
 __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, uint32_t cap,
                                                      const uint32_t *__restrict__ err) {
+    __shared__ uint64_t c[kHotCandMax];
     if (*err) return;
     const uint32_t t = threadIdx.x;
-    const uint32_t nc = min(next->n_cand, cap);
-    const uint32_t k = (t < nc) ? next->cand[t] : kHotEmpty;
-    for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot_key[j] = kHotEmpty;
+    const uint32_t nc = min(next->n_cand, kHotCandMax);
+    for (uint32_t j = t; j < kHotCandMax; j += 1024) c[j] = j < nc ? next->cand[j] : 0ull;
+    for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot[j] = kHotSlotEmpty;
     __syncthreads();
-    if (t < nc) {
-        next->key[t] = k;
-        uint32_t h = hot_hash(k);
-        for (;;) {
-            const uint32_t old = atomicCAS(&next->slot_key[h], kHotEmpty, k);
-            if (old == kHotEmpty) {
-                next->slot_idx[h] = t;
-                break;
+    for (uint32_t k = 2; nc > cap && k <= kHotCandMax; k <<= 1) {   // select only when over capacity
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < kHotCandMax; i += 1024) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = c[i], b = c[l];
+                    const bool desc = (i & k) == 0;
+                    if (desc ? (a < b) : (a > b)) {
+                        c[i] = b;
+                        c[l] = a;
+                    }
+                }
             }
-            if (old == k) break;                    // nominated twice: one run is enough
+            __syncthreads();
+        }
+    }
+    const uint32_t nh = min(nc, cap);
+    if (t < nh) {
+        const uint32_t key = (uint32_t)c[t];
+        next->key[t] = key;
+        const unsigned long long mine = ((unsigned long long)t << 32) | key;
+        uint32_t h = hot_hash(key);
+        for (;;) {
+            const unsigned long long old = atomicCAS(
+                reinterpret_cast<unsigned long long *>(&next->slot[h]), kHotSlotEmpty, mine);
+            if (old == kHotSlotEmpty) break;
+            if ((uint32_t)old == key) break;        // nominated twice: one run is enough
             h = (h + 1) & (kHotSlots - 1);
         }
     }
-    if (t == 0) next->count = nc;
+    if (t == 0) next->count = nh;
 }
 
 // ----------------------------------------------------------------------------- queueing kind

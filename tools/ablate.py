@@ -17,9 +17,9 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "wide": ([], ["--no-pack"]),
-    "nohot": ([], ["--no-hot"]),
-    "part1024x8": (["TBE_PART_BLOCK=1024", "TBE_PART_ITEMS=8"], []),
+    "match": (["TBE_HIST_MATCH"], []),
+    "zipf": ([], ["--workload", "zipf", "--zipf-batches", "1"]),
+    "zipf_match": (["TBE_HIST_MATCH"], ["--workload", "zipf", "--zipf-batches", "1"]),
 }
 
 
@@ -31,7 +31,9 @@ def build():
     spec.loader.exec_module(m)
     os.makedirs(OUTDIR, exist_ok=True)
     for name, (defs, _) in VARIANTS.items():
-        m.build_engine(force=True, defines=defs, out=os.path.join(OUTDIR, f"libtbe_{name}.so"))
+        lib = os.path.join(OUTDIR, f"libtbe_{'_'.join(defs) or 'base'}.so")
+        if not os.path.exists(lib):
+            m.build_engine(force=True, defines=defs, out=lib)
         print("built", name)
 
 
@@ -39,7 +41,8 @@ def run(rounds: int, steps: int):
     results = {}
     for r in range(rounds):
         for name, (_, extra) in VARIANTS.items():
-            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{name}.so"))
+            defs = VARIANTS[name][0]
+            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs) or 'base'}.so"))
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps),
                                   "--warmup", "2", "--cpu-seconds", "0"] + extra, env=env, capture_output=True,
                                  text=True, timeout=300)

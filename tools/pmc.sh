@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per run, as MI355X_MICROARCH.md prescribes) over a short
-# bench run; CSVs land in gpurun_out/pmc_<pass>/.  Usage: bash tools/pmc.sh
+# bench run; CSVs land in gpurun_out/pmc_<pass>/.  Usage: [BENCH_ARGS=...] bash tools/pmc.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 pass() {  # pass NAME COUNTERS...
     local name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/pmc_$name" -o run -- \
-        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing \
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing ${BENCH_ARGS:-} \
         > "$OUT/pmc_$name.log" 2>&1
     local rc=$?
     echo "[pmc $name] rc=$rc"
