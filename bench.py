@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-pack", action="store_true",
                     help="wide pass records even where the packed 8-byte form applies (A/B)")
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     return ap.parse_args()
 
 
@@ -96,7 +98,8 @@ def main():
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                             args.period_ticks, device=dev.index,
                             stage_timing=not args.no_stage_timing, max_batch=n,
-                            pack=not args.no_pack, hot=not args.no_hot)
+                            pack=not args.no_pack, hot=not args.no_hot,
+                            pipeline=not args.no_pipeline)
     layout = eng.layout()
     total_steps = args.warmup + args.steps
     seed = (SEED_C if args.workload == "zipf" else SEED_B) + 7919 * rank

@@ -1764,6 +1764,24 @@ struct PassBufs {
     uint32_t *digit_total = nullptr;
 };
 
+// Everything one batch owns while it is in flight: the partition passes' output, the
+// replies before unscatter, the bucket starts and the batch's error flag.  A token-bucket
+// engine keeps two, so batch b+1 can be partitioned while batch b is folded.
+struct Workspace {
+    uint64_t cap_n = 0;
+    std::vector<PassBufs> pass;
+    uint32_t *blocksum = nullptr;
+    uint32_t *res[2] = {nullptr, nullptr};
+    uint32_t *bstart = nullptr;
+    uint32_t *bcount = nullptr;   // requests per bucket of the batch
+    uint32_t *err = nullptr;      // the batch's invalid-request flag
+    uint32_t *segbase = nullptr;  // hot runs
+    SegSummary *summ = nullptr;
+    SegState *sst = nullptr;
+    hipEvent_t done = nullptr;    // recorded after the batch's last kernel
+    bool used = false;
+};
+
 inline int ceil_log2(uint64_t x) {
     int b = 0;
     while ((1ull << b) < x) ++b;
@@ -1783,14 +1801,13 @@ struct tbe_engine {
     int passes = 0;          // 8-bit LSD passes over the bucket id
     bool packed = false;     // token bucket: passes move packed u64 records (PackFmt)
     PackFmt pf{};
-    // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys
+    // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
+    // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
+    // batch b+1 is partitioned by was complete before batch b's fold began.
     uint32_t hot_cap = 0;
     uint32_t nb_total = 0;
-    HotSet *hot[2] = {nullptr, nullptr};   // this batch's set / the next batch's, alternating
-    int hot_cur = 0;
-    uint32_t *segbase = nullptr;
-    SegSummary *summ = nullptr;            // per run segment, sized with the workspace
-    SegState *sst = nullptr;
+    HotSet *hot[3] = {nullptr, nullptr, nullptr};
+    uint64_t nbatch = 0;
     Slot *table = nullptr;
     // queueing kind
     QParams qp{};
@@ -1816,15 +1833,18 @@ struct tbe_engine {
     std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
     std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
 
-    // workspace (sized for `cap_n` requests)
-    uint64_t cap_n = 0;
-    std::vector<PassBufs> pass;
-    uint32_t *blocksum = nullptr;
-    uint32_t *res[2] = {nullptr, nullptr};
-    uint32_t *bstart = nullptr;
-    uint32_t *bcount = nullptr;  // requests per bucket of the current batch
-    uint32_t *err = nullptr;     // [0] per-batch flag, [1] sticky flag
+    // Batch workspaces.  Pipelined (token bucket): batch b uses ws[b % 2]; its partition
+    // passes run on `pstream`, its fold, hot runs and unscatter on `stream`, so the next
+    // batch's partition overlaps this batch's fold.  Other kinds use ws[0] on one stream.
+    Workspace ws[2];
+    int ws_cur = 0;
+    bool pipeline = false;
+    hipStream_t pstream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_out = nullptr;
+    uint32_t *sticky = nullptr;      // set by any skipped batch until tbe_synchronize reads it
+    uint32_t *last_err = nullptr;    // the error flag of the last enqueued batch
     // host-buffer path staging
+    uint64_t stage_cap = 0;
     uint64_t *d_keys = nullptr;
     int32_t *d_permits = nullptr;
     int64_t *d_ts = nullptr;
@@ -1867,8 +1887,9 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
-void free_workspace(tbe_engine *e) {
-    for (auto &pb : e->pass) {
+void free_workspace(Workspace &w) {
+    if (w.used && w.done) (void)hipEventSynchronize(w.done);   // its last batch has finished
+    for (auto &pb : w.pass) {
         dfree(pb.rec);
         dfree(pb.keys);
         dfree(pb.permits);
@@ -1879,18 +1900,27 @@ void free_workspace(tbe_engine *e) {
         dfree(pb.blockprefix);
         dfree(pb.digit_total);
     }
-    e->pass.clear();
-    dfree(e->blocksum);
-    dfree(e->summ);
-    dfree(e->sst);
-    dfree(e->res[0]);
-    dfree(e->res[1]);
+    w.pass.clear();
+    dfree(w.blocksum);
+    dfree(w.summ);
+    dfree(w.sst);
+    dfree(w.segbase);
+    dfree(w.res[0]);
+    dfree(w.res[1]);
+    dfree(w.bstart);
+    dfree(w.bcount);
+    dfree(w.err);
+    w.cap_n = 0;
+    w.used = false;
+}
+
+void free_staging(tbe_engine *e) {
     dfree(e->d_keys);
     dfree(e->d_permits);
     dfree(e->d_ts);
     dfree(e->d_granted);
     dfree(e->d_remaining);
-    e->cap_n = 0;
+    e->stage_cap = 0;
 }
 
 void tiles_for(uint64_t n, uint32_t &ntiles, uint32_t &nblk, uint32_t &tpb) {
@@ -1900,14 +1930,14 @@ void tiles_for(uint64_t n, uint32_t &ntiles, uint32_t &nblk, uint32_t &tpb) {
     nblk = (ntiles + tpb - 1) / tpb;
 }
 
-tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
-    if (n <= e->cap_n) return TBE_OK;
-    free_workspace(e);
+tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
+    if (n <= w.cap_n) return TBE_OK;
+    free_workspace(w);
     uint64_t cap = std::max<uint64_t>(n, 1u << 16);
     uint32_t ntiles, nblk, tpb;
     tiles_for(cap, ntiles, nblk, tpb);
-    e->pass.resize(e->passes);
-    for (auto &pb : e->pass) {
+    w.pass.resize(e->passes);
+    for (auto &pb : w.pass) {
         if (e->packed) {
             HIP_TRY(e, hipMalloc(&pb.rec, cap * sizeof(uint64_t)));
         } else {
@@ -1921,30 +1951,33 @@ tbe_status ensure_workspace(tbe_engine *e, uint64_t n) {
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.digit_total, kDigits * sizeof(uint32_t)));
     }
-    HIP_TRY(e, hipMalloc(&e->blocksum, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.blocksum, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
     if (e->hot_cap) {
         const uint64_t segs = cap / kSeg + kHotKeysMax + 1;
-        HIP_TRY(e, hipMalloc(&e->summ, segs * sizeof(SegSummary)));
-        HIP_TRY(e, hipMalloc(&e->sst, segs * sizeof(SegState)));
+        HIP_TRY(e, hipMalloc(&w.summ, segs * sizeof(SegSummary)));
+        HIP_TRY(e, hipMalloc(&w.sst, segs * sizeof(SegState)));
+        HIP_TRY(e, hipMalloc(&w.segbase, (kHotKeysMax + 1) * sizeof(uint32_t)));
     }
-    HIP_TRY(e, hipMalloc(&e->res[0], cap * sizeof(uint32_t)));
-    HIP_TRY(e, hipMalloc(&e->res[1], cap * sizeof(uint32_t)));
-    e->cap_n = cap;
+    HIP_TRY(e, hipMalloc(&w.res[0], cap * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.res[1], cap * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.bcount, (uint64_t)e->nb_total * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.err, sizeof(uint32_t)));
+    w.cap_n = cap;
     return TBE_OK;
 }
 
 tbe_status ensure_host_staging(tbe_engine *e, uint64_t n) {
-    // Staging for the host-buffer entry point lives with the workspace; reallocated with it.
-    if (e->d_keys && n <= e->cap_n) return TBE_OK;
-    tbe_status st = ensure_workspace(e, n);
-    if (st != TBE_OK) return st;
-    if (!e->d_keys) {
-        HIP_TRY(e, hipMalloc(&e->d_keys, e->cap_n * sizeof(uint64_t)));
-        HIP_TRY(e, hipMalloc(&e->d_permits, e->cap_n * sizeof(int32_t)));
-        HIP_TRY(e, hipMalloc(&e->d_ts, e->cap_n * sizeof(int64_t)));
-        HIP_TRY(e, hipMalloc(&e->d_granted, e->cap_n * sizeof(uint8_t)));
-        HIP_TRY(e, hipMalloc(&e->d_remaining, e->cap_n * sizeof(int32_t)));
-    }
+    // Staging for the host-buffer entry points (each such call synchronises before it returns).
+    if (n <= e->stage_cap) return TBE_OK;
+    free_staging(e);
+    const uint64_t cap = std::max<uint64_t>(n, 1u << 16);
+    HIP_TRY(e, hipMalloc(&e->d_keys, cap * sizeof(uint64_t)));
+    HIP_TRY(e, hipMalloc(&e->d_permits, cap * sizeof(int32_t)));
+    HIP_TRY(e, hipMalloc(&e->d_ts, cap * sizeof(int64_t)));
+    HIP_TRY(e, hipMalloc(&e->d_granted, cap * sizeof(uint8_t)));
+    HIP_TRY(e, hipMalloc(&e->d_remaining, cap * sizeof(int32_t)));
+    e->stage_cap = cap;
     return TBE_OK;
 }
 
@@ -1970,165 +2003,200 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
     (void)hipEventRecord(e->ev_pool[e->ev_marks.back().second + 1], st);
 }
 
-// Enqueue the whole pipeline for one device-resident batch.
+// Enqueue the whole pipeline for one device-resident batch.  `caller` is the stream the
+// inputs were produced on and the replies are awaited on; NULL: the inputs are complete
+// at the call and the replies are ordered on the engine's stream.
+//
+// Pipelined engines (token bucket) split a batch over two streams: the partition passes
+// and the bucket starts run on pstream (sp), the fold, hot runs and unscatter, the only
+// kernels that touch the table, on the engine's stream (sf).  Batch b+1's partition then
+// runs while batch b is folded: it reads only its inputs, its own workspace (free once
+// batch b-1 is done) and hot[(b+1) % 3] (complete since batch b-1's hot update).
 tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                      const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
-                     hipStream_t st, int64_t id_base = 0) {
+                     hipStream_t caller, int64_t id_base = 0) {
     const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
     const bool wait = e->cfg.kind != TBE_KIND_TOKEN_BUCKET;   // status-packed replies
     if (n == 0) return TBE_OK;
     if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
                                        (unsigned long long)n);
-    tbe_status rc = ensure_workspace(e, n);
+    const bool pipe = e->pipeline;
+    Workspace &w = e->ws[pipe ? e->ws_cur : 0];
+    tbe_status rc = ensure_workspace(e, w, n);
     if (rc != TBE_OK) return rc;
     uint32_t ntiles, nblk, tpb;
     tiles_for(n, ntiles, nblk, tpb);
-    HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(uint32_t), st));
+    hipStream_t sf = caller ? caller : e->stream, sp = sf;
+    if (pipe) {
+        sf = e->stream;
+        sp = e->pstream;
+        if (caller) {
+            HIP_TRY(e, hipEventRecord(e->ev_in, caller));
+            HIP_TRY(e, hipStreamWaitEvent(sp, e->ev_in, 0));
+        }
+        if (w.used) HIP_TRY(e, hipStreamWaitEvent(sp, w.done, 0));
+    }
+    HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
-    HIP_TRY(e, hipMemsetAsync(e->bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), st));
-    // hot runs: this batch partitions by hot[cur] and nominates into hot[cur ^ 1]
-    HotSet *hot = e->hot_cap ? e->hot[e->hot_cur] : nullptr;
-    HotSet *hot_next = e->hot_cap ? e->hot[e->hot_cur ^ 1] : nullptr;
-    if (hot_next) HIP_TRY(e, hipMemsetAsync(&hot_next->n_cand, 0, sizeof(uint32_t), st));
+    HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
+    // hot runs: see tbe_engine::hot
+    HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
+    HotSet *hot_next = e->hot_cap ? e->hot[(e->nbatch + 2) % 3] : nullptr;
     for (int p = 0; p < e->passes; ++p) {
         const int shift = e->r_bits + kDigitBits * p;
-        PassBufs &out = e->pass[p];
-        stage_begin(e, ST_HIST, st);
+        PassBufs &out = w.pass[p];
+        stage_begin(e, ST_HIST, sp);
         // the last pass also counts requests per bucket (k_bscan turns them into bstart)
-        uint32_t *bc = (p == e->passes - 1) ? e->bcount : nullptr;
+        uint32_t *bc = (p == e->passes - 1) ? w.bcount : nullptr;
         const int lowbits = kDigitBits * p;
         if (p == 0 && hot)
-            k_hist<uint64_t, true><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
-                                                             e->blocksum, e->cfg.n_keys, e->err, 1, kmask,
+            k_hist<uint64_t, true><<<nblk, kBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+                                                             w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                              hot, e->nbuckets, e->r_bits, bc, lowbits,
                                                              e->nb_total);
         else if (p == 0)
-            k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
-                                                       e->blocksum, e->cfg.n_keys, e->err, 1, kmask,
+            k_hist<uint64_t><<<nblk, kBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+                                                       w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total);
         else if (e->packed)
-            k_hist<uint64_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].rec, n, shift, tpb, ntiles,
-                                                       out.tileprefix, e->blocksum, e->cfg.n_keys,
-                                                       e->err, 0, kmask, nullptr, e->nbuckets,
+            k_hist<uint64_t><<<nblk, kBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
+                                                       out.tileprefix, w.blocksum, e->cfg.n_keys,
+                                                       w.err, 0, kmask, nullptr, e->nbuckets,
                                                        e->r_bits, bc, lowbits, e->nb_total);
         else
-            k_hist<uint32_t><<<nblk, kBlock, 0, st>>>(e->pass[p - 1].keys, n, shift, tpb, ntiles,
-                                                       out.tileprefix, e->blocksum, e->cfg.n_keys,
-                                                       e->err, 0, kmask, nullptr, e->nbuckets,
+            k_hist<uint32_t><<<nblk, kBlock, 0, sp>>>(w.pass[p - 1].keys, n, shift, tpb, ntiles,
+                                                       out.tileprefix, w.blocksum, e->cfg.n_keys,
+                                                       w.err, 0, kmask, nullptr, e->nbuckets,
                                                        e->r_bits, bc, lowbits, e->nb_total);
-        stage_end(e, ST_HIST, st);
-        stage_begin(e, ST_COLSCAN, st);
-        k_colscan<<<kDigits, kBlock, 0, st>>>(e->blocksum, nblk, out.blockprefix, out.digit_total);
-        stage_end(e, ST_COLSCAN, st);
-        stage_begin(e, ST_SCATTER, st);
+        stage_end(e, ST_HIST, sp);
+        stage_begin(e, ST_COLSCAN, sp);
+        k_colscan<<<kDigits, kBlock, 0, sp>>>(w.blocksum, nblk, out.blockprefix, out.digit_total);
+        stage_end(e, ST_COLSCAN, sp);
+        stage_begin(e, ST_SCATTER, sp);
         if (e->packed && p == 0 && hot)
-            k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, st>>>(
+            k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, e->err, hot, e->nbuckets, e->r_bits);
+                out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits);
         else if (e->packed && p == 0)
-            k_scatter_rec<true><<<ntiles, kPartBlock, 0, st>>>(
+            k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, e->err);
+                out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed)
-            k_scatter_rec<false><<<ntiles, kPartBlock, 0, st>>>(
-                nullptr, nullptr, nullptr, e->pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
-                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, e->err);
+            k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (approx && p == 0)
-            k_scatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
+            k_scatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, nullptr, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.perm, e->err, 1);
+                out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.perm, w.err, 1);
         else if (approx)
-            k_scatter<uint32_t, true, false><<<ntiles, kPartBlock, 0, st>>>(
-                e->pass[p - 1].keys, e->pass[p - 1].permits, nullptr, e->pass[p - 1].idx, n, shift,
+            k_scatter<uint32_t, true, false><<<ntiles, kPartBlock, 0, sp>>>(
+                w.pass[p - 1].keys, w.pass[p - 1].permits, nullptr, w.pass[p - 1].idx, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits, nullptr,
-                out.idx, out.perm, e->err, 0);
+                out.idx, out.perm, w.err, 0);
         else if (p == 0 && !wait)
-            k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, st>>>(
+            k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.perm, e->err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.perm, w.err, 1);
         else if (p == 0)
-            k_scatter<uint64_t, true><<<ntiles, kPartBlock, 0, st>>>(
+            k_scatter<uint64_t, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, out.perm, e->err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, out.perm, w.err, 1);
         else if (!wait)
-            k_scatter<uint32_t, false><<<ntiles, kPartBlock, 0, st>>>(
-                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, nullptr, n, shift,
+            k_scatter<uint32_t, false><<<ntiles, kPartBlock, 0, sp>>>(
+                w.pass[p - 1].keys, w.pass[p - 1].permits, w.pass[p - 1].ts, nullptr, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits,
-                out.ts, nullptr, out.perm, e->err, 0);
+                out.ts, nullptr, out.perm, w.err, 0);
         else
-            k_scatter<uint32_t, true><<<ntiles, kPartBlock, 0, st>>>(
-                e->pass[p - 1].keys, e->pass[p - 1].permits, e->pass[p - 1].ts, e->pass[p - 1].idx,
+            k_scatter<uint32_t, true><<<ntiles, kPartBlock, 0, sp>>>(
+                w.pass[p - 1].keys, w.pass[p - 1].permits, w.pass[p - 1].ts, w.pass[p - 1].idx,
                 n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys,
-                out.permits, out.ts, out.idx, out.perm, e->err, 0);
-        stage_end(e, ST_SCATTER, st);
+                out.permits, out.ts, out.idx, out.perm, w.err, 0);
+        stage_end(e, ST_SCATTER, sp);
     }
-    const PassBufs &sorted = e->pass[e->passes - 1];
-    stage_begin(e, ST_BOUNDS, st);
-    k_bscan<<<1, 1024, 0, st>>>(e->bcount, e->nb_total, e->bstart);
-    stage_end(e, ST_BOUNDS, st);
-    stage_begin(e, ST_FOLD, st);
+    const PassBufs &sorted = w.pass[e->passes - 1];
+    stage_begin(e, ST_BOUNDS, sp);
+    k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart);
+    stage_end(e, ST_BOUNDS, sp);
+    if (pipe) {
+        HIP_TRY(e, hipEventRecord(e->ev_part, sp));
+        HIP_TRY(e, hipStreamWaitEvent(sf, e->ev_part, 0));
+    }
+    // hot_next was last read by batch b-1's partition and hot runs, both done by now
+    if (hot_next) HIP_TRY(e, hipMemsetAsync(&hot_next->n_cand, 0, sizeof(uint32_t), sf));
+    stage_begin(e, ST_FOLD, sf);
     if (approx) {
         AParams a = e->ap;
         a.id_base = id_base;
         a.wait = e->wait_mode;
-        k_fold_a<<<e->nbuckets, kFoldBlock, 0, st>>>(
-            sorted.keys, sorted.permits, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys, e->alocal,
-            e->ring, a, e->res[0], e->ev_cause, e->ev_id, e->counters,
-            (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), e->err);
+        k_fold_a<<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            sorted.keys, sorted.permits, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
+            e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
+            (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
         q.wait = e->wait_mode;
-        k_fold_q<<<e->nbuckets, kBlock, 0, st>>>(
-            sorted.keys, sorted.permits, sorted.ts, sorted.idx, e->bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->qhdr, e->ring, e->params, q, e->res[0], e->ev_cause, e->ev_id,
-            e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), e->err);
+        k_fold_q<<<e->nbuckets, kBlock, 0, sf>>>(
+            sorted.keys, sorted.permits, sorted.ts, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys,
+            e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
+            e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (e->packed) {
-        k_fold<true><<<e->nbuckets, kFoldBlock, 0, st>>>(
-            nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, e->bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, e->res[0], e->err, hot_next);
+        k_fold<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+            e->table, e->params, w.res[0], w.err, hot_next);
     } else {
-        k_fold<false><<<e->nbuckets, kFoldBlock, 0, st>>>(
-            sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, e->bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, e->res[0], e->err, nullptr);
+        k_fold<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr);
     }
-    stage_end(e, ST_FOLD, st);
+    stage_end(e, ST_FOLD, sf);
     if (hot) {
         // runs of this batch's hot keys, after the fold (which may write back a hot key's
-        // unchanged row as part of its bucket's slice), then the next batch's hot set
-        stage_begin(e, ST_HOT, st);
+        // unchanged row as part of its bucket's slice), then the hot set of batch b+2
+        stage_begin(e, ST_HOT, sf);
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
-        k_hot_plan<<<1, 1024, 0, st>>>(hot, e->bstart, e->nbuckets, e->segbase, e->err);
-        k_hot_summary<<<sgrid, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets,
-                                                   e->segbase, e->summ, e->err);
-        k_hot_chain<<<e->hot_cap, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets, hot,
-                                                      hot_next, e->segbase, e->summ, e->sst, e->table,
-                                                      e->params, e->res[0], e->err);
-        k_hot_replies<<<sgrid, kSegBlock, 0, st>>>(sorted.rec, ts, e->pf, e->bstart, e->nbuckets,
-                                                   e->segbase, e->sst, e->params, e->res[0], e->err);
-        k_hot_update<<<1, 1024, 0, st>>>(hot_next, e->hot_cap, e->err);
-        stage_end(e, ST_HOT, st);
-        e->hot_cur ^= 1;
+        k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
+        k_hot_summary<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
+                                                   w.segbase, w.summ, w.err);
+        k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
+                                                      hot_next, w.segbase, w.summ, w.sst, e->table,
+                                                      e->params, w.res[0], w.err);
+        k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
+                                                   w.segbase, w.sst, e->params, w.res[0], w.err);
+        k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap, w.err);
+        stage_end(e, ST_HOT, sf);
     }
-    stage_begin(e, ST_UNSCATTER, st);
+    stage_begin(e, ST_UNSCATTER, sf);
     const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        k_unscatter<false, false><<<untiles, kUnBlock, 0, st>>>(n, e->pass[p].perm, e->res[cur],
-                                                                e->res[cur ^ 1], nullptr, nullptr);
+        k_unscatter<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
     if (wait)
-        k_unscatter<true, true><<<untiles, kUnBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+        k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                               nullptr, granted, remaining);
     else
-        k_unscatter<true, false><<<untiles, kUnBlock, 0, st>>>(n, e->pass[0].perm, e->res[cur],
+        k_unscatter<true, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                nullptr, granted, remaining);
-    stage_end(e, ST_UNSCATTER, st);
-    k_sticky<<<1, 64, 0, st>>>(e->err, e->err + 1);
+    stage_end(e, ST_UNSCATTER, sf);
+    k_sticky<<<1, 64, 0, sf>>>(w.err, e->sticky);
     HIP_TRY(e, hipGetLastError());
+    if (pipe) {
+        HIP_TRY(e, hipEventRecord(w.done, sf));
+        w.used = true;
+        if (caller && caller != sf) {
+            HIP_TRY(e, hipEventRecord(e->ev_out, sf));
+            HIP_TRY(e, hipStreamWaitEvent(caller, e->ev_out, 0));
+        }
+        e->ws_cur ^= 1;
+    }
+    e->last_err = w.err;
+    ++e->nbatch;
     return TBE_OK;
 }
 
@@ -2238,20 +2306,20 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
     e->own_stream = true;
+    e->pipeline = c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_NO_PIPELINE) == 0;
+    if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
+        return bail(TBE_EDEVICE);
+    for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ws[0].done, &e->ws[1].done})
+        if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(TBE_EDEVICE);
     if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
-    if (hipMalloc(&e->bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)) != hipSuccess)
-        return bail(TBE_ENOMEM);
-    if (hipMalloc(&e->bcount, (uint64_t)e->nb_total * sizeof(uint32_t)) != hipSuccess)
-        return bail(TBE_ENOMEM);
     if (e->hot_cap) {
         for (auto &hs : e->hot) {
             if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
             if (hipMemsetAsync(hs, 0, sizeof(HotSet), e->stream) != hipSuccess) return bail(TBE_EDEVICE);
         }
-        if (hipMalloc(&e->segbase, (kHotKeysMax + 1) * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     }
-    if (hipMalloc(&e->err, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
-    if (hipMemsetAsync(e->err, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess)
+    if (hipMalloc(&e->sticky, sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), e->stream) != hipSuccess)
         return bail(TBE_EDEVICE);
     k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
     if (c.kind == TBE_KIND_QUEUEING) {
@@ -2283,7 +2351,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,
                                                    c.token_limit);
     }
-    if (c.max_batch && ensure_workspace(e, c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
+    for (int i = 0; i < (e->pipeline ? 2 : 1); ++i)
+        if (c.max_batch && ensure_workspace(e, e->ws[i], c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(TBE_EDEVICE);
     *out_engine = e;
     return TBE_OK;
@@ -2291,8 +2360,11 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
 
 void tbe_destroy(tbe_engine *e) {
     if (!e) return;
+    if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    free_workspace(e);
+    free_workspace(e->ws[0]);
+    free_workspace(e->ws[1]);
+    free_staging(e);
     dfree(e->table);
     dfree(e->alocal);
     dfree(e->aclient);
@@ -2308,14 +2380,13 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->log_keyseq);
     dfree(e->log_id);
     dfree(e->log_rem);
-    dfree(e->bstart);
-    dfree(e->bcount);
-    dfree(e->err);
-    dfree(e->hot[0]);
-    dfree(e->hot[1]);
-    dfree(e->segbase);
+    dfree(e->sticky);
+    for (auto &hs : e->hot) dfree(hs);
     for (auto &ev : e->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ws[0].done, e->ws[1].done})
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->pstream) (void)hipStreamDestroy(e->pstream);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -2342,12 +2413,12 @@ tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t 
     rc = run_batch(e, e->d_keys, e->d_permits, e->d_ts, n, e->d_granted, e->d_remaining, st);
     if (rc != TBE_OK) return rc;
     uint32_t flag = 0;
-    HIP_TRY(e, hipMemcpyAsync(&flag, e->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(&flag, e->last_err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipMemcpyAsync(granted, e->d_granted, n, hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipStreamSynchronize(st));
     if (flag) {
-        HIP_TRY(e, hipMemsetAsync(e->err + 1, 0, sizeof(uint32_t), st));
+        HIP_TRY(e, hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), st));
         HIP_TRY(e, hipStreamSynchronize(st));
         return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
     }
@@ -2363,8 +2434,7 @@ tbe_status tbe_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys, const
     if (!d_keys || !d_permits || !d_ts_us || !d_granted || !d_remaining)
         return fail(e, TBE_EINVAL, "null buffer");
     HIP_TRY(e, hipSetDevice(e->device));
-    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
-    return run_batch(e, d_keys, d_permits, d_ts_us, n, d_granted, d_remaining, st);
+    return run_batch(e, d_keys, d_permits, d_ts_us, n, d_granted, d_remaining, (hipStream_t)stream);
 }
 
 tbe_status tbe_synchronize(tbe_engine *e) {
@@ -2372,9 +2442,9 @@ tbe_status tbe_synchronize(tbe_engine *e) {
     HIP_TRY(e, hipSetDevice(e->device));
     HIP_TRY(e, hipDeviceSynchronize());
     uint32_t sticky = 0;
-    HIP_TRY(e, hipMemcpy(&sticky, e->err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(&sticky, e->sticky, sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (sticky) {
-        HIP_TRY(e, hipMemset(e->err + 1, 0, sizeof(uint32_t)));
+        HIP_TRY(e, hipMemset(e->sticky, 0, sizeof(uint32_t)));
         return fail(e, TBE_EINVAL, "an enqueued batch held an invalid request and was skipped");
     }
     return TBE_OK;
@@ -2483,13 +2553,13 @@ static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_
                    e->d_remaining, st, id_base);
     if (rc != TBE_OK) return rc;
     uint32_t flag = 0, nev = 0;
-    HIP_TRY(e, hipMemcpyAsync(&flag, e->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipMemcpyAsync(&flag, e->last_err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipMemcpyAsync(&nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipMemcpyAsync(status, e->d_granted, n, hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipStreamSynchronize(st));
     if (flag) {
-        HIP_TRY(e, hipMemsetAsync(e->err + 1, 0, sizeof(uint32_t), st));
+        HIP_TRY(e, hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), st));
         HIP_TRY(e, hipStreamSynchronize(st));
         return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
     }
@@ -2714,7 +2784,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     if (!e || !passes || !r_bits || !packed) return TBE_EINVAL;
     *passes = (uint32_t)e->passes;
     *r_bits = (uint32_t)e->r_bits;
-    *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u);
+    *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u);
     return TBE_OK;
 }
 

@@ -71,7 +71,10 @@ typedef struct tbe_config {
                                              the packed 8-byte form applies (A/B checks) */
 #define TBE_FLAG_NO_HOT 0x4u              /* token bucket: no hot-key runs (A/B checks); keys
                                              that take >= 2048 requests of a batch otherwise get
-                                             a run of their own in the next batch */
+                                             a run of their own two batches later */
+#define TBE_FLAG_NO_PIPELINE 0x8u         /* token bucket: run every stage of a batch on one
+                                             stream (A/B checks); by default batch b+1's
+                                             partition overlaps batch b's fold */
 
 typedef struct tbe_engine tbe_engine;
 
@@ -101,9 +104,14 @@ tbe_status tbe_acquire_batch(tbe_engine *engine, const uint64_t *keys, const int
                              const int64_t *ts_us, uint64_t n, uint8_t *granted,
                              int32_t *remaining);
 
-/* Same decision on device-resident buffers, enqueued on `stream` (a hipStream_t, or
- * NULL for the engine's own stream).  Returns once enqueued; a batch found invalid
- * on the device is skipped (no state change) and reported by tbe_synchronize. */
+/* Same decision on device-resident buffers.  Returns once enqueued; a batch found
+ * invalid on the device is skipped (no state change) and reported by tbe_synchronize.
+ * `stream` (a hipStream_t): the engine waits on it for the inputs and makes it wait for
+ * the replies, so work enqueued on it afterwards may read the replies and overwrite the
+ * inputs.  NULL: the inputs must be complete when the call is made and stay untouched
+ * until the replies are; the replies are complete at tbe_synchronize (or for any later
+ * call on this engine).  Batches are applied in call order either way; consecutive
+ * batches of a token-bucket engine overlap on the device (TBE_FLAG_NO_PIPELINE). */
 tbe_status tbe_acquire_batch_device(tbe_engine *engine, const uint64_t *d_keys,
                                     const int32_t *d_permits, const int64_t *d_ts_us,
                                     uint64_t n, uint8_t *d_granted, int32_t *d_remaining,
@@ -213,7 +221,8 @@ tbe_status tbe_approx_query(tbe_engine *engine, uint64_t key, int32_t *local, in
  * passes over the bucket id, *r_bits = log2 of the keys per bucket (one workgroup
  * each), *packed: bit 0 set when the passes move packed 8-byte request records (token
  * bucket kind) rather than the wide {key, permits, ts} records, bit 1 set
- * when hot keys get runs of their own (TBE_FLAG_NO_HOT clears it). */
+ * when hot keys get runs of their own (TBE_FLAG_NO_HOT clears it), bit 2 set when
+ * consecutive device batches overlap (TBE_FLAG_NO_PIPELINE clears it). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* Per-stage device time (ms) accumulated since the last call, when
