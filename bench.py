@@ -11,8 +11,10 @@ Multi-GPU (torchrun, one rank per GPU): keys are hash-partitioned, each rank own
 collective: weak scaling).  value = all ranks' decisions / max-over-ranks time.
 
 Also reported: per-stage device time, the roofline of the dominant kernel (HIP events
-on the engine stream over the timed region), and the CPU baseline (the C restatement
-of the reference script, oracle/tb_ref.c, on a bounded sample of the same trace).
+on the engine stream; for the pipelined engine, over a serial replay of the same timed
+batches, since overlapped stages share the chip), and the CPU baseline (the C
+restatement of the reference script, oracle/tb_ref.c, on a bounded sample of the same
+trace).
 """
 from __future__ import annotations
 
@@ -40,18 +42,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("uniform", "zipf"), default="uniform",
-                    help="uniform: config B (the headline); zipf: config C's per-GPU slice")
+    ap.add_argument("--workload", choices=("uniform", "zipf", "queue", "approx"), default="uniform",
+                    help="uniform: config B (the headline); zipf: config C's per-GPU slice; "
+                         "queue: config D (TokenBucketWithQueue); approx: config E (two-tier)")
     ap.add_argument("--keys", type=int, default=None,
                     help="total keys (uniform, default 1e8) / keys per GPU (zipf, default 1.25e8)")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     ap.add_argument("--zipf-batches", type=int, default=2,
                     help="distinct Zipf key batches drawn on the host, reused in turn")
     ap.add_argument("--batch", type=int, default=1 << 26)
-    ap.add_argument("--interval-us", type=int, default=10_000)
-    ap.add_argument("--token-limit", type=int, default=10)
+    ap.add_argument("--interval-us", type=int, default=None,
+                    help="injected time per batch (default 10 ms; 1 ms for queue)")
+    ap.add_argument("--token-limit", type=int, default=None,
+                    help="TokenLimit (default 10; 4 for queue, 100 for approx)")
+    ap.add_argument("--queue-limit", type=int, default=16)
     ap.add_argument("--tokens-per-period", type=int, default=1)
-    ap.add_argument("--period-ticks", type=int, default=10_000_000)
+    ap.add_argument("--period-ticks", type=int, default=None,
+                    help="ReplenishmentPeriod in 100 ns ticks (default 1 s; approx: one batch interval)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate CPU-baseline budget (0 disables)")
     ap.add_argument("--no-stage-timing", action="store_true")
@@ -60,7 +67,16 @@ def parse():
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.interval_us is None:
+        args.interval_us = 1_000 if args.workload == "queue" else 10_000
+    if args.token_limit is None:
+        args.token_limit = {"queue": 4, "approx": 100}.get(args.workload, 10)
+    if args.period_ticks is None:
+        args.period_ticks = args.interval_us * 10 if args.workload == "approx" else 10_000_000
+    if args.workload == "approx" and args.tokens_per_period == 1:
+        args.tokens_per_period = 10
+    return args
 
 
 def main():
@@ -83,6 +99,14 @@ def main():
     lib.tbe_gen_batch_device.restype = ctypes.c_int
     lib.tbe_gen_batch_device.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_int32] * 2 + \
         [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 4
+    if args.workload in ("queue", "approx"):
+        import bench_kinds
+        line = bench_kinds.run(args, lib, dev, world, rank, dist)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            td.destroy_process_group()
+        return
 
     # Hash partition: this rank owns keys_local = ceil(K / world) dense local ids.  The
     # synthetic stream is generated directly in the rank's local id space (uniform keys
@@ -145,12 +169,37 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         elapsed = float(tt.item())
-    stages = eng.stage_times()
+    stages_overlapped = eng.stage_times()
     grant_rate = float(granted.float().mean().item())
 
     decisions = n * args.steps * world
     value = decisions / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- per-kernel times for the roofline.  A pipelined engine overlaps batch b+1's
+    # partition with batch b's fold, so its per-stage event intervals include the time the
+    # two share the chip.  Kernel durations are therefore taken from a serial replay (one
+    # stream, pipeline off) of exactly the same warm-up + timed batches on a second engine,
+    # right after the timed region; its replies must equal the pipelined run's.
+    stages, replay_check = stages_overlapped, None
+    if layout.get("pipeline") and not args.no_stage_timing:
+        eng.close()
+        ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
+                                args.period_ticks, device=dev.index, stage_timing=True,
+                                max_batch=n, pack=not args.no_pack, hot=not args.no_hot,
+                                pipeline=False)
+        g2 = torch.empty_like(granted)
+        r2 = torch.empty_like(remaining)
+        for s in range(args.warmup):
+            ser.acquire_batch_device(*bufs[s], g2, r2)
+        ser.synchronize()
+        ser.stage_times()
+        for s in range(args.warmup, total_steps):
+            ser.acquire_batch_device(*bufs[s], g2, r2)
+        ser.synchronize()
+        stages = ser.stage_times()
+        replay_check = bool(torch.equal(g2, granted) and torch.equal(r2, remaining))
+        eng = ser
 
     # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
     roofline = None
@@ -168,7 +217,14 @@ def main():
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": pmc_traffic(name), "alg_bytes_per_launch": alg_bytes,
-                    "avg_launch_ms": round(per_launch_ms, 4)}
+                    "avg_launch_ms": round(per_launch_ms, 4),
+                    "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
+                               "engine stream" if replay_check is not None else
+                               "HIP events on the engine stream over the timed region")}
+        if replay_check is not None:
+            roofline["overlapped_avg_launch_ms"] = round(
+                stages_overlapped.get(name, 0.0) / (args.steps * launches[name]), 4)
+            roofline["replay_replies_identical"] = replay_check
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -198,6 +254,9 @@ def main():
                        "layout": layout},
             "grant_rate_last_batch": round(grant_rate, 4),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
+            "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
+                                              for k, v in stages_overlapped.items()}
+                                             if replay_check is not None else None),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -1,0 +1,317 @@
+"""bench.py --workload queue | approx: SURVEY.md §8d configs D and E.
+
+Config D (TokenBucketWithQueue, Q): 1e8 keys (ceil(1e8 / N) per rank), 2^26-request
+batches, permits 1, TokenLimit 4, 1 token / s, QueueLimit 16, OldestFirst, 1 ms of
+injected time per batch (demand >> fill, so queues saturate).  A step is one
+WaitAsyncCore batch (tbe_wait_batch_device) plus the replenish tick at the batch's end
+(tbe_refresh_device, Q:237-271), both on device buffers.
+
+Config E (ApproximateTokenBucket, A): 1e7 shared keys replicated on every rank, each rank
+decides its own 2^26 AcquireCore requests per batch over them, then one refresh epoch:
+collect the local counts (A:430-435), exchange them between the ranks (RCCL all-gather
+over xGMI; nothing to exchange at N = 1), and replay the sync script for every client in
+rank order with staggered timestamps T + r*P/N (A:241-270, SURVEY.md §8e option 2).
+
+value = all ranks' requests / max-over-ranks time (weak scaling); per-stage times come
+from the engine's HIP events, the refresh kernels' from HIP events on the same stream.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+HBM_PEAK_GBS = 8000.0
+SEED_D = 0x5EED000D
+SEED_E = 0x5EED000E
+T0_US = 1_760_000_000_000_000
+METRIC = "acquire decisions/sec (node) at 100M keys, 1/2/4/8 GPU; % HBM roofline"
+
+
+def _gen(lib, seed, n_keys, s, n, interval_us, dev):
+    k = torch.empty(n, dtype=torch.int64, device=dev)
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    t = torch.empty(n, dtype=torch.int64, device=dev)
+    rc = lib.tbe_gen_batch_device(seed, n_keys, s * n, n, 1, 1, T0_US + s * interval_us, interval_us,
+                                  k.data_ptr(), p.data_ptr(), t.data_ptr(), None)
+    assert rc == 0
+    return k, p, t
+
+
+def _distinct(n: int, k: int) -> float:
+    return k * (1.0 - np.exp(-n / k))
+
+
+def _roofline(name, alg_bytes, ms, note):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4),
+            "alg_bytes_note": note,
+            "timing": "HIP events on the engine's launch stream over the timed region"}
+
+
+def run(args, lib, dev, world, rank, dist):
+    if args.workload == "queue":
+        return run_queue(args, lib, dev, world, rank, dist)
+    return run_approx(args, lib, dev, world, rank, dist)
+
+
+def _barrier_time(dist, dev, t0):
+    torch.cuda.synchronize()
+    if dist:
+        import torch.distributed as td
+        td.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch.distributed as td
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        td.all_reduce(tt, op=td.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
+
+
+def run_queue(args, lib, dev, world, rank, dist):
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine
+
+    keys_total = args.keys or 100_000_000
+    kl = (keys_total + world - 1) // world
+    n, steps, warm = args.batch, args.steps, args.warmup
+    total = warm + steps
+    eng = QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, args.period_ticks,
+                                    args.queue_limit, 0, device=dev.index,
+                                    stage_timing=not args.no_stage_timing, max_batch=n)
+    seed = SEED_D + 7919 * rank
+    bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    rem = torch.empty(n, dtype=torch.int32, device=dev)
+    # drain log: a tick grants at most min(QueueLimit, TokenLimit) entries per key
+    cap = min(kl * min(max(1, args.queue_limit), args.token_limit), total * n)
+    lk = torch.empty(cap, dtype=torch.int64, device=dev)
+    li = torch.empty(cap, dtype=torch.int64, device=dev)
+    lr = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    # a stream of our own (the default stream's handle is NULL, which the engine reads as
+    # "its own stream"), so the drain's HIP events sit on the stream the kernels run on
+    stream = torch.cuda.Stream(dev)
+    sh = stream.cuda_stream
+    torch.cuda.synchronize()
+
+    def step(s, ev=None):
+        eng.wait_batch_device(*bufs[s], st, rem, id_base=s * n, stream=sh)
+        if ev:
+            ev[0].record(stream)
+        eng.refresh_device(T0_US + (s + 1) * args.interval_us, lk, li, lr, cnt, stream=sh)
+        if ev:
+            ev[1].record(stream)
+
+    for s in range(warm):
+        step(s)
+    torch.cuda.synchronize()
+    eng.synchronize()
+    eng.stage_times()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    queued = torch.zeros((), dtype=torch.int64, device=dev)
+    drained = torch.zeros((), dtype=torch.int64, device=dev)
+    if dist:
+        import torch.distributed as td
+        td.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, s in enumerate(range(warm, total)):
+        step(s, evs[i])
+    elapsed = _barrier_time(dist, dev, t0)
+    eng.synchronize()
+    stages = eng.stage_times()
+    drain_ms = sum(a.elapsed_time(b) for a, b in evs)
+    # outcome mix of the last batch and its tick (outside the timed region)
+    queued += (st == 2).sum()
+    drained += cnt.sum()
+    q_last, d_last = int(queued.item()), int(drained.item())
+    granted = float((st == 1).float().mean().item())
+
+    value = n * steps * world / elapsed
+    passes = eng.layout()["passes"]
+    stages["drain"] = drain_ms
+    launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
+                "unscatter": passes, "hot": 1, "drain": 1}
+    name = max(stages, key=stages.get)
+    ms = stages[name] / (steps * launches[name])
+    u = _distinct(n, kl)
+    if name == "fold":
+        # wide records (key 4, permits 4, ts 8, arrival index 4) + packed reply 4 per request;
+        # per distinct key: bucket row 16 + queue header 8, read and written; 8 per enqueue
+        alg = n * 24 + u * 48 + q_last * 8
+        note = "n*24 + distinct*48 + enqueued*8 (last batch's enqueues)"
+    elif name == "drain":
+        # every key's queue header 8; per grant: ring entry 8 + log record 20 (lower bound)
+        alg = kl * 8 + d_last * 28
+        note = "n_keys*8 + grants*28 (lower bound: rows of keys with queues not counted)"
+    else:
+        alg = n * 20
+        note = "n*20"
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
+        "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (splitmix64 seeded trace generated in HBM)",
+        "config": {"workload": f"TokenBucketWithQueue OldestFirst, QueueLimit {args.queue_limit}, "
+                               f"2^{n.bit_length() - 1}-request batches + replenish tick (config D)",
+                   "keys_total": keys_total, "keys_per_gpu": kl, "batch_per_gpu": n,
+                   "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
+                   "period_ticks": args.period_ticks, "interval_us": args.interval_us,
+                   "partitioning": f"key-hash x{world}, no data-path collective"},
+        "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
+        "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
+        "roofline": _roofline(name, alg, ms, note),
+        "cpu_baseline": None,
+    }
+    eng.close()
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_queue(args, kl)
+    return line
+
+
+def cpu_queue(args, kl):
+    """oracle/tb_ref.c tbrq_* (serial): the first 2^20 requests of each config-D batch,
+    each followed by that batch's tick, until ~args.cpu_seconds."""
+    from oracle import cref
+    from distributedratelimiting.redis_amd import fill_rate
+
+    ref = cref.CQueueingTokenBucket(kl, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks),
+                                    args.queue_limit, 0)
+    sample = min(args.batch, 1 << 20)
+    done, spent, b = 0, 0.0, 0
+    while spent < args.cpu_seconds and b < 64:
+        k, p, t = cref.gen_batch(SEED_D, kl, b, args.batch, args.interval_us)
+        k, p, t = k[:sample], p[:sample], t[:sample]
+        t0 = time.perf_counter()
+        ref.acquire_batch(k, p, t, b * args.batch)
+        ref.refresh(T0_US + (b + 1) * args.interval_us)
+        spent += time.perf_counter() - t0
+        done += sample
+        b += 1
+    ref.close()
+    return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} requests of each of {b} config-D batches + their ticks "
+                      f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c tbrq_* single thread",
+            "host_cpus": os.cpu_count()}
+
+
+def run_approx(args, lib, dev, world, rank, dist):
+    from distributedratelimiting.redis_amd import ApproximateEngine
+
+    kshared = args.keys or 10_000_000
+    n, steps, warm = args.batch, args.steps, args.warmup
+    total = warm + steps
+    eng = ApproximateEngine(kshared, args.token_limit, args.tokens_per_period, args.period_ticks,
+                            0, 0, device=dev.index, stage_timing=not args.no_stage_timing, max_batch=n)
+    seed = SEED_E + 7919 * rank
+    bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    av = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.empty(kshared, dtype=torch.int32, device=dev)
+    allc = torch.empty(kshared * world, dtype=torch.int32, device=dev) if dist else counts
+    period_us = args.period_ticks // 10
+    stagger = period_us // world
+    torch.cuda.synchronize()
+    refresh_s = [0.0]
+
+    def step(s, timed=False):
+        # everything on the engine's stream; collect synchronises it
+        eng.acquire_batch_device(*bufs[s], st, av, wait=False, id_base=s * n)
+        if timed:   # collect would wait for the batch anyway; this keeps it out of refresh time
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.collect(counts)             # A:430-435
+        if dist:
+            import torch.distributed as td
+            td.all_gather_into_tensor(allc, counts)   # RCCL over xGMI
+            torch.cuda.current_stream(dev).synchronize()   # the sync replay reads allc
+        eng.sync(allc, world, rank, T0_US + (s + 1) * args.interval_us, stagger)
+        if timed:
+            refresh_s[0] += time.perf_counter() - t1
+
+    for s in range(warm):
+        step(s)
+    torch.cuda.synchronize()
+    eng.synchronize()
+    eng.stage_times()
+    if dist:
+        import torch.distributed as td
+        td.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(warm, total):
+        step(s, timed=True)
+    elapsed = _barrier_time(dist, dev, t0)
+    eng.synchronize()
+    stages = eng.stage_times()
+    granted = float((st == 1).float().mean().item())
+
+    value = n * steps * world / elapsed
+    passes = eng.layout()["passes"]
+    launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
+                "unscatter": passes, "hot": 1}
+    name = max(stages, key=stages.get)
+    ms = stages[name] / (steps * launches[name])
+    u = _distinct(n, kshared)
+    if name == "fold":
+        # records (key 4, permits 4, arrival index 4) + reply 4 per request; local-tier row
+        # 16 B read + written per distinct key
+        alg, note = n * 16 + u * 32, "n*16 + distinct*32"
+    else:
+        alg, note = n * 16, "n*16"
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
+        "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (splitmix64 seeded trace generated in HBM)",
+        "config": {"workload": f"ApproximateTokenBucket AcquireCore, {kshared} shared keys, "
+                               f"2^{n.bit_length() - 1}-request batches + one refresh epoch per batch "
+                               f"(config E)",
+                   "keys_shared": kshared, "batch_per_gpu": n, "token_limit": args.token_limit,
+                   "tokens_per_period": args.tokens_per_period, "period_ticks": args.period_ticks,
+                   "interval_us": args.interval_us, "clients": world,
+                   "exchange": "RCCL all-gather of int32 counts" if dist else "none (one client)"},
+        "granted_frac_last_batch": round(granted, 4),
+        "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
+        "refresh_ms_per_step_wall": round(refresh_s[0] / steps * 1e3, 4),
+        "roofline": _roofline(name, alg, ms, note),
+        "cpu_baseline": None,
+    }
+    eng.close()
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_approx(args, kshared)
+    return line
+
+
+def cpu_approx(args, kshared):
+    """The Python restatement (oracle/semantics.py ApproxClient, one client, pure Python):
+    AcquireCore over the first 2^16 requests of each config-E batch plus a refresh of the
+    keys those requests touched, until ~min(args.cpu_seconds, 10) s."""
+    from oracle import cref
+    from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
+
+    c = ApproxClient(args.token_limit, args.tokens_per_period, args.period_ticks, 0, 0)
+    table = ApproxGlobalTable(c.decay_rate)
+    sample = min(args.batch, 1 << 16)
+    done, spent, b = 0, 0.0, 0
+    budget = min(args.cpu_seconds, 10.0)
+    while spent < budget and b < 64:
+        k, p, _ = cref.gen_batch(SEED_E, kshared, b, args.batch, args.interval_us)
+        k, p = k[:sample].tolist(), p[:sample].tolist()
+        t0 = time.perf_counter()
+        for key, pm in zip(k, p):
+            c.acquire(key, pm)
+        approx_refresh_all([c], table, T0_US + (b + 1) * args.interval_us, 0, sorted(set(k)))
+        spent += time.perf_counter() - t0
+        done += sample
+        b += 1
+    return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} requests of each of {b} config-E batches + a refresh of their "
+                      f"keys ({done} decisions, {spent:.1f} s), oracle/semantics.py pure Python",
+            "host_cpus": os.cpu_count()}

@@ -29,7 +29,8 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_acquire_batch_device", "tbe_synchronize", "tbe_query", "tbe_export_state",
             "tbe_wait_batch", "tbe_queue_attempt_batch", "tbe_evicted", "tbe_refresh", "tbe_refresh_log", "tbe_queue_of",
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
-            "tbe_approx_query", "tbe_layout", "tbe_stage_times")
+            "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
+            "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -117,6 +118,17 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_approx_query.restype = c_int32
     lib.tbe_approx_query.argtypes = [c_void_p, c_uint64, POINTER(c_int32), POINTER(c_int32),
                                      POINTER(c_double), POINTER(c_int32), POINTER(c_uint32)]
+    lib.tbe_wait_batch_device.restype = c_int32
+    lib.tbe_wait_batch_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_int64,
+                                          c_int32, c_void_p, c_void_p, c_void_p]
+    lib.tbe_refresh_bound.restype = c_int32
+    lib.tbe_refresh_bound.argtypes = [c_void_p, POINTER(c_uint64)]
+    lib.tbe_refresh_device.restype = c_int32
+    lib.tbe_refresh_device.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
+                                       c_void_p, c_void_p]
+    lib.tbe_approx_acquire_batch_device.restype = c_int32
+    lib.tbe_approx_acquire_batch_device.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int32,
+                                                    c_int64, c_void_p, c_void_p, c_void_p]
     lib.tbe_layout.restype = c_int32
     lib.tbe_layout.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     lib.tbe_stage_times.restype = c_int32

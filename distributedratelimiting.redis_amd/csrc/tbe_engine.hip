@@ -1749,6 +1749,26 @@ __global__ void k_sticky(const uint32_t *__restrict__ err, uint32_t *__restrict_
     if (threadIdx.x == 0 && *err) *sticky = 1u;
 }
 
+// Entries in all queues: qhdr count bits (queueing kind) or ALocal.hc count bits
+// (approximate kind).  Re-establishes the host's count after device-pointer batches.
+__global__ __launch_bounds__(kBlock) void k_count_queued(uint64_t n_keys, const uint64_t *__restrict__ qhdr,
+                                                        const ALocal *__restrict__ alocal,
+                                                        unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long part[kBlock / 64];
+    unsigned long long c = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride)
+        c += qhdr ? ((qhdr[k] >> 16) & 0xFFFFu) : ((alocal[k].hc >> 16) & 0xFFFFu);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+        if (t) atomicAdd(out, t);
+    }
+}
+
 // ----------------------------------------------------------------------------- host side
 enum Stage { ST_HIST = 0, ST_COLSCAN, ST_SCATTER, ST_BOUNDS, ST_FOLD, ST_UNSCATTER, ST_HOT, ST_COUNT };
 
@@ -1814,6 +1834,12 @@ struct tbe_engine {
     uint64_t *qhdr = nullptr;      // per-key queue header
     uint64_t *ring = nullptr;      // per-key rings of qp.cap entries
     uint64_t queued_total = 0;     // entries in all queues (host-side count)
+    // After a device-pointer wait batch or drain the host cannot see how many entries
+    // were queued or drained: queued_total is then an upper bound (queued_exact false)
+    // until a host-buffer call recounts the queues on the device (sync_queued).
+    bool queued_exact = true;
+    bool ev_pending = false;       // the eviction log of a device wait batch is unread
+    unsigned long long *qcount = nullptr;
     uint32_t *ev_cause = nullptr;  // eviction log of the last wait batch
     int64_t *ev_id = nullptr;
     uint64_t ev_cap = 0;
@@ -2375,6 +2401,7 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->qhdr);
     dfree(e->ring);
     dfree(e->counters);
+    dfree(e->qcount);
     dfree(e->ev_cause);
     dfree(e->ev_id);
     dfree(e->log_keyseq);
@@ -2487,6 +2514,72 @@ tbe_status tbe_export_state(tbe_engine *e, uint64_t first, uint64_t count, doubl
     return TBE_OK;
 }
 
+// Ring entries of all keys: the most any sequence of batches can leave queued.
+static uint64_t ring_entries(const tbe_engine *e) {
+    const uint32_t cap = e->cfg.kind == TBE_KIND_APPROXIMATE ? e->ap.cap : e->qp.cap;
+    return e->cfg.n_keys * (uint64_t)cap;
+}
+
+// Host-buffer calls size their logs from queued_total; after device-pointer batches it is
+// only an upper bound, so count the queues on the device once (all streams drained first:
+// device batches may have run on caller streams).
+static tbe_status sync_queued(tbe_engine *e) {
+    if (e->queued_exact) return TBE_OK;
+    HIP_TRY(e, hipDeviceSynchronize());
+    if (!e->qcount) HIP_TRY(e, hipMalloc(&e->qcount, sizeof(unsigned long long)));
+    hipStream_t st = e->stream;
+    HIP_TRY(e, hipMemsetAsync(e->qcount, 0, sizeof(unsigned long long), st));
+    const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+    k_count_queued<<<(unsigned)blocks, kBlock, 0, st>>>(
+        e->cfg.n_keys, e->cfg.kind == TBE_KIND_QUEUEING ? e->qhdr : nullptr, e->alocal, e->qcount);
+    HIP_TRY(e, hipGetLastError());
+    unsigned long long q = 0;
+    HIP_TRY(e, hipMemcpyAsync(&q, e->qcount, sizeof q, hipMemcpyDeviceToHost, st));
+    HIP_TRY(e, hipStreamSynchronize(st));
+    e->queued_total = q;
+    e->queued_exact = true;
+    return TBE_OK;
+}
+
+// Device-pointer variant of status_batch: the whole batch stays in HBM, nothing is
+// synchronised.  Evictions (NewestFirst waits only) go to the engine's eviction log, read
+// lazily by tbe_evicted; its capacity n + queued_total bounds them (every eviction
+// removes an entry queued before the batch or by it).
+static tbe_status status_batch_device(tbe_engine *e, const uint64_t *d_keys, const int32_t *d_permits,
+                                      const int64_t *d_ts, uint64_t n, int64_t id_base,
+                                      uint8_t *d_status, int32_t *d_remaining, void *stream) {
+    e->evicted.clear();
+    e->ev_pending = false;
+    if (n == 0) return TBE_OK;
+    if (!d_keys || !d_permits || !d_status || !d_remaining) return fail(e, TBE_EINVAL, "null buffer");
+    if (id_base < 0 || (uint64_t)id_base + n > (1ull << 47))
+        return fail(e, TBE_EINVAL, "request ids must lie in [0, 2^47)");
+    HIP_TRY(e, hipSetDevice(e->device));
+    const int32_t order = e->cfg.kind == TBE_KIND_APPROXIMATE ? e->ap.order : e->qp.order;
+    const bool may_evict = e->wait_mode == 1 && order == 1;
+    if (may_evict) {
+        const uint64_t need_ev = e->queued_total + n;
+        if (need_ev > e->ev_cap) {
+            dfree(e->ev_cause);
+            dfree(e->ev_id);
+            e->ev_cap = 0;
+            HIP_TRY(e, hipMalloc(&e->ev_cause, need_ev * sizeof(uint32_t)));
+            HIP_TRY(e, hipMalloc(&e->ev_id, need_ev * sizeof(int64_t)));
+            e->ev_cap = need_ev;
+        }
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), st));
+    tbe_status rc = run_batch(e, d_keys, d_permits, d_ts, n, d_status, d_remaining, st, id_base);
+    if (rc != TBE_OK) return rc;
+    e->ev_pending = may_evict;
+    if (e->wait_mode == 1) {
+        e->queued_total = std::min<uint64_t>(e->queued_total + n, ring_entries(e));
+        e->queued_exact = false;
+    }
+    return TBE_OK;
+}
+
 static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                                const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                                int32_t *remaining, uint64_t *n_evicted);
@@ -2521,13 +2614,37 @@ tbe_status tbe_approx_acquire_batch(tbe_engine *e, const uint64_t *keys, const i
     return status_batch(e, keys, permits, nullptr, n, id_base, status, available, n_evicted);
 }
 
+tbe_status tbe_wait_batch_device(tbe_engine *e, const uint64_t *d_keys, const int32_t *d_permits,
+                                 const int64_t *d_ts_us, uint64_t n, int64_t id_base, int32_t wait,
+                                 uint8_t *d_status, int32_t *d_remaining, void *stream) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (n && !d_ts_us) return fail(e, TBE_EINVAL, "null buffer");
+    e->wait_mode = wait ? 1 : 0;
+    return status_batch_device(e, d_keys, d_permits, d_ts_us, n, id_base, d_status, d_remaining, stream);
+}
+
+tbe_status tbe_approx_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys, const int32_t *d_permits,
+                                           uint64_t n, int32_t wait, int64_t id_base, uint8_t *d_status,
+                                           int32_t *d_available, void *stream) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    e->wait_mode = wait ? 1 : 0;
+    return status_batch_device(e, d_keys, d_permits, nullptr, n, id_base, d_status, d_available, stream);
+}
+
 static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                                const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                                int32_t *remaining, uint64_t *n_evicted) {
     *n_evicted = 0;
     e->evicted.clear();
+    e->ev_pending = false;
     if (n == 0) return TBE_OK;
     if (!keys || !permits || !status || !remaining) return fail(e, TBE_EINVAL, "null buffer");
+    {
+        tbe_status qrc = sync_queued(e);
+        if (qrc != TBE_OK) return qrc;
+    }
     if (id_base < 0 || (uint64_t)id_base + n > (1ull << 47))
         return fail(e, TBE_EINVAL, "request ids must lie in [0, 2^47)");
     HIP_TRY(e, hipSetDevice(e->device));
@@ -2582,6 +2699,23 @@ static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_
 tbe_status tbe_evicted(tbe_engine *e, uint64_t *cause_index, int64_t *request_id, uint64_t capacity,
                        uint64_t *n_written) {
     if (!e || !n_written) return TBE_EINVAL;
+    if (e->ev_pending) {   // the last batch was a device-pointer wait batch
+        HIP_TRY(e, hipSetDevice(e->device));
+        HIP_TRY(e, hipDeviceSynchronize());
+        uint32_t nev = 0;
+        HIP_TRY(e, hipMemcpy(&nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (nev > e->ev_cap) return fail(e, TBE_EDEVICE, "eviction log overflow");
+        std::vector<uint32_t> cause(nev);
+        std::vector<int64_t> id(nev);
+        if (nev) {
+            HIP_TRY(e, hipMemcpy(cause.data(), e->ev_cause, nev * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            HIP_TRY(e, hipMemcpy(id.data(), e->ev_id, nev * sizeof(int64_t), hipMemcpyDeviceToHost));
+        }
+        e->evicted.resize(nev);
+        for (uint32_t i = 0; i < nev; ++i) e->evicted[i] = {cause[i], id[i]};
+        std::sort(e->evicted.begin(), e->evicted.end());
+        e->ev_pending = false;
+    }
     const uint64_t m = std::min<uint64_t>(capacity, e->evicted.size());
     if (m && (!cause_index || !request_id)) return fail(e, TBE_EINVAL, "null buffer");
     for (uint64_t i = 0; i < m; ++i) {
@@ -2598,8 +2732,12 @@ tbe_status tbe_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
     if (ts_us < 0) return fail(e, TBE_EINVAL, "ts_us < 0");
     *n_granted = 0;
     e->drained.clear();
-    if (e->queued_total == 0) return TBE_OK;
     HIP_TRY(e, hipSetDevice(e->device));
+    {
+        tbe_status qrc = sync_queued(e);
+        if (qrc != TBE_OK) return qrc;
+    }
+    if (e->queued_total == 0) return TBE_OK;
     if (e->queued_total > e->log_cap) {
         dfree(e->log_keyseq);
         dfree(e->log_id);
@@ -2640,6 +2778,42 @@ tbe_status tbe_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
     return TBE_OK;
 }
 
+tbe_status tbe_refresh_bound(tbe_engine *e, uint64_t *bound) {
+    if (!e || !bound) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    // every drained entry holds >= 1 permit (zero-permit requests are never queued) and a
+    // tick grants at most TokenLimit tokens per key
+    const uint64_t per_key = std::min<uint64_t>(e->qp.cap, (uint64_t)std::max(e->qp.token_limit, 1));
+    *bound = std::min<uint64_t>(e->queued_total, e->cfg.n_keys * per_key);
+    return TBE_OK;
+}
+
+tbe_status tbe_refresh_device(tbe_engine *e, int64_t ts_us, uint64_t *d_keyseq, int64_t *d_request_id,
+                              int32_t *d_remaining, uint64_t capacity, uint32_t *d_count, void *stream) {
+    if (!e || !d_count) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (ts_us < 0) return fail(e, TBE_EINVAL, "ts_us < 0");
+    uint64_t bound = 0;
+    tbe_status rc = tbe_refresh_bound(e, &bound);
+    if (rc != TBE_OK) return rc;
+    if (capacity < bound || bound > 0xFFFFFFFFull)
+        return fail(e, TBE_EINVAL, "drain log capacity %llu below the bound %llu (tbe_refresh_bound)",
+                    (unsigned long long)capacity, (unsigned long long)bound);
+    if (bound && (!d_keyseq || !d_request_id || !d_remaining)) return fail(e, TBE_EINVAL, "null buffer");
+    HIP_TRY(e, hipSetDevice(e->device));
+    e->drained.clear();
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    HIP_TRY(e, hipMemsetAsync(d_count, 0, sizeof(uint32_t), st));
+    if (bound == 0) return TBE_OK;   // nothing queued
+    const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+    k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params,
+                                                e->qp, ts_us, d_keyseq, d_request_id, d_remaining, d_count,
+                                                (uint32_t)std::min<uint64_t>(capacity, 0xFFFFFFFFu));
+    HIP_TRY(e, hipGetLastError());
+    e->queued_exact = false;   // queued_total stays an upper bound
+    return TBE_OK;
+}
+
 tbe_status tbe_approx_collect(tbe_engine *e, int32_t *d_counts, void *stream) {
     if (!e || !d_counts) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
@@ -2661,6 +2835,10 @@ tbe_status tbe_approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t 
     *n_granted = 0;
     e->drained.clear();
     HIP_TRY(e, hipSetDevice(e->device));
+    {
+        tbe_status qrc = sync_queued(e);
+        if (qrc != TBE_OK) return qrc;
+    }
     const uint64_t need = std::max<uint64_t>(e->queued_total, 1);
     if (need > e->log_cap) {
         dfree(e->log_keyseq);

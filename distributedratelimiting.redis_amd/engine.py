@@ -180,6 +180,43 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
                                                       remaining.ctypes.data))
         return status, remaining
 
+    def wait_batch_device(self, d_keys, d_permits, d_ts, d_status, d_remaining, id_base: int,
+                          wait: bool = True, stream: Optional[int] = None) -> None:
+        """Device tensors in and out; enqueued, not synchronised (tbe_wait_batch_device).
+        NewestFirst evictions: ``evicted()`` after the call."""
+        n = d_keys.numel()
+        self._check(self._lib.tbe_wait_batch_device(
+            self.handle, d_keys.data_ptr(), d_permits.data_ptr(), d_ts.data_ptr(), n, id_base,
+            1 if wait else 0, d_status.data_ptr(), d_remaining.data_ptr(), stream))
+
+    def evicted(self):
+        """(cause index u64, request id i64) of the last wait batch, sorted (tbe_evicted)."""
+        nw = ctypes.c_uint64()
+        self._check(self._lib.tbe_evicted(self.handle, None, None, 0, byref(nw)))
+        # capacity 0 fetched the log; a second call copies it out
+        cap = 1 << 20
+        while True:
+            cause = np.empty(cap, dtype=np.uint64)
+            ids = np.empty(cap, dtype=np.int64)
+            self._check(self._lib.tbe_evicted(self.handle, cause.ctypes.data, ids.ctypes.data, cap,
+                                              byref(nw)))
+            if nw.value < cap:
+                return cause[: nw.value], ids[: nw.value]
+            cap *= 4
+
+    def refresh_bound(self) -> int:
+        b = ctypes.c_uint64()
+        self._check(self._lib.tbe_refresh_bound(self.handle, byref(b)))
+        return b.value
+
+    def refresh_device(self, ts_us: int, d_keyseq, d_ids, d_rem, d_count,
+                       stream: Optional[int] = None) -> None:
+        """Enqueue one replenish tick; the drain log lands in the device tensors
+        (capacity = d_keyseq.numel(), which must be >= refresh_bound())."""
+        self._check(self._lib.tbe_refresh_device(self.handle, ts_us, d_keyseq.data_ptr(), d_ids.data_ptr(),
+                                                 d_rem.data_ptr(), d_keyseq.numel(), d_count.data_ptr(),
+                                                 stream))
+
     def refresh(self, ts_us: int):
         """One replenish tick; returns (keys u64, request ids i64, remaining i32) in (key, drain) order."""
         n = ctypes.c_uint64()
@@ -232,6 +269,14 @@ class ApproximateEngine(QueueingTokenBucketEngine):
         if m:
             self._check(self._lib.tbe_evicted(self.handle, cause.ctypes.data, ids.ctypes.data, m, byref(nw)))
         return status, avail, (cause, ids)
+
+    def acquire_batch_device(self, d_keys, d_permits, d_status, d_available, wait: bool = False,
+                             id_base: int = 0, stream: Optional[int] = None) -> None:
+        """Device tensors in and out; enqueued (tbe_approx_acquire_batch_device)."""
+        n = d_keys.numel()
+        self._check(self._lib.tbe_approx_acquire_batch_device(
+            self.handle, d_keys.data_ptr(), d_permits.data_ptr(), n, 1 if wait else 0, id_base,
+            d_status.data_ptr(), d_available.data_ptr(), stream))
 
     def collect(self, d_counts) -> None:
         """Local scores of every key into the int32 device tensor `d_counts` [n_keys]."""

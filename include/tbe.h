@@ -176,6 +176,29 @@ tbe_status tbe_refresh(tbe_engine *engine, int64_t ts_us, uint64_t *n_granted);
 tbe_status tbe_refresh_log(tbe_engine *engine, uint64_t *keys, int64_t *request_id,
                            int32_t *remaining, uint64_t capacity, uint64_t *n_written);
 
+/* Device-pointer tbe_wait_batch (wait = 1, Q:67-134) / tbe_queue_attempt_batch (wait = 0,
+ * Q:136-165): every buffer is device memory on the engine's GPU, the call only enqueues
+ * (stream semantics as tbe_acquire_batch_device) and the replies equal the host-buffer
+ * call's.  NewestFirst evictions are fetched with tbe_evicted (which then synchronises).
+ * Invalid requests skip the batch and surface at tbe_synchronize. */
+tbe_status tbe_wait_batch_device(tbe_engine *engine, const uint64_t *d_keys, const int32_t *d_permits,
+                                 const int64_t *d_ts_us, uint64_t n, int64_t id_base, int32_t wait,
+                                 uint8_t *d_status, int32_t *d_remaining, void *stream);
+
+/* Upper bound on the grants one tbe_refresh_device can log: min(entries possibly queued,
+ * n_keys * min(max(1, QueueLimit), TokenLimit)) -- a queued entry holds >= 1 permit and
+ * a tick grants at most TokenLimit tokens per key. */
+tbe_status tbe_refresh_bound(tbe_engine *engine, uint64_t *bound);
+
+/* Device-pointer tbe_refresh (Q:237-271): enqueues one replenish tick at ts_us.  Grants
+ * land in the caller's device buffers as (key << 16 | drain position, request id,
+ * trunc(new_v)), grouped arbitrarily across keys, and *d_count (device u32) receives
+ * their number.  capacity must be >= tbe_refresh_bound (TBE_EINVAL otherwise), so no
+ * grant is ever dropped. */
+tbe_status tbe_refresh_device(tbe_engine *engine, int64_t ts_us, uint64_t *d_keyseq,
+                              int64_t *d_request_id, int32_t *d_remaining, uint64_t capacity,
+                              uint32_t *d_count, void *stream);
+
 /* Queue of one key, oldest first (Deque enumeration order, DQ:116-125). */
 tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, int32_t *permits,
                         uint32_t capacity, uint32_t *count);
@@ -192,6 +215,13 @@ tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, i
 tbe_status tbe_approx_acquire_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
                                     uint64_t n, int32_t wait, int64_t id_base, uint8_t *status,
                                     int32_t *available, uint64_t *n_evicted);
+
+/* Device-pointer tbe_approx_acquire_batch (A:84-183): device buffers, enqueue only
+ * (stream semantics as tbe_acquire_batch_device); evictions via tbe_evicted. */
+tbe_status tbe_approx_acquire_batch_device(tbe_engine *engine, const uint64_t *d_keys,
+                                           const int32_t *d_permits, uint64_t n, int32_t wait,
+                                           int64_t id_base, uint8_t *d_status, int32_t *d_available,
+                                           void *stream);
 
 /* Refresh step 1 (A:430-435): d_counts[k] = _localThrottleScore of key k, then 0.
  * d_counts is device memory for n_keys int32 (the caller exchanges it between clients,

@@ -1,0 +1,165 @@
+"""GPU parity of the device-pointer queue and approximate entry points
+(tbe_wait_batch_device, tbe_refresh_device, tbe_approx_acquire_batch_device): the same
+traces as tests/test_gpu_queue.py / test_gpu_approx.py, inputs and replies in HBM, checked
+against the C restatement (oracle/tb_ref.c) and the Python restatement (oracle/semantics.py),
+including host-buffer calls made after device calls (the engine recounts its queues)."""
+import numpy as np
+import pytest
+
+from oracle import cref
+
+pytestmark = pytest.mark.gpu
+
+S_US = 1_760_572_800 * 1_000_000
+
+
+def _dev(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _sorted_log(keyseq, ids, rem, count):
+    """Device drain log -> the host call's (key, drain order) listing."""
+    m = int(count.item())
+    ks = keyseq[:m].cpu().numpy().view(np.uint64)
+    o = np.argsort(ks, kind="stable")
+    return (ks[o] >> np.uint64(16)), ids[:m].cpu().numpy()[o], rem[:m].cpu().numpy()[o]
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("n_keys,qlimit,n,rounds", [(40, 4, 3000, 5), (5000, 16, 60000, 4), (7, 0, 2000, 3)])
+def test_wait_and_refresh_device(engine_lib, gpu, order, n_keys, qlimit, n, rounds):
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    rng = np.random.default_rng(n_keys + 31 * qlimit + order + 7)
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, qlimit, order, device=0)
+    ref = cref.CQueueingTokenBucket(n_keys, 4, fill_rate(1, 10_000_000), qlimit, order)
+    t, rid = S_US, 0
+    for rnd in range(rounds):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 1, 2, 3, 5], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, rid)
+        d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+        d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
+        eng.wait_batch_device(_dev(keys.view(np.int64), gpu), _dev(permits, gpu), _dev(ts, gpu),
+                              d_st, d_rem, rid)
+        eng.synchronize()
+        assert np.array_equal(d_st.cpu().numpy(), st2)
+        assert np.array_equal(d_rem.cpu().numpy(), rem2)
+        cause, ids = eng.evicted()
+        assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2)
+        rid += n
+        t += 1_000 + int(rng.integers(0, 3_000_000))
+        k2, i2, r2 = ref.refresh(t)
+        if rnd % 2 == 0:   # device drain
+            cap = max(eng.refresh_bound(), 1)
+            lk = torch.empty(cap, dtype=torch.int64, device=gpu)
+            li = torch.empty(cap, dtype=torch.int64, device=gpu)
+            lr = torch.empty(cap, dtype=torch.int32, device=gpu)
+            cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+            eng.refresh_device(t, lk, li, lr, cnt)
+            eng.synchronize()
+            k1, i1, r1 = _sorted_log(lk, li, lr, cnt)
+        else:              # host drain after device batches: the engine recounts its queues
+            k1, i1, r1 = eng.refresh(t)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    for k in range(min(n_keys, 50)):
+        assert eng.queue_of(k) == ref.queue_of(k)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+def test_refresh_device_capacity_checked(engine_lib, gpu):
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, TbeError
+    eng = QueueingTokenBucketEngine(100, 2, 1, 10_000_000, 8, 0, device=0)
+    n = 5000
+    keys = np.arange(n, dtype=np.int64) % 100
+    d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+    d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
+    eng.wait_batch_device(_dev(keys, gpu), torch.ones(n, dtype=torch.int32, device=gpu),
+                          torch.full((n,), S_US, dtype=torch.int64, device=gpu), d_st, d_rem, 0)
+    eng.synchronize()
+    assert eng.refresh_bound() == 100 * 2   # n_keys * min(QueueLimit, TokenLimit)
+    small = torch.empty(10, dtype=torch.int64, device=gpu)
+    with pytest.raises(TbeError):
+        eng.refresh_device(S_US + 1, small, small, small.view(torch.int32)[:10],
+                           torch.zeros(1, dtype=torch.int32, device=gpu))
+
+
+def test_config_d_shape_device(engine_lib, gpu):
+    """Config D shape (QueueLimit 16, OldestFirst, TokenLimit 4, 1 ms batches, refresh at
+    each batch boundary) through the device entry points, as bench.py --workload queue."""
+    import torch
+    from oracle import trace
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    n_keys, n = 1_000_000, 1 << 20
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, 16, 0, device=0)
+    ref = cref.CQueueingTokenBucket(n_keys, 4, fill_rate(1, 10_000_000), 16, 0)
+    cap = n_keys * 4
+    lk = torch.empty(cap, dtype=torch.int64, device=gpu)
+    li = torch.empty(cap, dtype=torch.int64, device=gpu)
+    lr = torch.empty(cap, dtype=torch.int32, device=gpu)
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+    d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
+    for b in range(4):
+        k, p, ts = trace.make_batch(0x5EED000D, n_keys, b, n, 1_000)
+        st2, rem2, _, _ = ref.acquire_batch(k, p, ts, b * n)
+        eng.wait_batch_device(_dev(k.view(np.int64), gpu), _dev(p, gpu), _dev(ts, gpu), d_st, d_rem, b * n)
+        t_ref = trace.T0_US + (b + 1) * 1_000
+        eng.refresh_device(t_ref, lk, li, lr, cnt)
+        eng.synchronize()
+        assert np.array_equal(d_st.cpu().numpy(), st2) and np.array_equal(d_rem.cpu().numpy(), rem2)
+        k1, i1, r1 = _sorted_log(lk, li, lr, cnt)
+        k2, i2, r2 = ref.refresh(t_ref)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    assert (st2 == 2).mean() > 0.05
+
+
+@pytest.mark.parametrize("order,qlimit,wait", [(0, 8, True), (1, 4, True), (0, 0, False)])
+def test_approx_acquire_device(engine_lib, gpu, order, qlimit, wait):
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
+    n_keys, n, limit, tokens, ticks = 300, 4000, 20, 10, 10_000_000
+    rng = np.random.default_rng(order * 10 + qlimit + 5)
+    eng = ApproximateEngine(n_keys, limit, tokens, ticks, qlimit, order, device=0)
+    client = ApproxClient(limit, tokens, ticks, qlimit, order)
+    table = ApproxGlobalTable(client.decay_rate)
+    counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+    d_av = torch.empty(n, dtype=torch.int32, device=gpu)
+    rid = 0
+    for epoch in range(5):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 2, 3, 25], n).astype(np.int32)
+        eng.acquire_batch_device(_dev(keys.view(np.int64), gpu), _dev(permits, gpu), d_st, d_av,
+                                 wait=wait, id_base=rid)
+        eng.synchronize()
+        exp, exp_ev = [], []
+        for i, (k, p) in enumerate(zip(keys.tolist(), permits.tolist())):
+            if wait:
+                status, ev = client.wait(k, p, rid + i)
+            else:
+                status, ev = client.acquire(k, p), []
+            exp.append((status, -1 if status == 3 else client.available(client.st(k))))
+            exp_ev += [(i, x) for x in ev]
+        assert d_st.cpu().tolist() == [x[0] for x in exp]
+        assert d_av.cpu().tolist() == [x[1] for x in exp]
+        cause, ids = eng.evicted()
+        assert list(zip(cause.tolist(), ids.tolist())) == exp_ev
+        rid += n
+        ts = S_US + epoch * 1_000_000
+        eng.collect(counts)
+        k, i, _ = eng.sync(counts, 1, 0, ts, 0)   # host sync after device batches: recount
+        exp_log = approx_refresh_all([client], table, ts, 0, range(n_keys))[0]
+        assert list(zip(k.tolist(), i.tolist())) == exp_log
+        for key in range(0, n_keys, 11):
+            lo, gl, est, av, q = eng.local_state(key)
+            s = client.st(key)
+            assert (lo, gl, est, av, q) == (s.local, s.global_, s.est, client.available(s), len(s.queue))
