@@ -45,6 +45,8 @@ def _distinct(n: int, k: int) -> float:
 
 
 def _roofline(name, alg_bytes, ms, note):
+    if not ms > 0:    # --no-stage-timing: no kernel times
+        return None
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

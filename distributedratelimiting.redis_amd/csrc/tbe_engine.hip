@@ -1234,12 +1234,15 @@ __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t
     return (uint64_t)(head & 0xFFFFu) | ((uint64_t)(cnt & 0xFFFFu) << 16) | ((uint64_t)qsum << 32);
 }
 
+constexpr int kQBlock = 512;                       // k_fold_q workgroup (4 waves/SIMD at 2 per CU)
+constexpr int kQItems = 4;
+constexpr int kQChunk = kQBlock * kQItems;         // 2048 requests per chunk
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
 // the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
 // LDS and its ring in HBM.  A ring entry written in one round and read (evicted) in a
 // later round of the same workgroup is ordered by the round's __syncthreads
 // (workgroup-scope fence; one CU, one vector L1).
-__global__ __launch_bounds__(kBlock) void k_fold_q(
+__global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint32_t *__restrict__ sidx,
     const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
@@ -1264,21 +1267,34 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
     Slot *__restrict__ rows = table + row0;
     uint64_t *__restrict__ hrows = qhdr + row0;
 
-    for (uint32_t j = tid; j < R; j += kBlock) own[j] = kNoOwner;
-    for (uint32_t j = tid; j < (R + 31) / 32; j += kBlock) {
-        loaded[j] = 0;
+    // A dense bucket (>= R/8 requests: nearly every 128-byte line of its slice is touched)
+    // pulls its whole slice of rows and queue headers with coalesced loads and writes it
+    // back whole; a sparse one gathers and writes back only the rows it touches.
+    const bool dense = (e - s) >= (R >> 3);
+    if (dense) {
+        for (uint32_t j = tid; j < R; j += kQBlock) {
+            const uint32_t jj = j < nrows ? j : nrows - 1;
+            const Slot t = rows[jj];
+            const uint64_t h = hrows[jj];
+            slot[j] = t;
+            qh[j] = h;
+        }
+    }
+    for (uint32_t j = tid; j < R; j += kQBlock) own[j] = kNoOwner;
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kQBlock) {
+        loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
     __syncthreads();
 
-    for (uint32_t c = s; c < e; c += kChunk) {
-        uint32_t kl[kFoldItems], ai[kFoldItems];
-        int32_t pm[kFoldItems];
-        int64_t ts[kFoldItems];
+    for (uint32_t c = s; c < e; c += kQChunk) {
+        uint32_t kl[kQItems], ai[kQItems];
+        int32_t pm[kQItems];
+        int64_t ts[kQItems];
         uint32_t pend = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldItems; ++r) {
-            const uint32_t q = c + r * kBlock + tid;
+        for (int r = 0; r < kQItems; ++r) {
+            const uint32_t q = c + r * kQBlock + tid;
             if (q < e) {
                 kl[r] = skeys[q] & rmask;
                 pm[r] = sperm[q];
@@ -1291,7 +1307,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
         }
         uint32_t mine = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldItems; ++r) {
+        for (int r = 0; r < kQItems; ++r) {
             if (pend & (1u << r)) {
                 const uint32_t bit = 1u << (kl[r] & 31);
                 const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
@@ -1299,28 +1315,28 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
             }
         }
         {
-            Slot tmp[kFoldItems];
-            uint64_t th[kFoldItems];
+            Slot tmp[kQItems];
+            uint64_t th[kQItems];
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r) {
+            for (int r = 0; r < kQItems; ++r) {
                 tmp[r] = Slot{0.0, 0};
                 th[r] = 0;
                 if (mine & (1u << r)) { tmp[r] = rows[kl[r]]; th[r] = hrows[kl[r]]; }
             }
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
+            for (int r = 0; r < kQItems; ++r)
                 if (mine & (1u << r)) { slot[kl[r]] = tmp[r]; qh[kl[r]] = th[r]; }
         }
         __syncthreads();
         for (;;) {
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
-                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kBlock + tid));
+            for (int r = 0; r < kQItems; ++r)
+                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kQBlock + tid));
             __syncthreads();
             uint32_t won = 0;
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r) {
-                if (!((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kBlock + tid))) continue;
+            for (int r = 0; r < kQItems; ++r) {
+                if (!((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kQBlock + tid))) continue;
                 won |= 1u << r;
                 Slot st = slot[kl[r]];
                 const uint64_t h0 = qh[kl[r]];
@@ -1378,22 +1394,22 @@ __global__ __launch_bounds__(kBlock) void k_fold_q(
                         }
                     }
                 }
-                res[c + r * kBlock + tid] = pack_wait(status, evaluated, rem);
+                res[c + r * kQBlock + tid] = pack_wait(status, evaluated, rem);
                 if (smod) slot[kl[r]] = st;
                 if (hmod) qh[kl[r]] = qh_pack(head, cnt, qsum);
                 if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
             __syncthreads();
 #pragma unroll
-            for (int r = 0; r < kFoldItems; ++r)
+            for (int r = 0; r < kQItems; ++r)
                 if (won & (1u << r)) own[kl[r]] = kNoOwner;
             pend &= ~won;
             if (!__syncthreads_or(pend != 0)) break;
         }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < nrows; j += kBlock)
-        if (dirty[j >> 5] & (1u << (j & 31))) {
+    for (uint32_t j = tid; j < nrows; j += kQBlock)
+        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) {
             rows[j] = slot[j];
             hrows[j] = qh[j];
         }
@@ -1419,6 +1435,18 @@ __global__ __launch_bounds__(kBlock) void k_drain(
         uint32_t seq = 0;
         const uint64_t *__restrict__ kr = ring + key * (uint64_t)Q.cap;
         while (cnt > 0) {
+            // Every queued entry holds >= 1 permit, so when one permit is denied the entry
+            // is too, with the same state change (a denial only ever deletes a lapsed
+            // key, whatever the permits): decide that case without reading the ring.
+            {
+                Slot probe = st;
+                bool pm;
+                if (!(tb_acquire(probe, 1, ts_us, P, pm) >> 31)) {
+                    st = probe;
+                    smod |= pm;
+                    break;
+                }
+            }
             uint32_t idx = head;
             if (Q.order == 1) {
                 idx = head + cnt - 1;
@@ -2165,7 +2193,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         QParams q = e->qp;
         q.id_base = id_base;
         q.wait = e->wait_mode;
-        k_fold_q<<<e->nbuckets, kBlock, 0, sf>>>(
+        k_fold_q<<<e->nbuckets, kQBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
             e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
