@@ -44,12 +44,36 @@ def _distinct(n: int, k: int) -> float:
     return k * (1.0 - np.exp(-n / k))
 
 
-def _roofline(name, alg_bytes, ms, note):
+def _pmc_traffic(workload, kernels):
+    """HBM bytes per launch of the named kernels (mean over them) in `workload`'s runs,
+    from the committed PMC summary (tools/pmc_summary.py --write), or None."""
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f).get("workloads", {}).get(workload, {})
+    except (OSError, ValueError):
+        return None
+    v = [d[k]["hbm_bytes_per_launch"] for k in kernels if "hbm_bytes_per_launch" in d.get(k, {})]
+    return round(sum(v) / len(v), 1) if len(v) == len(kernels) and v else None
+
+
+PMC_KERNELS = {
+    ("queue", "fold"): ["k_fold_q"],
+    ("queue", "drain"): ["k_drain"],
+    ("queue", "scatter"): ["k_scatter<unsigned long, true, true>", "k_scatter<unsigned int, true, true>"],
+    ("approx", "fold"): ["k_fold_a"],
+    ("approx", "scatter"): ["k_scatter<unsigned long, true, false>", "k_scatter<unsigned int, true, false>"],
+}
+
+
+def _roofline(name, alg_bytes, ms, note, workload=None):
     if not ms > 0:    # --no-stage-timing: no kernel times
         return None
     achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic = _pmc_traffic(workload, PMC_KERNELS[(workload, name)]) if (workload, name) in PMC_KERNELS else None
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4),
             "alg_bytes_note": note,
             "timing": "HIP events on the engine's launch stream over the timed region"}
@@ -152,6 +176,10 @@ def run_queue(args, lib, dev, world, rank, dist):
         # every key's queue header 8; per grant: ring entry 8 + log record 20 (lower bound)
         alg = kl * 8 + d_last * 28
         note = "n_keys*8 + grants*28 (lower bound: rows of keys with queues not counted)"
+    elif name == "scatter":
+        # per pass: read the caller's key 8 + permits 4 + ts 8 (pass 0) or one wide record
+        # 20; write the wide record {key 4, permits 4, ts 8, index 4} and perm 4
+        alg, note = n * 44, "n*44 (wide records, per pass)"
     else:
         alg = n * 20
         note = "n*20"
@@ -168,7 +196,7 @@ def run_queue(args, lib, dev, world, rank, dist):
                    "partitioning": f"key-hash x{world}, no data-path collective"},
         "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
-        "roofline": _roofline(name, alg, ms, note),
+        "roofline": _roofline(name, alg, ms, note, "queue"),
         "cpu_baseline": None,
     }
     eng.close()
@@ -265,6 +293,10 @@ def run_approx(args, lib, dev, world, rank, dist):
         # records (key 4, permits 4, arrival index 4) + reply 4 per request; local-tier row
         # 16 B read + written per distinct key
         alg, note = n * 16 + u * 32, "n*16 + distinct*32"
+    elif name == "scatter":
+        # per pass: read key 8 + permits 4 (pass 0) or a record {key 4, permits 4, index 4};
+        # write the record and perm 4
+        alg, note = n * 28, "n*28 (wide records without ts, per pass)"
     else:
         alg, note = n * 16, "n*16"
     line = {
@@ -282,7 +314,7 @@ def run_approx(args, lib, dev, world, rank, dist):
         "granted_frac_last_batch": round(granted, 4),
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
         "refresh_ms_per_step_wall": round(refresh_s[0] / steps * 1e3, 4),
-        "roofline": _roofline(name, alg, ms, note),
+        "roofline": _roofline(name, alg, ms, note, "approx"),
         "cpu_baseline": None,
     }
     eng.close()

@@ -27,21 +27,27 @@ def short(name):
 
 
 def main():
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    # gpurun_out/pmc_<workload>_<counter>/ (tools/pmc_all.sh); older pmc_<name>/ dirs count
+    # as the uniform workload
+    agg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc_*", "run_counter_collection.csv"))):
+        tag = os.path.basename(os.path.dirname(f))[4:]
+        w = tag.split("_")[0] if tag.split("_")[0] in ("uniform", "zipf", "queue", "approx") else "uniform"
         for r in csv.DictReader(open(f)):
-            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out = {}
-    for k in sorted(agg):
-        if not k.startswith("k_"):
-            continue
-        d = {c: sum(v) / len(v) for c, v in agg[k].items()}
-        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
-        out[k] = d
-        print(k, " ".join(f"{c}={v:.4g}" for c, v in d.items()))
+            agg[w][short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    by_w = {}
+    for w in sorted(agg):
+        out = by_w.setdefault(w, {})
+        for k in sorted(agg[w]):
+            if not k.startswith("k_"):
+                continue
+            d = {c: sum(v) / len(v) for c, v in agg[w][k].items()}
+            if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+                d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+            out[k] = d
+            print(w, k, " ".join(f"{c}={v:.4g}" for c, v in d.items()))
     stages = {}
-    for k, d in out.items():
+    for k, d in by_w.get("uniform", {}).items():   # bench.py's stages: the token-bucket path
         st = STAGE.get(k.split("<")[0])
         if st and "hbm_bytes_per_launch" in d:
             e = stages.setdefault(st, {"hbm_bytes_per_launch": 0.0, "kernels": []})
@@ -52,8 +58,9 @@ def main():
     if "--write" in sys.argv:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
             json.dump({"note": "per-launch averages; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
-                               "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section)",
-                       **stages, "kernels": out}, f, indent=1)
+                               "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section); "
+                               "stages = the token-bucket (uniform) path",
+                       **stages, "kernels": by_w.get("uniform", {}), "workloads": by_w}, f, indent=1)
 
 
 if __name__ == "__main__":
