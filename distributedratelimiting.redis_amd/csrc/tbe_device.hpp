@@ -92,6 +92,53 @@ __device__ __forceinline__ ReqTime req_time(int64_t ts_us, int64_t ttl_ms) {
     return r;
 }
 
+// The same quantities for timestamps close above a base: a batch's timestamps lie in a
+// window of well under 2^32 us above its packed-record base, so (sec, usec) and the
+// millisecond snapshot follow from the base's own split plus 32-bit arithmetic on the
+// delta.  The results are identical to req_time's: sec = sec0 + (usec0 + d) / 1e6,
+// usec = (usec0 + d) % 1e6, ts / 1000 = m0 + (r0 + d) / 1000, and new_t is formed from
+// (sec, usec) by the same operations as new_t_of.  Timestamps outside the window (or a
+// base that does not split) take req_time.
+struct TimeBase {
+    int64_t tbase;
+    int64_t e0;        // 1000 * (tbase / 1000 - ttl_ms)
+    uint32_t sec0;     // tbase / 1e6
+    uint32_t usec0;    // tbase % 1e6
+    uint32_t r0;       // tbase % 1000
+    uint32_t ok;
+};
+constexpr uint64_t kRelMax = 0xFFFFFFFFull - 1000000ull;   // usec0 + d and r0 + d stay in u32
+__host__ __device__ inline TimeBase time_base(int64_t tbase, int64_t ttl_ms) {
+    TimeBase b{tbase, 0, 0, 0, 0, 0};
+    if (tbase < 0) return b;
+    const int64_t sec0 = tbase / 1000000;
+    if (sec0 > (int64_t)0xFFFFFFFFll - 10000) return b;   // sec0 + (u32 / 1e6) fits in u32
+    b.sec0 = (uint32_t)sec0;
+    b.usec0 = (uint32_t)(tbase - sec0 * 1000000);
+    b.r0 = (uint32_t)(tbase % 1000);
+    b.e0 = (tbase / 1000 - ttl_ms) * 1000;
+    b.ok = 1;
+    return b;
+}
+__device__ __forceinline__ ReqTime req_time_rel(int64_t ts_us, const TimeBase &B, int64_t ttl_ms) {
+    const uint64_t d = (uint64_t)ts_us - (uint64_t)B.tbase;
+    if (!B.ok || ts_us < B.tbase || d > kRelMax) return req_time(ts_us, ttl_ms);
+    const uint32_t u = B.usec0 + (uint32_t)d;
+    const uint32_t s1 = u / 1000000u;
+    const uint32_t usec = u - s1 * 1000000u;
+    const uint32_t sec = B.sec0 + s1;
+    const double x = (double)usec;
+    const double rcp = 1.0 / 1000000.0;
+    const double q0 = x * rcp;
+    const double r = __builtin_fma(-q0, 1000000.0, x);
+    const double q = __builtin_fma(r, rcp, q0);
+    ReqTime rt;
+    rt.new_t = (double)sec + q;
+    rt.exp_lt = B.e0 + (int64_t)((B.r0 + (uint32_t)d) / 1000u) * 1000;
+    rt.ts = ts_us;
+    return rt;
+}
+
 // One evaluation of the acquire script (TB:202-238) on a key's stored row {v, t_us}
 // (the Redis hash {v, t}), with the row's field t supplied by the caller as ft =
 // new_t_of(row.t_us) (ignored while the key is absent).  Returns the packed reply: bit
@@ -136,6 +183,15 @@ __device__ __forceinline__ uint32_t tb_acquire(Slot &s, int32_t permits, int64_t
                                                const TbParams &P, bool &modified) {
     return tb_step(s, permits, req_time(ts_us, P.ttl_ms), P, modified);
 }
+
+// ----------------------------------------------------------------- streaming memory hints
+// Non-temporal loads/stores for data touched once per kernel (table slices, pass records,
+// permutations, replies): they stream through the caches instead of displacing lines
+// that other waves are still reusing.
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T *p) { return __builtin_nontemporal_load(p); }
+template <typename T>
+__device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
 
 // ----------------------------------------------------------------- wave / block helpers
 // XCD-aware block -> tile remap (cdna_hip_programming.md T1, the bijective form): blocks

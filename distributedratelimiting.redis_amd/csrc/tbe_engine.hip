@@ -45,6 +45,29 @@ using namespace tbe;
 namespace {
 
 #ifndef TBE_PART_BLOCK
+// Non-temporal hints where data is touched once (tools/ablate.py A/B, profiles/
+// r01_v10_ablate.log): partition-pass input loads and permutation stores, the
+// un-partition passes, the fold's table slices.  NOT the partition passes' record runs
+// (their partial lines merge in L2: 50% slower streamed) nor the fold's replies (the
+// un-partition gather reuses their lines).  -DTBE_NO_NT turns them off for A/B runs.
+#ifndef TBE_NO_NT
+#define LD_P(p) ld_nt(p)
+#define ST_PERM(p, v) st_nt((p), (v))
+#define LD_U(p) ld_nt(p)
+#define ST_U(p, v) st_nt((p), (v))
+#define LD_S(p) slot_load_nt(p)
+#define ST_S(p, v) slot_store_nt((p), (v))
+#else
+#define LD_P(p) (*(p))
+#define ST_PERM(p, v) (*(p) = (v))
+#define LD_U(p) (*(p))
+#define ST_U(p, v) (*(p) = (v))
+#define LD_S(p) (*(p))
+#define ST_S(p, v) (*(p) = (v))
+#endif
+#define LD_F(p) (*(p))
+#define ST_F(p, v) (*(p) = (v))
+
 #define TBE_PART_BLOCK 512
 #endif
 #ifndef TBE_PART_ITEMS
@@ -165,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
 #pragma unroll
         for (int it = 0; it < kHistItems; ++it) {
             const uint64_t i = base + it * kBlock + tid;
-            kv[it] = (i < n) ? keys[i] : (KeyT)0;
+            kv[it] = (i < n) ? LD_P(keys + i) : (KeyT)0;
         }
         uint32_t skv[kHistItems];
         if (HOT && any_hot) {
@@ -539,9 +562,9 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         for (int it = 0; it < kPartItems; ++it) {
             const int e = it * kPartBlock + tid;
             const bool v = e < nvalid;
-            kv[it] = v ? kin[base + e] : 0ull;
-            pv[it] = v ? pin[base + e] : 0;
-            tv[it] = v ? tin[base + e] : 0;
+            kv[it] = v ? LD_P(kin + base + e) : 0ull;
+            pv[it] = v ? LD_P(pin + base + e) : 0;
+            tv[it] = v ? LD_P(tin + base + e) : 0;
         }
         // the table fill overlaps the tile loads above
         any_hot = HOT && hot_load<kPartBlock>(hot, hs);
@@ -564,7 +587,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
             const int e = it * kPartBlock + tid;
-            rec[it] = (e < nvalid) ? rin[base + e] : 0ull;
+            rec[it] = (e < nvalid) ? LD_P(rin + base + e) : 0ull;
             key[it] = (uint32_t)(rec[it] & F.kmask);
         }
     }
@@ -577,7 +600,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         if (e < nvalid) {
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             stage[lpos[it]] = rec[it];
-            perm[base + e] = goff[d] + lpos[it] - L.lstart[d];
+            ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
         }
     }
     __syncthreads();
@@ -587,7 +610,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         if (j < nvalid) {
             const uint64_t s = stage[j];
             const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
-            rout[goff[d] + (uint32_t)j - L.lstart[d]] = s;
+            rout[goff[d] + (uint32_t)j - L.lstart[d]] = s;   // runs merge in L2: keep cached
         }
     }
     if (FIRST && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
@@ -610,6 +633,19 @@ constexpr int kFoldPer = 4;                                 // requests per thre
 constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
 constexpr int kMaxRows = 1 << kMaxRBits;
 constexpr int kFoldTail = kFoldBlock;                       // compact pending list after round 1
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Slot slot_load_nt(const Slot *p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    Slot s;
+    __builtin_memcpy(&s, &v, sizeof s);
+    return s;
+}
+__device__ __forceinline__ void slot_store_nt(Slot *p, const Slot &s) {
+    u32x4 v;
+    __builtin_memcpy(&v, &s, sizeof v);
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
 
 template <bool PACKED>
 __global__ __launch_bounds__(kFoldBlock) void k_fold(
@@ -647,6 +683,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
     Slot *__restrict__ rows = table + row0;
     const bool dense = (e - s) >= (R >> 3);
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
 
     uint32_t kl[kFoldPer];
@@ -664,7 +701,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
             if (q < e) {
                 if (PACKED) {
                     uint32_t k;
-                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], tsv[r]);
+                    unpack_rec(LD_F(srec + q), ts_orig, tbase, F, k, pm[r], tsv[r]);
                     kl[r] = k & rmask;
                 } else {
                     kl[r] = skeys[q] & rmask;
@@ -682,7 +719,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
             const uint32_t j = tid + u * kFoldBlock;
-            tmp[u] = rows[j < nrows ? j : nrows - 1];   // unconditional: keeps tmp in VGPRs
+            tmp[u] = LD_S(rows + (j < nrows ? j : nrows - 1));   // unconditional: keeps tmp in VGPRs
         }
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
@@ -733,7 +770,8 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         }
         ReqTime rq[kFoldPer];
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) rq[r] = req_time(tsv[r], P.ttl_ms);
+        for (int r = 0; r < kFoldPer; ++r) rq[r] = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms)
+                                                           : req_time(tsv[r], P.ttl_ms);
         __syncthreads();   // claimed rows and their field t visible
         uint32_t rep[kFoldPer];
 #pragma unroll
@@ -849,12 +887,13 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            if (q < e && (keep & (1u << r))) res[q] = rep[r];
+            if (q < e && (keep & (1u << r))) ST_F(res + q, rep[r]);
         }
     }
     __syncthreads();
+    // the slice streams out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log)
     for (uint32_t j = tid; j < nrows; j += kFoldBlock)
-        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) rows[j] = row[j];
+        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) ST_S(rows + j, row[j]);
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
         for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
@@ -891,7 +930,7 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
 #pragma unroll
     for (int it = 0; it < kUnItems; ++it) {
         const int e = it * kUnBlock + tid;
-        pv[it] = (e < nvalid) ? perm[base + e] : 0u;
+        pv[it] = (e < nvalid) ? LD_U(perm + base + e) : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kUnItems; ++it) {
@@ -904,14 +943,14 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
         if (FINAL && WAIT) {
-            granted[i] = (uint8_t)(r[it] >> 30);
+            ST_U(granted + i, (uint8_t)(r[it] >> 30));
             const uint32_t rem = r[it] & kRemNone;
-            remaining[i] = (rem == kRemNone) ? -1 : (int32_t)rem;
+            ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
         } else if (FINAL) {
-            granted[i] = (uint8_t)(r[it] >> 31);
-            remaining[i] = (int32_t)(r[it] & 0x7FFFFFFFu);
+            ST_U(granted + i, (uint8_t)(r[it] >> 31));
+            ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
         } else {
-            res_out[i] = r[it];
+            ST_U(res_out + i, r[it]);
         }
     }
 }
@@ -1046,6 +1085,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     if (s0 == e0) return;
     const uint32_t j0 = segbase[h], nseg = segbase[h + 1] - j0;
     const int64_t tbase = pack_base(ts_orig, F);
+    const TimeBase TB = time_base(tbase, P.ttl_ms);
     if (tid == 0) {
         S = table[key];
         ftS = new_t_of(S.t_us == kAbsent ? 0 : S.t_us);
@@ -1094,7 +1134,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
                     unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts);
                     pend |= 1u << r;
                 }
-                rq[r] = req_time(ts, P.ttl_ms);
+                rq[r] = req_time_rel(ts, TB, P.ttl_ms);
             }
             if (tid == 0) own = 0;
             __syncthreads();
@@ -1155,6 +1195,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     const int tid = threadIdx.x;
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
+    const TimeBase TB = time_base(tbase, P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const SegState st = sst[j];
         if (!st.pass) continue;
@@ -1168,7 +1209,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
             unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
             Slot c = st.s;
             bool m;
-            res[q] = tb_step_ft(c, st.ft, p, req_time(ts, P.ttl_ms), P, m);
+            res[q] = tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m);
         }
     }
 }
@@ -1274,8 +1315,8 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
     if (dense) {
         for (uint32_t j = tid; j < R; j += kQBlock) {
             const uint32_t jj = j < nrows ? j : nrows - 1;
-            const Slot t = rows[jj];
-            const uint64_t h = hrows[jj];
+            const Slot t = LD_S(rows + jj);
+            const uint64_t h = LD_U(hrows + jj);
             slot[j] = t;
             qh[j] = h;
         }
@@ -1410,8 +1451,8 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
     __syncthreads();
     for (uint32_t j = tid; j < nrows; j += kQBlock)
         if (dense || (dirty[j >> 5] & (1u << (j & 31)))) {
-            rows[j] = slot[j];
-            hrows[j] = qh[j];
+            ST_S(rows + j, slot[j]);
+            ST_U(hrows + j, qh[j]);
         }
 }
 

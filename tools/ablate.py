@@ -17,9 +17,7 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "match": (["TBE_HIST_MATCH"], []),
-    "zipf": ([], ["--workload", "zipf", "--zipf-batches", "1"]),
-    "zipf_match": (["TBE_HIST_MATCH"], ["--workload", "zipf", "--zipf-batches", "1"]),
+    "no_nt": (["TBE_NO_NT"], []),
 }
 
 
