@@ -216,7 +216,7 @@ def main():
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(name), "alg_bytes_per_launch": alg_bytes,
+                    "traffic": pmc_traffic(name, args.workload), "alg_bytes_per_launch": alg_bytes,
                     "avg_launch_ms": round(per_launch_ms, 4),
                     "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
                                "engine stream" if replay_check is not None else
@@ -291,15 +291,23 @@ def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool
     return n * 4
 
 
-def pmc_traffic(stage: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+def pmc_traffic(stage: str, workload: str = "uniform"):
+    """HBM bytes per launch of `stage` in `workload`'s runs, from the committed rocprofv3
+    PMC summary (tools/pmc_all.sh + tools/pmc_summary.py --write), if present."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(stage, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    if workload == "uniform":
+        return d.get(stage, {}).get("hbm_bytes_per_launch")
+    prefix = {"fold": "k_fold<", "scatter": "k_scatter_rec<", "hist": "k_hist<",
+              "unscatter": "k_unscatter<"}.get(stage)
+    kern = d.get("workloads", {}).get(workload, {})
+    v = [k["hbm_bytes_per_launch"] for name, k in kern.items()
+         if prefix and name.startswith(prefix) and "hbm_bytes_per_launch" in k]
+    return round(sum(v) / len(v), 1) if v else None
 
 
 def workload_name(args, n: int) -> str:

@@ -681,7 +681,8 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-    const bool dense = (e - s) >= (R >> 3);
+    // Whole slice (dense) or touched rows only (sparse), decided below.
+    bool dense = (e - s) >= (R >> 1);
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
@@ -713,6 +714,24 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         }
     };
     load_chunk(s);   // in flight together with the dense slice
+    if (!dense && (e - s) >= (R >> 3)) {
+        // Between R/8 and R/2 requests (one chunk) the distinct rows decide: uniform
+        // traffic touches nearly every 128-byte line of the slice, skewed traffic (few
+        // keys, many requests each) a fraction of them, which it gathers instead.
+        for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) dirty[j] = 0;
+        __syncthreads();
+        uint32_t first = 0;
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r) {
+            if (pend & (1u << r)) {
+                const uint32_t bit = 1u << (kl[r] & 31);
+                if (!(atomicOr(&dirty[kl[r] >> 5], bit) & bit)) ++first;
+            }
+        }
+        uint32_t distinct;
+        (void)block_excl_scan<kFoldBlock>(first, wsum, &distinct);
+        dense = distinct >= (R >> 2);
+    }
     if (dense) {
         constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
         Slot tmp[kRowsPerThread];

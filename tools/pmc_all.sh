@@ -8,7 +8,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-for W in ${WORKLOADS:-uniform queue approx}; do
+for W in ${WORKLOADS:-uniform zipf queue approx}; do
     for C in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$C" -o run -- \
             python3 "$ROOT/bench.py" --workload $W --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline \

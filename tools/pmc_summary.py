@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs (gpurun_out/pmc_*/run_counter_collection.csv) per kernel:
-average counter value per dispatch, plus HBM bytes per launch with the gfx950 correction
+median counter value per dispatch, plus HBM bytes per launch with the gfx950 correction
 from MI355X_MICROARCH.md (FETCH_SIZE counts half of a wide coalesced read: x2; both
 counters are in KiB).  Writes profiles/pmc_summary.json when --write is given."""
 import collections
@@ -41,7 +41,9 @@ def main():
         for k in sorted(agg[w]):
             if not k.startswith("k_"):
                 continue
-            d = {c: sum(v) / len(v) for c, v in agg[w][k].items()}
+            # median per dispatch: robust to warm-up dispatches (a Zipf run's first batches
+            # fold hot keys in their buckets before the hot set exists)
+            d = {c: sorted(v)[len(v) // 2] for c, v in agg[w][k].items()}
             if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
                 d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
             out[k] = d
@@ -57,7 +59,7 @@ def main():
         e["hbm_bytes_per_launch"] /= len(e["kernels"])
     if "--write" in sys.argv:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
-            json.dump({"note": "per-launch averages; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
+            json.dump({"note": "per-launch medians; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
                                "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section); "
                                "stages = the token-bucket (uniform) path",
                        **stages, "kernels": by_w.get("uniform", {}), "workloads": by_w}, f, indent=1)
