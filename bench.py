@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-pack", action="store_true",
                     help="wide pass records even where the packed 8-byte form applies (A/B)")
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
+    ap.add_argument("--no-narrow", action="store_true",
+                    help="4-byte replies even where TokenLimit <= 127 allows 1-byte ones (A/B)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     args = ap.parse_args()
@@ -122,7 +124,7 @@ def main():
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                             args.period_ticks, device=dev.index,
                             stage_timing=not args.no_stage_timing, max_batch=n,
-                            pack=not args.no_pack, hot=not args.no_hot,
+                            pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                             pipeline=not args.no_pipeline)
     layout = eng.layout()
     total_steps = args.warmup + args.steps
@@ -186,7 +188,7 @@ def main():
         eng.close()
         ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                                 args.period_ticks, device=dev.index, stage_timing=True,
-                                max_batch=n, pack=not args.no_pack, hot=not args.no_hot,
+                                max_batch=n, pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                                 pipeline=False)
         g2 = torch.empty_like(granted)
         r2 = torch.empty_like(remaining)
@@ -212,7 +214,8 @@ def main():
         distinct = None
         if zkeys:   # distinct keys per batch, measured (the uniform estimate does not apply)
             distinct = float(np.mean([np.unique(zk).size for zk, _ in zkeys]))
-        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct)
+        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct,
+                                      1 if layout.get("narrow") else 4)
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -267,16 +270,16 @@ def main():
 
 
 def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool,
-                      distinct: float = None) -> int:
+                      distinct: float = None, reply: int = 4) -> int:
     """Bytes one launch of `stage` must move at minimum for its function,
     averaged over the passes where a stage runs once per pass.  Packed: the passes and
     the fold move one 8-byte record per request; wide: {key u32, permits i32, ts i64}."""
     rec = 8 if packed else 16
     if stage == "fold":
-        # sorted records + packed reply 4 per request, plus the table rows of the distinct
-        # keys in the batch (16 B read + 16 B written each)
+        # sorted records + packed reply (4 bytes, or 1 when TokenLimit <= 127) per request,
+        # plus the table rows of the distinct keys in the batch (16 B read + 16 B written)
         u = distinct if distinct is not None else n_keys * (1.0 - np.exp(-n / n_keys))
-        return int(n * (rec + 4) + u * 32)
+        return int(n * (rec + reply) + u * 32)
     if stage == "scatter":
         # pass 0 reads the caller's key 8 + permits 4 + ts 8, later passes one record;
         # every pass writes a record and its 4-byte permutation entry
@@ -286,8 +289,8 @@ def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool
     if stage == "bounds":
         return n * (8 if packed else 4)
     if stage == "unscatter":
-        # perm 4 + gathered reply 4 + written 4 (inner passes) or 5 (final: u8 + i32)
-        return int(n * (12 * (passes - 1) + 13) / passes)
+        # perm 4 + gathered reply + written reply (inner passes) or 5 (final: u8 + i32)
+        return int(n * ((4 + 2 * reply) * (passes - 1) + 9 + reply) / passes)
     return n * 4
 
 

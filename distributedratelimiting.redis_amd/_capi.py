@@ -22,6 +22,7 @@ TBE_FLAG_STAGE_TIMING = 0x1
 TBE_FLAG_NO_PACK = 0x2
 TBE_FLAG_NO_HOT = 0x4
 TBE_FLAG_NO_PIPELINE = 0x8
+TBE_FLAG_NO_NARROW = 0x10
 STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter", "hot")
 
 # Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).

@@ -647,13 +647,24 @@ __device__ __forceinline__ void slot_store_nt(Slot *p, const Slot &s) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
 }
 
+// A token-bucket reply is {granted, trunc(new_v)} with 0 <= trunc(new_v) <= TokenLimit.
+// When TokenLimit <= 127 it travels as one byte (bit 7 granted, bits 0-6 remaining)
+// through the fold and the un-partition passes instead of four.
+__device__ __forceinline__ void put_reply(uint32_t *res, uint32_t q, uint32_t rep, uint32_t narrow) {
+    if (narrow)
+        reinterpret_cast<uint8_t *>(res)[q] = (uint8_t)(((rep >> 24) & 0x80u) | (rep & 0x7Fu));
+    else
+        res[q] = rep;
+}
+
 template <bool PACKED>
 __global__ __launch_bounds__(kFoldBlock) void k_fold(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
-    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next) {
+    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
+    uint32_t narrow) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -890,7 +901,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
                         if (!dense) atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
                         tp = false;
                     }
-                    if (!tp) res[c + tlid] = trep;
+                    if (!tp) put_reply(res, c + tlid, trep, narrow);
                 }
                 if (!__syncthreads_or(tp)) break;
             }
@@ -906,7 +917,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            if (q < e && (keep & (1u << r))) ST_F(res + q, rep[r]);
+            if (q < e && (keep & (1u << r))) put_reply(res, q, rep[r], narrow);
         }
     }
     __syncthreads();
@@ -933,7 +944,7 @@ __device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, u
     return (status << 30) | (evaluated ? (rem & kRemNone) : kRemNone);
 }
 
-template <bool FINAL, bool WAIT>
+template <bool FINAL, bool WAIT, bool NARROW = false>
 __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
                                                           const uint32_t *__restrict__ res_in,
                                                           uint32_t *__restrict__ res_out,
@@ -954,7 +965,9 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
 #pragma unroll
     for (int it = 0; it < kUnItems; ++it) {
         const int e = it * kUnBlock + tid;
-        r[it] = (e < nvalid) ? res_in[pv[it]] : 0u;
+        r[it] = (e < nvalid) ? (NARROW ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[pv[it]]
+                                       : res_in[pv[it]])
+                             : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kUnItems; ++it) {
@@ -965,9 +978,14 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
             ST_U(granted + i, (uint8_t)(r[it] >> 30));
             const uint32_t rem = r[it] & kRemNone;
             ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
+        } else if (FINAL && NARROW) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 7));
+            ST_U(remaining + i, (int32_t)(r[it] & 0x7Fu));
         } else if (FINAL) {
             ST_U(granted + i, (uint8_t)(r[it] >> 31));
             ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
+        } else if (NARROW) {
+            ST_U(reinterpret_cast<uint8_t *>(res_out) + i, (uint8_t)r[it]);
         } else {
             ST_U(res_out + i, r[it]);
         }
@@ -1091,7 +1109,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     const uint32_t *__restrict__ bstart, uint32_t nb, const HotSet *__restrict__ hot,
     HotSet *__restrict__ hot_next, const uint32_t *__restrict__ segbase,
     const SegSummary *__restrict__ summ, SegState *__restrict__ sst, Slot *__restrict__ table,
-    TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err) {
+    TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow) {
     __shared__ Slot S;
     __shared__ double ftS;
     __shared__ uint32_t first, own;
@@ -1189,7 +1207,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
                 const uint32_t q = c + r * kSegBlock + tid;
-                if (q < b) res[q] = rep[r];
+                if (q < b) put_reply(res, q, rep[r], narrow);
             }
         }
         __syncthreads();
@@ -1209,7 +1227,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
     const SegState *__restrict__ sst, TbParams P, uint32_t *__restrict__ res,
-    const uint32_t *__restrict__ err) {
+    const uint32_t *__restrict__ err, uint32_t narrow) {
     if (*err) return;
     const int tid = threadIdx.x;
     const uint32_t total = segbase[kHotKeysMax];
@@ -1228,7 +1246,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
             unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
             Slot c = st.s;
             bool m;
-            res[q] = tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m);
+            put_reply(res, q, tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m), narrow);
         }
     }
 }
@@ -1908,6 +1926,7 @@ struct tbe_engine {
     uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
     int passes = 0;          // 8-bit LSD passes over the bucket id
     bool packed = false;     // token bucket: passes move packed u64 records (PackFmt)
+    bool narrow = false;     // token bucket, packed, TokenLimit <= 127: one-byte replies (put_reply)
     PackFmt pf{};
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
@@ -2260,11 +2279,11 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     } else if (e->packed) {
         k_fold<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, w.res[0], w.err, hot_next);
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
     } else {
         k_fold<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr);
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {
@@ -2277,9 +2296,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                    w.segbase, w.summ, w.err);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
                                                       hot_next, w.segbase, w.summ, w.sst, e->table,
-                                                      e->params, w.res[0], w.err);
+                                                      e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                   w.segbase, w.sst, e->params, w.res[0], w.err);
+                                                   w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
         k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap, w.err);
         stage_end(e, ST_HOT, sf);
     }
@@ -2287,11 +2306,18 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        k_unscatter<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
-                                                                w.res[cur ^ 1], nullptr, nullptr);
+        if (e->narrow && !wait && !approx)
+            k_unscatter<false, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                      w.res[cur ^ 1], nullptr, nullptr);
+        else
+            k_unscatter<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                    w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
-    if (wait)
+    if (e->narrow && !wait && !approx)
+        k_unscatter<true, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                     nullptr, granted, remaining);
+    else if (wait)
         k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                               nullptr, granted, remaining);
     else
@@ -2405,6 +2431,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
+        e->narrow = e->packed && c.token_limit <= 127 && (c.flags & TBE_FLAG_NO_NARROW) == 0;
     }
 
     auto bail = [&](tbe_status st) {
@@ -3050,7 +3077,8 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     if (!e || !passes || !r_bits || !packed) return TBE_EINVAL;
     *passes = (uint32_t)e->passes;
     *r_bits = (uint32_t)e->r_bits;
-    *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u);
+    *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
+              (e->narrow ? 8u : 0u);
     return TBE_OK;
 }
 

@@ -75,6 +75,9 @@ typedef struct tbe_config {
 #define TBE_FLAG_NO_PIPELINE 0x8u         /* token bucket: run every stage of a batch on one
                                              stream (A/B checks); by default batch b+1's
                                              partition overlaps batch b's fold */
+#define TBE_FLAG_NO_NARROW 0x10u          /* token bucket: keep 4-byte replies through the fold
+                                             and un-partition passes even when TokenLimit
+                                             <= 127 allows 1-byte ones (A/B checks) */
 
 typedef struct tbe_engine tbe_engine;
 
@@ -252,7 +255,8 @@ tbe_status tbe_approx_query(tbe_engine *engine, uint64_t key, int32_t *local, in
  * each), *packed: bit 0 set when the passes move packed 8-byte request records (token
  * bucket kind) rather than the wide {key, permits, ts} records, bit 1 set
  * when hot keys get runs of their own (TBE_FLAG_NO_HOT clears it), bit 2 set when
- * consecutive device batches overlap (TBE_FLAG_NO_PIPELINE clears it). */
+ * consecutive device batches overlap (TBE_FLAG_NO_PIPELINE clears it), bit 3 set when
+ * replies travel as one byte (TBE_FLAG_NO_NARROW clears it). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* Per-stage device time (ms) accumulated since the last call, when

@@ -323,3 +323,26 @@ def test_single_hot_key_many_segments(engine_lib, gpu):
         t = (S_US + b * 300_000_000 + np.arange(n, dtype=np.int64) * 1000).astype(np.int64)
         run_and_compare(eng, ref, k, np.ones(n, np.int32), t)
     assert_same_state(eng, ref)
+
+
+@pytest.mark.parametrize("narrow,cap", [(True, 127), (False, 10), (True, 1000)],
+                         ids=["narrow_cap127", "wide_forced", "wide_cap1000"])
+def test_reply_width(engine_lib, gpu, narrow, cap):
+    """One-byte replies (TokenLimit <= 127) and four-byte ones (forced, or TokenLimit too
+    large) through the fold, the hot-key runs and the un-partition passes, on Zipf traffic
+    with a fast refill so remaining values span 0..TokenLimit."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate, workloads
+    n_keys, n = 500_000, 1 << 19
+    tokens = cap * 50
+    eng = TokenBucketEngine(n_keys, cap, tokens, 10_000_000, device=0, narrow=narrow)
+    assert eng.layout()["narrow"] == (narrow and cap <= 127)
+    ref = cref.CTokenBucket(n_keys, cap, fill_rate(tokens, 10_000_000))
+    zs = workloads.ZipfSampler(n_keys, 1.1)
+    rng = np.random.default_rng(cap)
+    for b in range(4):
+        k = workloads.zipf_keys(0x5EED0007, n_keys, b * n, n, sampler=zs)
+        p = rng.integers(0, 4, n).astype(np.int32)
+        t = workloads.batch_timestamps(b, n, 10_000, trace.T0_US)
+        g, r = run_and_compare(eng, ref, k, p, t)
+    assert r.max() == cap or r.max() >= cap - 3
+    assert_same_state(eng, ref)
