@@ -657,8 +657,11 @@ __device__ __forceinline__ void put_reply(uint32_t *res, uint32_t q, uint32_t re
         res[q] = rep;
 }
 
+// Full buckets (>= R/2 requests, uniform traffic): 512-thread workgroups with the rows'
+// field t cached in LDS (74.5 KB, two workgroups per CU), one chunk of 2048 requests.
+// k_fold below takes the other buckets.
 template <bool PACKED>
-__global__ __launch_bounds__(kFoldBlock) void k_fold(
+__global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
@@ -692,8 +695,10 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-    // Whole slice (dense) or touched rows only (sparse), decided below.
-    bool dense = (e - s) >= (R >> 1);
+    // Buckets with >= R/2 requests only (k_fold takes the others): nearly every line of
+    // the slice is touched, so the whole slice is pulled in and written back.
+    if (e - s < (R >> 1)) return;
+    const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
@@ -725,24 +730,6 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
         }
     };
     load_chunk(s);   // in flight together with the dense slice
-    if (!dense && (e - s) >= (R >> 3)) {
-        // Between R/8 and R/2 requests (one chunk) the distinct rows decide: uniform
-        // traffic touches nearly every 128-byte line of the slice, skewed traffic (few
-        // keys, many requests each) a fraction of them, which it gathers instead.
-        for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) dirty[j] = 0;
-        __syncthreads();
-        uint32_t first = 0;
-#pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
-            if (pend & (1u << r)) {
-                const uint32_t bit = 1u << (kl[r] & 31);
-                if (!(atomicOr(&dirty[kl[r] >> 5], bit) & bit)) ++first;
-            }
-        }
-        uint32_t distinct;
-        (void)block_excl_scan<kFoldBlock>(first, wsum, &distinct);
-        dense = distinct >= (R >> 2);
-    }
     if (dense) {
         constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
         Slot tmp[kRowsPerThread];
@@ -927,6 +914,308 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold(
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
         for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
+            if (hcnt[j] >= kHotMin) {
+                const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
+                if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)hcnt[j] << 32) | (uint32_t)(row0 + j);
+            }
+        }
+    }
+}
+
+// k_fold's shape: 256-thread workgroups, 4 requests per thread per chunk, 48.5 KB of
+// LDS, so three workgroups share a CU (the fold is latency-bound: one workgroup per CU
+// instead of two doubles its time, profiles/r01_v11_ablate_occupancy.log).  The row's
+// field t is derived per evaluation (field_t) instead of being cached in LDS.
+constexpr int kTbBlock = 256;
+constexpr int kTbPer = 4;
+constexpr int kTbTail = kTbBlock;                         // compact pending list after round 1
+constexpr int kTbChunk = kTbBlock * kTbPer;               // 1024 requests per chunk
+constexpr int kTailPer = kTbTail / kTbBlock;              // its entries per thread
+constexpr int64_t kRowWindow = (int64_t)1 << 31;          // field_t fast path: rows up to ~35 min older
+
+// Field t of a stored row (TB:203 applied to t_us; only used while the key is present).
+__device__ __forceinline__ double field_t(int64_t t_us, const TimeBase &B) {
+    return req_time_rel(t_us == kAbsent ? 0 : t_us, B, 0).new_t;
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(kTbBlock) void k_fold(
+    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
+    const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
+    const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
+    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
+    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
+    uint32_t narrow) {
+    __shared__ Slot row[kMaxRows];
+    // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
+    // compact list of requests still pending after round 1 (t_*)
+    __shared__ uint32_t aux[kMaxRows];
+    __shared__ uint32_t wsum[kTbBlock / 64];
+    uint32_t *hcnt = aux;
+    uint32_t *t_kl_lid = aux;
+    int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kTbTail;
+    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kTbTail;
+    static_assert(kTbTail * 16 <= kMaxRows * 4, "tail list fits in aux");
+    static_assert(kTbChunk <= 4096, "election tags hold 12-bit local ids");
+    __shared__ uint32_t own[kMaxRows];
+    __shared__ uint32_t loaded[kMaxRows / 32];
+    __shared__ uint32_t dirty[kMaxRows / 32];
+
+    if (*err) return;
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) return;
+    const uint32_t R = 1u << r_bits;
+    const uint32_t rmask = R - 1;
+    const uint64_t row0 = (uint64_t)b << r_bits;
+    const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
+    Slot *__restrict__ rows = table + row0;
+    if (e - s >= (R >> 1)) return;   // k_fold_wide's
+    // Whole slice (dense) or touched rows only (sparse), decided below.
+    bool dense = false;
+    const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    // one time base for request times and row field times: kRowWindow below the packed
+    // base, so rows granted up to ~35 minutes before the batch also take the fast path
+    const TimeBase TB = time_base(PACKED ? tbase - kRowWindow : -1, P.ttl_ms);
+    const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
+
+    uint32_t kl[kTbPer];
+    int32_t pm[kTbPer];
+    int64_t tsv[kTbPer];
+    uint32_t pend = 0;
+    auto load_chunk = [&](uint32_t c) {
+        pend = 0;
+#pragma unroll
+        for (int r = 0; r < kTbPer; ++r) {
+            const uint32_t q = c + r * kTbBlock + tid;
+            kl[r] = 0;
+            pm[r] = 0;
+            tsv[r] = 0;
+            if (q < e) {
+                if (PACKED) {
+                    uint32_t k;
+                    unpack_rec(LD_F(srec + q), ts_orig, tbase, F, k, pm[r], tsv[r]);
+                    kl[r] = k & rmask;
+                } else {
+                    kl[r] = skeys[q] & rmask;
+                    pm[r] = sperm[q];
+                    tsv[r] = sts[q];
+                }
+                pend |= 1u << r;
+            }
+        }
+    };
+    load_chunk(s);   // in flight together with the dense slice
+    if (!dense && (e - s) >= (R >> 3)) {
+        // Between R/8 and R/2 requests the distinct rows of the first chunk decide:
+        // uniform traffic touches nearly every 128-byte line of the slice, skewed traffic
+        // (few keys, many requests each) a fraction of them, which it gathers instead.
+        for (uint32_t j = tid; j < (R + 31) / 32; j += kTbBlock) dirty[j] = 0;
+        __syncthreads();
+        uint32_t first = 0;
+#pragma unroll
+        for (int r = 0; r < kTbPer; ++r) {
+            if (pend & (1u << r)) {
+                const uint32_t bit = 1u << (kl[r] & 31);
+                if (!(atomicOr(&dirty[kl[r] >> 5], bit) & bit)) ++first;
+            }
+        }
+        uint32_t distinct;
+        (void)block_excl_scan<kTbBlock>(first, wsum, &distinct);
+        dense = distinct >= (R >> 2);
+    }
+    if (dense) {
+        constexpr int kHalf = kMaxRows / kTbBlock / 2;   // two rounds of 4 rows per thread
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            Slot tmp[kHalf];
+#pragma unroll
+            for (int u = 0; u < kHalf; ++u) {
+                const uint32_t j = tid + (h * kHalf + u) * kTbBlock;
+                tmp[u] = LD_S(rows + (j < nrows ? j : nrows - 1));   // unconditional: keeps tmp in VGPRs
+            }
+#pragma unroll
+            for (int u = 0; u < kHalf; ++u) {
+                const uint32_t j = tid + (h * kHalf + u) * kTbBlock;
+                if (j < nrows) row[j] = tmp[u];
+            }
+        }
+    }
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kTbBlock) {
+        loaded[j] = 0;
+        dirty[j] = 0;
+    }
+
+    for (uint32_t c = s; c < e; c += kTbChunk) {
+        if (c != s) load_chunk(c);
+        for (uint32_t j = tid; j < R; j += kTbBlock) own[j] = 0;
+        if (count_hot && c == s)
+            for (uint32_t j = tid; j < R; j += kTbBlock) hcnt[j] = 0;
+        __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
+        if (count_hot) {
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r)
+                if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
+        }
+        if (!dense) {
+            // First touch of a row in a sparse bucket: claim it and pull it into LDS.
+            uint32_t mine = 0;
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r) {
+                if (pend & (1u << r)) {
+                    const uint32_t bit = 1u << (kl[r] & 31);
+                    if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
+                }
+            }
+            Slot tmp[kTbPer];
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r) {
+                tmp[r] = Slot{0.0, 0};                   // fully initialised: stays in VGPRs
+                if (mine & (1u << r)) tmp[r] = rows[kl[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r)
+                if (mine & (1u << r)) row[kl[r]] = tmp[r];
+        }
+        __syncthreads();   // claimed rows visible
+        uint32_t rep[kTbPer];
+#pragma unroll
+        for (int r = 0; r < kTbPer; ++r) rep[r] = 0;
+        // Speculative rounds.  Every pending request evaluates the script
+        // against its key's current row.  An evaluation that does not modify the row (a
+        // deny without expiry) leaves it as it found it, so the key's pending requests up
+        // to its earliest modifying one are decided by this round's evaluations; that
+        // earliest one commits the row it computed and later ones wait for the next
+        // round.  A key whose requests in the chunk all deny settles in one round.
+        // Election slot: (round << 12) | (4095 - local id); the max is the key's earliest
+        // modifier of the newest round, so no reset between rounds.  Workgroup-uniform
+        // loops: every thread runs every round and the only exits are __syncthreads_or.
+        auto eval_slots = [&](uint32_t round, Slot (&nrow)[kTbPer]) {
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r) {
+                nrow[r] = Slot{0.0, 0};
+                if (pend & (1u << r)) {
+                    nrow[r] = row[kl[r]];
+                    bool m;
+                    const ReqTime rq = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
+                    rep[r] = tb_step_ft(nrow[r], field_t(nrow[r].t_us, TB), pm[r], rq, P, m);
+                    if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kTbBlock + tid)));
+                }
+            }
+        };
+        auto resolve_slots = [&](uint32_t round, const Slot (&nrow)[kTbPer]) {
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r) {
+                if (!(pend & (1u << r))) continue;
+                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kTbBlock + tid));
+                const uint32_t o = own[kl[r]];
+                if ((o >> 12) != round || o < tag) {
+                    pend &= ~(1u << r);             // before the key's first modifier: decided
+                } else if (o == tag) {
+                    row[kl[r]] = nrow[r];           // the row this round's evaluation produced
+                    if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                    pend &= ~(1u << r);
+                }
+            }
+        };
+        {
+            Slot nrow[kTbPer];
+            eval_slots(1u, nrow);
+            __syncthreads();
+            resolve_slots(1u, nrow);
+        }
+        // Round 1 settles every key's first request.  The few left pending move to a
+        // compact list (one per thread) so later rounds evaluate one request per thread
+        // instead of every slot of every lane.
+        uint32_t n_tail;
+        const uint32_t tail_at = block_excl_scan<kTbBlock>(__popc(pend), wsum, &n_tail);
+        uint32_t keep = ~0u;                     // slots whose reply this thread stores
+        if (n_tail != 0 && n_tail <= kTbTail && !count_hot) {
+            uint32_t at = tail_at;
+#pragma unroll
+            for (int r = 0; r < kTbPer; ++r) {
+                if (pend & (1u << r)) {
+                    t_kl_lid[at] = kl[r] | ((uint32_t)(r * kTbBlock + tid) << 16);
+                    t_pm[at] = pm[r];
+                    t_ts[at] = tsv[r];
+                    ++at;
+                }
+            }
+            keep = ~pend;
+            pend = 0;
+            __syncthreads();
+            bool tp[kTailPer];
+            uint32_t tkl[kTailPer], tlid[kTailPer], trep[kTailPer];
+            int32_t tpm[kTailPer];
+            ReqTime trq[kTailPer];
+#pragma unroll
+            for (int i = 0; i < kTailPer; ++i) {
+                const uint32_t x = tid + i * kTbBlock;
+                tp[i] = x < n_tail;
+                tkl[i] = tlid[i] = trep[i] = 0;
+                tpm[i] = 0;
+                trq[i] = ReqTime{0.0, 0, 0};
+                if (tp[i]) {
+                    tkl[i] = t_kl_lid[x] & 0xFFFFu;
+                    tlid[i] = t_kl_lid[x] >> 16;
+                    tpm[i] = t_pm[x];
+                    trq[i] = PACKED ? req_time_rel(t_ts[x], TB, P.ttl_ms) : req_time(t_ts[x], P.ttl_ms);
+                }
+            }
+            for (uint32_t round = 2;; ++round) {
+                Slot nr[kTailPer];
+#pragma unroll
+                for (int i = 0; i < kTailPer; ++i) {
+                    nr[i] = Slot{0.0, 0};
+                    if (tp[i]) {
+                        nr[i] = row[tkl[i]];
+                        bool m;
+                        trep[i] = tb_step_ft(nr[i], field_t(nr[i].t_us, TB), tpm[i], trq[i], P, m);
+                        if (m) atomicMax(&own[tkl[i]], (round << 12) | (4095u - tlid[i]));
+                    }
+                }
+                __syncthreads();
+                bool any = false;
+#pragma unroll
+                for (int i = 0; i < kTailPer; ++i) {
+                    if (!tp[i]) continue;
+                    const uint32_t tag = (round << 12) | (4095u - tlid[i]);
+                    const uint32_t o = own[tkl[i]];
+                    if ((o >> 12) != round || o < tag) {
+                        tp[i] = false;
+                    } else if (o == tag) {
+                        row[tkl[i]] = nr[i];
+                        if (!dense) atomicOr(&dirty[tkl[i] >> 5], 1u << (tkl[i] & 31));
+                        tp[i] = false;
+                    }
+                    if (!tp[i]) put_reply(res, c + tlid[i], trep[i], narrow);
+                    any |= tp[i];
+                }
+                if (!__syncthreads_or(any)) break;
+            }
+        } else if (n_tail != 0) {
+            for (uint32_t round = 2;; ++round) {
+                Slot nrow[kTbPer];
+                eval_slots(round, nrow);
+                __syncthreads();
+                resolve_slots(round, nrow);
+                if (!__syncthreads_or(pend != 0)) break;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kTbPer; ++r) {
+            const uint32_t q = c + r * kTbBlock + tid;
+            if (q < e && (keep & (1u << r))) put_reply(res, q, rep[r], narrow);
+        }
+    }
+    __syncthreads();
+    // the slice streams out (non-temporal: 12% faster fold, profiles/r01_v10_ablate_nt_variants.log)
+    for (uint32_t j = tid; j < nrows; j += kTbBlock)
+        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) ST_S(rows + j, row[j]);
+    if (count_hot) {
+        // nominate this bucket's hot keys for their own runs in the next batch
+        for (uint32_t j = tid; j < nrows; j += kTbBlock) {
             if (hcnt[j] >= kHotMin) {
                 const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
                 if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)hcnt[j] << 32) | (uint32_t)(row0 + j);
@@ -2277,11 +2566,18 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
             e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (e->packed) {
-        k_fold<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+        // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
+        k_fold_wide<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
+        k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
     } else {
-        k_fold<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+        k_fold_wide<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
+        k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
             e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
     }
@@ -2444,10 +2740,10 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     } else if (hipGetDevice(&e->device) != hipSuccess) {
         return bail(TBE_EDEVICE);
     }
+    e->pipeline = c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_NO_PIPELINE) == 0;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
     e->own_stream = true;
-    e->pipeline = c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_NO_PIPELINE) == 0;
     if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
     for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ws[0].done, &e->ws[1].done})
