@@ -17,6 +17,7 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
+    "no_nt": (["TBE_NO_NT"], []),
     "zipf": ([], ["--workload", "zipf", "--zipf-batches", "1"]),
 }
 
