@@ -305,12 +305,15 @@ def pmc_traffic(stage: str, workload: str = "uniform"):
         return None
     if workload == "uniform":
         return d.get(stage, {}).get("hbm_bytes_per_launch")
-    prefix = {"fold": "k_fold<", "scatter": "k_scatter_rec<", "hist": "k_hist<",
-              "unscatter": "k_unscatter<"}.get(stage)
+    prefixes = {"fold": ("k_fold<", "k_fold_wide<"), "scatter": ("k_scatter_rec<",),
+                "hist": ("k_hist<",), "unscatter": ("k_unscatter<",)}.get(stage, ())
     kern = d.get("workloads", {}).get(workload, {})
     v = [k["hbm_bytes_per_launch"] for name, k in kern.items()
-         if prefix and name.startswith(prefix) and "hbm_bytes_per_launch" in k]
-    return round(sum(v) / len(v), 1) if v else None
+         if name.startswith(prefixes) and "hbm_bytes_per_launch" in k]
+    if not v:
+        return None
+    # the fold stage is two launches (summed); other stages one per pass (averaged)
+    return round(sum(v) if stage == "fold" else sum(v) / len(v), 1)
 
 
 def workload_name(args, n: int) -> str:

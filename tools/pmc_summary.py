@@ -13,7 +13,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE = {"k_hist": "hist", "k_colscan": "colscan", "k_scatter": "scatter", "k_scatter_rec": "scatter",
-         "k_bounds": "bounds", "k_fold": "fold", "k_fold_q": "fold", "k_unscatter": "unscatter",
+         "k_bounds": "bounds", "k_fold": "fold", "k_fold_wide": "fold", "k_unscatter": "unscatter",
          "k_drain": "drain", "k_hot_plan": "hot", "k_hot_summary": "hot", "k_hot_chain": "hot",
          "k_hot_replies": "hot", "k_hot_update": "hot"}
 
@@ -55,8 +55,11 @@ def main():
             e = stages.setdefault(st, {"hbm_bytes_per_launch": 0.0, "kernels": []})
             e["kernels"].append(k)
             e["hbm_bytes_per_launch"] += d["hbm_bytes_per_launch"]
-    for st, e in stages.items():   # average over the kernels (passes) that make up a stage
-        e["hbm_bytes_per_launch"] /= len(e["kernels"])
+    for st, e in stages.items():
+        # the fold is two launches per batch (k_fold_wide: full buckets, k_fold: the rest),
+        # summed; other stages are one kernel per pass, averaged over the passes
+        if st != "fold":
+            e["hbm_bytes_per_launch"] /= len(e["kernels"])
     if "--write" in sys.argv:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
             json.dump({"note": "per-launch medians; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
