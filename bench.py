@@ -34,6 +34,7 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED_B = 0x5EED000B
 SEED_C = 0x5EED000C
+SEED_A = 0x5EED0001
 T0_US = 1_760_000_000_000_000
 
 
@@ -42,15 +43,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("uniform", "zipf", "queue", "approx"), default="uniform",
+    ap.add_argument("--workload", choices=("uniform", "zipf", "queue", "approx", "testapp"),
+                    default="uniform",
                     help="uniform: config B (the headline); zipf: config C's per-GPU slice; "
-                         "queue: config D (TokenBucketWithQueue); approx: config E (two-tier)")
+                         "queue: config D (TokenBucketWithQueue); approx: config E (two-tier); "
+                         "testapp: config A (the TestApp limiter: 10k keys, 1M requests per 2 s)")
     ap.add_argument("--keys", type=int, default=None,
                     help="total keys (uniform, default 1e8) / keys per GPU (zipf, default 1.25e8)")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     ap.add_argument("--zipf-batches", type=int, default=2,
                     help="distinct Zipf key batches drawn on the host, reused in turn")
-    ap.add_argument("--batch", type=int, default=1 << 26)
+    ap.add_argument("--batch", type=int, default=None, help="requests per batch (default 2^26; testapp 1M)")
     ap.add_argument("--interval-us", type=int, default=None,
                     help="injected time per batch (default 10 ms; 1 ms for queue)")
     ap.add_argument("--token-limit", type=int, default=None,
@@ -70,10 +73,15 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     args = ap.parse_args()
+    testapp = args.workload == "testapp"
+    if args.batch is None:
+        args.batch = 1_000_000 if testapp else 1 << 26
     if args.interval_us is None:
-        args.interval_us = 1_000 if args.workload == "queue" else 10_000
+        args.interval_us = {"queue": 1_000, "testapp": 2_000_000}.get(args.workload, 10_000)
     if args.token_limit is None:
-        args.token_limit = {"queue": 4, "approx": 100}.get(args.workload, 10)
+        args.token_limit = {"queue": 4, "approx": 100, "testapp": 20}.get(args.workload, 10)
+    if testapp and args.tokens_per_period == 1:
+        args.tokens_per_period = 10    # TokenLimit 20, 10 / s
     if args.period_ticks is None:
         args.period_ticks = args.interval_us * 10 if args.workload == "approx" else 10_000_000
     if args.workload == "approx" and args.tokens_per_period == 1:
@@ -118,7 +126,7 @@ def main():
         keys_local = args.keys or 125_000_000
         keys_total = keys_local * world
     else:
-        keys_total = args.keys or 100_000_000
+        keys_total = args.keys or (10_000 if args.workload == "testapp" else 100_000_000)
         keys_local = (keys_total + world - 1) // world
     n = args.batch
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
@@ -128,7 +136,7 @@ def main():
                             pipeline=not args.no_pipeline)
     layout = eng.layout()
     total_steps = args.warmup + args.steps
-    seed = (SEED_C if args.workload == "zipf" else SEED_B) + 7919 * rank
+    seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B) + 7919 * rank
     zkeys = []
     if args.workload == "zipf":
         from distributedratelimiting.redis_amd import workloads
@@ -229,9 +237,26 @@ def main():
                 stages_overlapped.get(name, 0.0) / (args.steps * launches[name]), 4)
             roofline["replay_replies_identical"] = replay_check
 
+    # config A is the reference's own per-request deployment: also time the host-buffer
+    # entry point (the P/Invoke path: copy in, decide, copy out, synchronise) on the same
+    # batches, after the timed region.  Reported beside `value`, never as it.
+    host_rate = None
+    if args.workload == "testapp":
+        host = [tuple(x.cpu().numpy() for x in b) for b in bufs[args.warmup:]]
+        hb = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period, args.period_ticks,
+                               device=dev.index, max_batch=n)
+        for k, p, t in host[:1]:
+            hb.acquire_batch(k.view(np.uint64), p, t)
+        t1 = time.perf_counter()
+        for k, p, t in host[1:]:
+            hb.acquire_batch(k.view(np.uint64), p, t)
+        host_rate = round(n * (len(host) - 1) / (time.perf_counter() - t1), 1) if len(host) > 1 else None
+        hb.close()
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, keys_local, [zk for zk, _ in zkeys])
+        cpu = cpu_baseline(args, keys_local, [zk for zk, _ in zkeys],
+                           SEED_A if args.workload == "testapp" else SEED_B)
 
     if rank == 0:
         line = {
@@ -256,6 +281,7 @@ def main():
                        "partitioning": f"key-hash x{world}, no data-path collective",
                        "layout": layout},
             "grant_rate_last_batch": round(grant_rate, 4),
+            **({"host_buffer_decisions_per_s": host_rate} if host_rate is not None else {}),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}
@@ -317,13 +343,16 @@ def pmc_traffic(stage: str, workload: str = "uniform"):
 
 
 def workload_name(args, n: int) -> str:
+    if args.workload == "testapp":
+        return (f"TestApp TokenBucket limiter (TokenLimit {args.token_limit}, {args.tokens_per_period}/s), "
+                f"{n}-request batches spanning {args.interval_us / 1e6:g} s each (config A)")
     if args.workload == "zipf":
         return (f"TokenBucket Zipf({args.zipf_s}) over each GPU's keys, 2^{n.bit_length() - 1}-request "
                 "batches (config C per-GPU slice)")
     return f"TokenBucket uniform keys, 2^{n.bit_length() - 1}-request batches (config B)"
 
 
-def cpu_baseline(args, n_keys: int, zkeys=()):
+def cpu_baseline(args, n_keys: int, zkeys=(), seed_b: int = SEED_B):
     """The C restatement of the reference script (oracle/tb_ref.c, serial like Redis'
     single script thread) timed on the same trace: the first `sample` requests of each
     batch, batches in order, until ~args.cpu_seconds of CPU work."""
@@ -332,7 +361,7 @@ def cpu_baseline(args, n_keys: int, zkeys=()):
 
     ref = cref.CTokenBucket(n_keys, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks))
     sample = min(args.batch, 1 << 22)
-    seed = SEED_C if zkeys else SEED_B
+    seed = SEED_C if zkeys else seed_b
     done, spent, b = 0, 0.0, 0
     while spent < args.cpu_seconds and b < 64:
         k, p, t = cref.gen_batch(seed, n_keys, b, args.batch, args.interval_us)
@@ -345,7 +374,7 @@ def cpu_baseline(args, n_keys: int, zkeys=()):
         done += sample
         b += 1
     ref.close()
-    what = "config-C (Zipf)" if zkeys else "config-B"
+    what = "config-C (Zipf)" if zkeys else ("config-A (TestApp)" if seed_b == SEED_A else "config-B")
     return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} requests of each of {b} {what} batches "
                       f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
