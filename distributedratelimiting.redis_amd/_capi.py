@@ -31,7 +31,8 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_wait_batch", "tbe_queue_attempt_batch", "tbe_evicted", "tbe_refresh", "tbe_refresh_log", "tbe_queue_of",
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
             "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
-            "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device")
+            "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device",
+            "tbe_import_state")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -130,6 +131,8 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_approx_acquire_batch_device.restype = c_int32
     lib.tbe_approx_acquire_batch_device.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int32,
                                                     c_int64, c_void_p, c_void_p, c_void_p]
+    lib.tbe_import_state.restype = c_int32
+    lib.tbe_import_state.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]
     lib.tbe_layout.restype = c_int32
     lib.tbe_layout.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     lib.tbe_stage_times.restype = c_int32

@@ -2991,6 +2991,25 @@ static tbe_status status_batch_device(tbe_engine *e, const uint64_t *d_keys, con
     return TBE_OK;
 }
 
+tbe_status tbe_import_state(tbe_engine *e, uint64_t first, uint64_t count, const double *v,
+                            const int64_t *t_us) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind == TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not a token-bucket engine");
+    if (first > e->cfg.n_keys || count > e->cfg.n_keys - first)
+        return fail(e, TBE_EINVAL, "range out of bounds");
+    if (count == 0) return TBE_OK;
+    if (!v || !t_us) return fail(e, TBE_EINVAL, "null buffer");
+    std::vector<Slot> tmp(count);
+    for (uint64_t i = 0; i < count; ++i) {
+        if (t_us[i] != kAbsent && t_us[i] < 0) return fail(e, TBE_EINVAL, "t_us < 0");
+        tmp[i] = t_us[i] == kAbsent ? Slot{e->params.cap, kAbsent} : Slot{v[i], t_us[i]};
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());   // after every enqueued batch, whatever its stream
+    HIP_TRY(e, hipMemcpy(e->table + first, tmp.data(), count * sizeof(Slot), hipMemcpyHostToDevice));
+    return TBE_OK;
+}
+
 static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                                const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                                int32_t *remaining, uint64_t *n_evicted);

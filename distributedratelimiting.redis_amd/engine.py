@@ -123,6 +123,15 @@ class TokenBucketEngine:
                                                t.ctypes.data))
         return v, t
 
+    def import_state(self, v, t_us, first: int = 0) -> None:
+        """Restore rows [first, first + len) from an export_state snapshot (tbe_import_state)."""
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        t_us = np.ascontiguousarray(t_us, dtype=np.int64)
+        if v.shape != t_us.shape:
+            raise ValueError("v and t_us must have the same length")
+        self._check(self._lib.tbe_import_state(self.handle, first, v.shape[0], v.ctypes.data,
+                                               t_us.ctypes.data))
+
     def layout(self) -> dict:
         """{passes, r_bits, packed, hot, pipeline, narrow} of this engine's batch pipeline (tbe_layout)."""
         a, b, c = c_uint32(), c_uint32(), c_uint32()

@@ -135,6 +135,14 @@ tbe_status tbe_query(tbe_engine *engine, uint64_t key, int64_t ts_us, double *v,
 tbe_status tbe_export_state(tbe_engine *engine, uint64_t first, uint64_t count, double *v,
                             int64_t *t_us);
 
+/* Restore of an exported range (snapshot/restore of the bucket hashes, the state Redis
+ * persists; the in-process queues of the queueing kind are not part of it, as they are
+ * not in the reference): keys [first, first + count) take {v[k], t_us[k]}; t_us =
+ * INT64_MIN makes the key absent.  Token-bucket and queueing kinds.  t_us must be
+ * INT64_MIN or >= 0; ordered after every batch enqueued before the call. */
+tbe_status tbe_import_state(tbe_engine *engine, uint64_t first, uint64_t count, const double *v,
+                            const int64_t *t_us);
+
 /* ---------------------------------------------------------------- TokenBucketWithQueue
  * Engines created with kind = TBE_KIND_QUEUEING.  The reference limiter
  * (TokenBucketWithQueue/RedisTokenBucketRateLimiter.cs, "Q") is commented out and does

@@ -346,3 +346,28 @@ def test_reply_width(engine_lib, gpu, narrow, cap):
         g, r = run_and_compare(eng, ref, k, p, t)
     assert r.max() == cap or r.max() >= cap - 3
     assert_same_state(eng, ref)
+
+
+def test_snapshot_restore(engine_lib, gpu):
+    """Snapshot/restore of the bucket hashes (tbe_export_state -> tbe_import_state into a
+    fresh engine): the restored engine continues the trace exactly like the original and
+    the oracle, including absent keys and a partial-range restore."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, TbeError
+    n_keys, n = 50_000, 200_000
+    eng, ref = make_pair(n_keys, 10, 3, 10_000_000)
+    for b in range(2):
+        k, p, t = trace.make_batch(0x5EED0009, n_keys, b, n, 700_000, 1, 3)
+        run_and_compare(eng, ref, k, p, t)
+    v, t_us = eng.export_state()
+    assert (t_us == ABSENT).any() and (t_us != ABSENT).any()
+    fresh = TokenBucketEngine(n_keys, 10, 3, 10_000_000, device=0)
+    fresh.import_state(v[:1000], t_us[:1000])                  # two ranges
+    fresh.import_state(v[1000:], t_us[1000:], first=1000)
+    for b in range(2, 4):
+        k, p, t = trace.make_batch(0x5EED0009, n_keys, b, n, 700_000, 1, 3)
+        g1, r1 = run_and_compare(eng, ref, k, p, t)
+        g2, r2 = fresh.acquire_batch(k, p, t)
+        assert np.array_equal(g1, g2) and np.array_equal(r1, r2)
+    assert_same_state(fresh, ref)
+    with pytest.raises(TbeError):
+        fresh.import_state(v[:10], t_us[:10], first=n_keys - 5)
