@@ -1,0 +1,50 @@
+"""bench.py's workload table and its algorithmic-byte model,
+checked without a GPU."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse(argv):
+    sys.path.insert(0, ROOT)
+    import bench
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+@pytest.mark.parametrize("workload,batch,interval,limit,tokens", [
+    ("uniform", 1 << 26, 10_000, 10, 1),       # config B
+    ("zipf", 1 << 26, 10_000, 10, 1),          # config C (per-GPU slice)
+    ("queue", 1 << 26, 1_000, 4, 1),           # config D
+    ("approx", 1 << 26, 10_000, 100, 10),      # config E
+    ("testapp", 1_000_000, 2_000_000, 20, 10),  # config A
+])
+def test_workload_defaults(workload, batch, interval, limit, tokens):
+    a = parse(["--workload", workload])
+    assert (a.batch, a.interval_us, a.token_limit, a.tokens_per_period) == (batch, interval, limit, tokens)
+    assert a.gpus == 1 and a.steps > 0 and a.warmup >= 0
+
+
+def test_explicit_flags_win():
+    a = parse(["--workload", "testapp", "--batch", "4096", "--token-limit", "7"])
+    assert (a.batch, a.token_limit) == (4096, 7)
+
+
+def test_algorithmic_bytes_model():
+    sys.path.insert(0, ROOT)
+    import bench
+    n, k = 1 << 26, 100_000_000
+    fold4 = bench.algorithmic_bytes("fold", n, k, 2, True, None, 4)
+    fold1 = bench.algorithmic_bytes("fold", n, k, 2, True, None, 1)
+    assert fold4 - fold1 == 3 * n                      # reply width
+    u = k * (1 - pow(2.718281828459045, -n / k))
+    assert abs(fold1 - (n * 9 + u * 32)) < n            # records 8 + reply 1, rows 32 per key
+    # the decision's own minimum is <= 48.3 B per request at config B
+    assert (n * 25 + u * 32) / n < 48.4
