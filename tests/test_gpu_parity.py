@@ -371,3 +371,20 @@ def test_snapshot_restore(engine_lib, gpu):
     assert_same_state(fresh, ref)
     with pytest.raises(TbeError):
         fresh.import_state(v[:10], t_us[:10], first=n_keys - 5)
+
+
+def test_hot_key_cools_down(engine_lib, gpu):
+    """A key hot for a few batches (its row written by the hot-key chain with ordinary
+    stores) then cold again (its row read back by the fold's streaming slice loads): the
+    fold must see the chain's last write."""
+    n_keys, n, hot_key = 100_000, 200_000, 4242
+    eng, ref = make_pair(n_keys, 50, 5000, 10_000_000)
+    rng = np.random.default_rng(11)
+    for b in range(8):
+        k = rng.integers(0, n_keys, n).astype(np.uint64)
+        m = 5000 if b < 3 else 10
+        k[rng.choice(n, m, replace=False)] = hot_key
+        p = rng.integers(1, 4, n).astype(np.int32)
+        t = trace.batch_timestamps(b, n, 10_000)
+        run_and_compare(eng, ref, k, p, t)
+        assert_same_state(eng, ref)
