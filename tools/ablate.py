@@ -17,7 +17,7 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "no_nt": (["TBE_NO_NT"], []),
+    "slice_load_cached": (["TBE_SLICE_LOAD_CACHED"], []),
     "zipf": ([], ["--workload", "zipf", "--zipf-batches", "1"]),
 }
 
