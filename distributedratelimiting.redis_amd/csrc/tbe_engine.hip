@@ -3393,6 +3393,119 @@ tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_
     return TBE_OK;
 }
 
+// CancelQueueState.TrySetCanceled (Q:480-506, A:531-557) for cancels grouped into runs of
+// one key (the host sorts them stably by key): one thread per run applies its cancels in
+// call order.  A found entry leaves the ring at once, the later entries close up behind
+// it (order kept), count -1 and qsum (_queueCount) -= its permits.  The reference instead
+// leaves a canceled registration in its deque until the drain reaches it, where it
+// consumes tokens and A:489 adds its count back a second time; a
+// bounded ring cannot hold entries that no longer count against QueueLimit.
+__global__ __launch_bounds__(256) void k_cancel(
+    const uint64_t *__restrict__ ckeys, const int64_t *__restrict__ cids,
+    const uint32_t *__restrict__ run_start, uint32_t n_runs, int32_t approx,
+    uint64_t *__restrict__ qhdr, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring,
+    uint32_t cap, uint8_t *__restrict__ hit) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_runs) return;
+    const uint32_t c0 = run_start[r], c1 = run_start[r + 1];
+    const uint64_t key = ckeys[c0];
+    uint32_t head, cnt;
+    int64_t qsum;
+    ALocal a{};
+    if (approx) {
+        a = alocal[key];
+        head = a.hc & 0xFFFFu;
+        cnt = a.hc >> 16;
+        qsum = a.qsum;
+    } else {
+        const uint64_t h = qhdr[key];
+        head = (uint32_t)(h & 0xFFFFu);
+        cnt = (uint32_t)((h >> 16) & 0xFFFFu);
+        qsum = (int64_t)(h >> 32);
+    }
+    uint64_t *__restrict__ kr = ring + key * (uint64_t)cap;
+    bool changed = false;
+    for (uint32_t c = c0; c < c1; ++c) {
+        const int64_t id = cids[c];
+        uint32_t j = 0;
+        if (id < 0) j = cnt;   // never a request id: not queued
+        while (j < cnt && (int64_t)(kr[(head + j) % cap] >> 16) != id) ++j;
+        if (j == cnt) {
+            hit[c] = 0;
+            continue;
+        }
+        qsum -= (int64_t)(kr[(head + j) % cap] & 0xFFFFu);
+        for (; j + 1 < cnt; ++j) kr[(head + j) % cap] = kr[(head + j + 1) % cap];
+        --cnt;
+        hit[c] = 1;
+        changed = true;
+    }
+    if (!changed) return;
+    if (approx) {
+        a.qsum = (int32_t)qsum;
+        a.hc = (head & 0xFFFFu) | (cnt << 16);
+        alocal[key] = a;
+    } else {
+        qhdr[key] = qh_pack(head, cnt, qsum);
+    }
+}
+
+tbe_status tbe_queue_cancel(tbe_engine *e, const uint64_t *keys, const int64_t *request_ids,
+                            uint64_t n, uint8_t *cancelled, uint64_t *n_cancelled) {
+    if (!e || !n_cancelled) return TBE_EINVAL;
+    *n_cancelled = 0;
+    if (e->cfg.kind == TBE_KIND_TOKEN_BUCKET) return fail(e, TBE_EINVAL, "engine has no queues");
+    if (n == 0) return TBE_OK;
+    if (!keys || !request_ids || !cancelled) return fail(e, TBE_EINVAL, "null buffer");
+    if (n >= (1ull << 31)) return fail(e, TBE_EINVAL, "batch too large");
+    for (uint64_t i = 0; i < n; ++i)
+        if (keys[i] >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
+    std::vector<uint32_t> ord(n);
+    for (uint32_t i = 0; i < (uint32_t)n; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return keys[x] < keys[y]; });
+    std::vector<uint64_t> ck(n);
+    std::vector<int64_t> ci(n);
+    std::vector<uint32_t> runs;
+    for (uint64_t c = 0; c < n; ++c) {
+        ck[c] = keys[ord[c]];
+        ci[c] = request_ids[ord[c]];
+        if (c == 0 || ck[c] != ck[c - 1]) runs.push_back((uint32_t)c);
+    }
+    const uint32_t n_runs = (uint32_t)runs.size();
+    runs.push_back((uint32_t)n);
+    // one scratch allocation: keys | ids | run starts | hits
+    const size_t off_ids = n * sizeof(uint64_t), off_runs = off_ids + n * sizeof(int64_t);
+    const size_t off_hit = off_runs + runs.size() * sizeof(uint32_t), bytes = off_hit + n;
+    struct Scratch {
+        char *p = nullptr;
+        ~Scratch() { dfree(p); }
+    } s;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());   // after every enqueued batch, whatever its stream
+    HIP_TRY(e, hipMalloc(&s.p, bytes));
+    HIP_TRY(e, hipMemcpy(s.p, ck.data(), off_ids, hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(s.p + off_ids, ci.data(), n * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(s.p + off_runs, runs.data(), runs.size() * sizeof(uint32_t),
+                         hipMemcpyHostToDevice));
+    const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
+    const uint32_t rcap = approx ? e->ap.cap : e->qp.cap;
+    k_cancel<<<(n_runs + 255) / 256, 256, 0, e->stream>>>(
+        (const uint64_t *)s.p, (const int64_t *)(s.p + off_ids), (const uint32_t *)(s.p + off_runs),
+        n_runs, approx ? 1 : 0, e->qhdr, e->alocal, e->ring, rcap, (uint8_t *)(s.p + off_hit));
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    std::vector<uint8_t> hit(n);
+    HIP_TRY(e, hipMemcpy(hit.data(), s.p + off_hit, n, hipMemcpyDeviceToHost));
+    uint64_t m = 0;
+    for (uint64_t c = 0; c < n; ++c) {
+        cancelled[ord[c]] = hit[c];
+        m += hit[c];
+    }
+    e->queued_total -= std::min(e->queued_total, m);
+    *n_cancelled = m;
+    return TBE_OK;
+}
+
 tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, uint32_t *packed) {
     if (!e || !passes || !r_bits || !packed) return TBE_EINVAL;
     *passes = (uint32_t)e->passes;

@@ -252,6 +252,20 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
         c = min(cnt.value, cap)
         return list(zip(ids[:c].tolist(), ps[:c].tolist()))
 
+    def cancel(self, keys, request_ids):
+        """Cancel queued requests (CancelQueueState.TrySetCanceled, Q:480-506 / A:531-557;
+        tbe_queue_cancel); returns u8[n], 1 where the request was queued and is removed."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        request_ids = np.ascontiguousarray(request_ids, dtype=np.int64)
+        n = keys.shape[0]
+        if request_ids.shape[0] != n:
+            raise ValueError("keys and request_ids differ in length")
+        out = np.empty(n, dtype=np.uint8)
+        m = ctypes.c_uint64()
+        self._check(self._lib.tbe_queue_cancel(self.handle, keys.ctypes.data, request_ids.ctypes.data,
+                                               n, out.ctypes.data, byref(m)))
+        return out
+
 
 class ApproximateEngine(QueueingTokenBucketEngine):
     """ApproximateTokenBucket (ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs, A):

@@ -214,6 +214,20 @@ tbe_status tbe_refresh_device(tbe_engine *engine, int64_t ts_us, uint64_t *d_key
 tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, int32_t *permits,
                         uint32_t capacity, uint32_t *count);
 
+/* Cancellation of queued requests (the CancellationToken registration of a queued
+ * WaitAsync: CancelQueueState.TrySetCanceled, Q:480-506 / A:531-557), queueing and
+ * approximate kinds.  Cancels are applied in call order; cancelled[i] = 1 when
+ * request_ids[i] was queued on keys[i] and is now removed: _queueCount (qsum) drops by its
+ * permits and the entries behind it keep their order.  0 when it is not queued there
+ * (already granted, evicted, failed or canceled: TrySetCanceled returns false).  Decision
+ * (DESIGN.md §2b): the entry leaves the queue at once, so the drain neither grants it nor
+ * waits on it; the reference leaves it in its deque until the drain dequeues it, which
+ * consumes its tokens and, in A:489, adds them back twice.
+ * Ordered after every batch enqueued before the call; synchronous.  *n_cancelled gets
+ * the number of 1s.  key >= n_keys: TBE_EINVAL, nothing canceled. */
+tbe_status tbe_queue_cancel(tbe_engine *engine, const uint64_t *keys, const int64_t *request_ids,
+                            uint64_t n, uint8_t *cancelled, uint64_t *n_cancelled);
+
 /* ---------------------------------------------------------------- ApproximateTokenBucket
  * Engines created with kind = TBE_KIND_APPROXIMATE hold ONE client's local tier for every
  * key (ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs, "A") plus a

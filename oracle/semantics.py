@@ -340,6 +340,19 @@ class QueueingTokenBucketTable:
     def queue_of(self, key: int) -> List[Tuple[int, int]]:
         return [(e.request_id, e.permits) for e in self.queues.get(key, [])]
 
+    def cancel(self, key: int, request_id: int) -> bool:
+        """CancelQueueState.TrySetCanceled (Q:480-506): True iff the request was queued on
+        `key`; _queueCount -= its permits (Q:499).  Build decision: the
+        registration leaves the deque at once instead of waiting for the drain (Q:256-262),
+        so it neither consumes tokens nor holds up the entries behind it."""
+        q = self.queues.get(key, [])
+        for j, e in enumerate(q):
+            if e.request_id == request_id:
+                del q[j]
+                self.qsum[key] -= e.permits
+                return True
+        return False
+
 
 # ---------------------------------------------------------------- approximate: local tier
 # ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs ("A") as one client's
@@ -457,6 +470,20 @@ class ApproxClient:
         s.queue.append(QueueEntry(request_id, p))
         s.qcount += p
         return AP_QUEUED, evicted
+
+    def cancel(self, key: int, request_id: int) -> bool:
+        """CancelQueueState.TrySetCanceled (A:545-556): True iff the request was queued on
+        `key`; _queueCount -= its permits.  Removed at once, so the drain
+        never reaches it and the A:489 double add-back cannot happen."""
+        s = self.keys.get(key)
+        if s is None:
+            return False
+        for j, e in enumerate(s.queue):
+            if e.request_id == request_id:
+                del s.queue[j]
+                s.qcount -= e.permits
+                return True
+        return False
 
     def collect(self) -> Dict[int, int]:
         """A:430-435: swap every key's local score to 0; returns the counts."""

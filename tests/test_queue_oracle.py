@@ -62,3 +62,28 @@ def test_python_vs_c(oracle_lib, order, qlimit):
         assert list(zip(lk.tolist(), lid.tolist(), lrem.tolist())) == py.refresh(t_refresh)
     for k in range(n_keys):
         assert c.queue_of(k) == py.queue_of(k)
+
+
+def test_cancel_hand_case():
+    """CancelQueueState.TrySetCanceled (Q:480-506): qsum drops at once, the entry leaves
+    the queue, a second cancel or a cancel of a finished request fails."""
+    q = QueueingTokenBucketTable(TokenBucketConfig(4, 1.0), 3, OLDEST_FIRST)
+    out = [q.acquire(1, p, S_US, i) for i, p in enumerate([4, 1, 2, 1])]
+    assert [o[0] for o in out] == [ST_GRANTED, ST_QUEUED, ST_QUEUED, ST_FAILED]
+    assert q.cancel(1, 1) and not q.cancel(1, 1) and not q.cancel(1, 0) and not q.cancel(2, 2)
+    assert q.queue_of(1) == [(2, 2)] and q.qsum[1] == 2
+    assert q.acquire(1, 1, S_US, 4)[0] == ST_QUEUED      # room freed by the cancel
+    # the canceled head neither consumes tokens nor blocks: 2 s refill 2 tokens -> id 2 first
+    assert q.refresh(S_US + 2_000_000) == [(1, 2, 0)]
+    assert q.queue_of(1) == [(4, 1)]
+
+
+def test_approx_cancel_hand_case():
+    from oracle.semantics import AP_GRANTED, AP_QUEUED, ApproxClient
+    c = ApproxClient(4, 4, 10_000_000, 4, OLDEST_FIRST)
+    assert [c.wait(7, p, i)[0] for i, p in enumerate([4, 2, 2])] == [AP_GRANTED, AP_QUEUED, AP_QUEUED]
+    assert c.cancel(7, 1) and not c.cancel(7, 1) and not c.cancel(8, 2)
+    s = c.st(7)
+    assert s.qcount == 2 and [e.request_id for e in s.queue] == [2]
+    # the count is not added back to the local score (the A:489 double count)
+    assert s.local == 4
