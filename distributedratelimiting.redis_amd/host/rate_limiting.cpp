@@ -90,9 +90,38 @@ RateLimitLease RateLimiter::AttemptAcquire(int permitCount) {
     return AttemptAcquireCore(permitCount);
 }
 
-std::future<RateLimitLease> RateLimiter::AcquireAsync(int permitCount) {
+std::future<RateLimitLease> RateLimiter::AcquireAsync(int permitCount, CancellationToken ct) {
     if (permitCount < 0) throw ArgumentOutOfRangeException("permitCount must be >= 0", "permitCount");
-    return AcquireAsyncCore(permitCount);
+    return AcquireAsyncCore(permitCount, ct);
+}
+
+bool CancellationToken::IsCancellationRequested() const {
+    if (!s_) return false;
+    std::lock_guard<std::mutex> g(s_->mu);
+    return s_->canceled;
+}
+
+void CancellationToken::Register(std::function<void()> fn) const {
+    if (!s_) return;
+    {
+        std::lock_guard<std::mutex> g(s_->mu);
+        if (!s_->canceled) {
+            s_->callbacks.push_back(std::move(fn));
+            return;
+        }
+    }
+    fn();  // already canceled: run at once, as CancellationToken.Register does
+}
+
+void CancellationTokenSource::Cancel() {
+    std::vector<std::function<void()>> fns;
+    {
+        std::lock_guard<std::mutex> g(s_->mu);
+        if (s_->canceled) return;
+        s_->canceled = true;
+        fns.swap(s_->callbacks);
+    }
+    for (auto &f : fns) f();
 }
 
 // ------------------------------------------------------------------ the core
@@ -130,6 +159,7 @@ public:
         const tbe_status st = tbe_create(&c, &eng_);
         if (st == TBE_EINVAL) throw ArgumentException(std::string("invalid limiter options: ") + tbe_last_error(nullptr), "options");
         if (st != TBE_OK) throw RateLimiterEngineException(st, std::string("tbe_create failed: ") + tbe_last_error(nullptr));
+        inbox_->core = this;
         submitter_ = std::thread([this] { Loop(); });
         if (kind != TBE_KIND_TOKEN_BUCKET && o.AutoReplenishment && o.ReplenishmentPeriod.ticks > 0)
             timer_ = std::thread([this] { TimerLoop(); });
@@ -164,11 +194,13 @@ public:
         if (disposed_.load()) throw ObjectDisposedException(type_name_);
     }
 
-    std::future<RateLimitLease> Submit(uint64_t key, int32_t permits, int mode) {
+    std::future<RateLimitLease> Submit(uint64_t key, int32_t permits, int mode,
+                                       const CancellationToken &ct = {}) {
         Req r;
         r.key = key;
         r.permits = permits;
         r.mode = mode;
+        r.ct = ct;
         std::future<RateLimitLease> f = r.done.get_future();
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -265,6 +297,10 @@ public:
             std::lock_guard<std::mutex> g(mu_);
             if (disposed_.exchange(true)) return;
         }
+        {  // later cancellations find nothing to cancel: dispose fails the queue below
+            std::lock_guard<std::mutex> g(inbox_->mu);
+            inbox_->closed = true;
+        }
         {
             std::lock_guard<std::mutex> g(timer_mu_);
             timer_stop_ = true;
@@ -291,11 +327,62 @@ private:
         int32_t permits = 0;
         int64_t ts = 0;
         int mode = 0;
+        CancellationToken ct;
         std::promise<RateLimitLease> done;
     };
     struct Cmd {
         std::function<void()> fn;
     };
+    // Cancellations of queued requests (CancelQueueState.TrySetCanceled, Q:480-506,
+    // A:531-557) arrive on whatever thread cancels the token; they wait here for the
+    // submitter, which applies them with one tbe_queue_cancel call before its next batch.
+    // Token callbacks hold the inbox, not the core, so they outlive a disposed limiter.
+    struct CancelInbox {
+        std::mutex mu;
+        bool closed = false;
+        LimiterCore *core = nullptr;
+        std::vector<std::pair<uint64_t, int64_t>> pending;  // (key, request id)
+        void Post(uint64_t key, int64_t id) {
+            std::lock_guard<std::mutex> g(mu);
+            if (closed) return;
+            pending.emplace_back(key, id);
+            core->WakeForCancel();
+        }
+    };
+
+    void WakeForCancel() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            cancel_wake_ = true;
+        }
+        cv_.notify_one();
+    }
+
+    void FlushCancels() {  // submitter thread
+        std::vector<std::pair<uint64_t, int64_t>> list;
+        {
+            std::lock_guard<std::mutex> g(inbox_->mu);
+            list.swap(inbox_->pending);
+        }
+        if (list.empty()) return;
+        const uint64_t n = list.size();
+        std::vector<uint64_t> keys(n);
+        std::vector<int64_t> ids(n);
+        std::vector<uint8_t> hit(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            keys[i] = list[i].first;
+            ids[i] = list[i].second;
+        }
+        uint64_t m = 0;
+        if (tbe_queue_cancel(eng_, keys.data(), ids.data(), n, hit.data(), &m) != TBE_OK) return;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (!hit[i]) continue;  // already completed: TrySetCanceled returns false
+            auto it = waiting_.find(ids[i]);
+            if (it == waiting_.end()) continue;
+            it->second.set_exception(std::make_exception_ptr(OperationCanceledException()));
+            waiting_.erase(it);
+        }
+    }
 
     static int64_t SteadyNs() {
         return std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -319,7 +406,13 @@ private:
         std::vector<Req> batch;
         for (;;) {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return !q_.empty() || stop_; });
+            cv_.wait(lk, [&] { return !q_.empty() || stop_ || cancel_wake_; });
+            if (cancel_wake_) {
+                cancel_wake_ = false;
+                lk.unlock();
+                FlushCancels();
+                continue;
+            }
             if (q_.empty()) break;  // stop_ and drained
             if (auto *c = std::get_if<Cmd>(&q_.front())) {
                 std::function<void()> fn = std::move(c->fn);
@@ -333,8 +426,13 @@ private:
             while (!q_.empty() && batch.size() < opt_.MaxBatch) {
                 Req *r = std::get_if<Req>(&q_.front());
                 if (!r || r->mode != mode) break;
+                const bool precanceled = r->ct.IsCancellationRequested();
                 batch.push_back(std::move(*r));
                 q_.pop_front();
+                // A token canceled before the call cancels the request as soon as it queues
+                // (Register runs the callback at once, A:169-175): end the batch here so the
+                // cancel lands before the next request of the key is decided.
+                if (precanceled && mode != kTbAcquire) break;
             }
             lk.unlock();
             try {
@@ -402,7 +500,13 @@ private:
                 if (mode == kApproxWait || mode == kApproxAttempt) idle_since_ns_.store(-1);  // A:204
                 r.done.set_value(RateLimitLease(true));
             } else if (s == TBE_WAIT_QUEUED) {
-                waiting_.emplace(id_base + (int64_t)i, std::move(r.done));
+                const int64_t id = id_base + (int64_t)i;
+                waiting_.emplace(id, std::move(r.done));
+                if (r.ct.CanBeCanceled()) {  // A:166-175
+                    std::shared_ptr<CancelInbox> box = inbox_;
+                    const uint64_t key = r.key;
+                    r.ct.Register([box, key, id] { box->Post(key, id); });
+                }
             } else if (mode == kApproxWait || mode == kApproxAttempt) {
                 auto it = approx.find(r.key);
                 if (it == approx.end()) it = approx.emplace(r.key, QueryApprox(r.key)).first;
@@ -459,6 +563,8 @@ private:
     std::condition_variable cv_;
     std::deque<std::variant<Req, Cmd>> q_;
     bool stop_ = false;
+    bool cancel_wake_ = false;  // under mu_
+    std::shared_ptr<CancelInbox> inbox_ = std::make_shared<CancelInbox>();
     std::atomic<bool> disposed_{false};
     std::thread submitter_;
 
@@ -501,7 +607,9 @@ RedisTokenBucketRateLimiter::RedisTokenBucketRateLimiter(const RedisTokenBucketR
 RedisTokenBucketRateLimiter::~RedisTokenBucketRateLimiter() = default;
 int RedisTokenBucketRateLimiter::GetAvailablePermits() { return core_->EstimatedRemaining(); }
 RateLimitLease RedisTokenBucketRateLimiter::AttemptAcquireCore(int p) { return core_->Submit(0, p, kTbAcquire).get(); }
-std::future<RateLimitLease> RedisTokenBucketRateLimiter::AcquireAsyncCore(int p) { return core_->Submit(0, p, kTbAcquire); }
+std::future<RateLimitLease> RedisTokenBucketRateLimiter::AcquireAsyncCore(int p, const CancellationToken &) {
+    return core_->Submit(0, p, kTbAcquire);  // never queues: nothing to cancel (TB:58-82)
+}
 void RedisTokenBucketRateLimiter::DisposeCore() { core_->Dispose(); }
 
 PartitionedRedisTokenBucketRateLimiter::PartitionedRedisTokenBucketRateLimiter(const RedisTokenBucketRateLimiterOptions &o)
@@ -517,7 +625,8 @@ RateLimitLease PartitionedRedisTokenBucketRateLimiter::AttemptAcquireCore(const 
     core_->ThrowIfDisposed();
     return core_->Submit(core_->KeyOf(id), p, kTbAcquire).get();
 }
-std::future<RateLimitLease> PartitionedRedisTokenBucketRateLimiter::AcquireAsyncCore(const std::string &id, int p) {
+std::future<RateLimitLease> PartitionedRedisTokenBucketRateLimiter::AcquireAsyncCore(const std::string &id, int p,
+                                                                                     const CancellationToken &) {
     core_->ThrowIfDisposed();
     return core_->Submit(core_->KeyOf(id), p, kTbAcquire);
 }
@@ -544,9 +653,9 @@ RateLimitLease RedisQueueingTokenBucketRateLimiter::AttemptAcquireCore(int p) {
     check_limit(p, core_->options().TokenLimit);
     return core_->Submit(0, p, kQueueAttempt).get();
 }
-std::future<RateLimitLease> RedisQueueingTokenBucketRateLimiter::AcquireAsyncCore(int p) {
+std::future<RateLimitLease> RedisQueueingTokenBucketRateLimiter::AcquireAsyncCore(int p, const CancellationToken &ct) {
     check_limit(p, core_->options().TokenLimit);
-    return core_->Submit(0, p, kQueueWait);
+    return core_->Submit(0, p, kQueueWait, ct);
 }
 void RedisQueueingTokenBucketRateLimiter::DisposeCore() { core_->Dispose(); }
 
@@ -586,10 +695,10 @@ RateLimitLease RedisApproximateTokenBucketRateLimiter::AttemptAcquireCore(int p)
     check_limit(p, core_->options().TokenLimit);
     return core_->Submit(0, p, kApproxAttempt).get();
 }
-std::future<RateLimitLease> RedisApproximateTokenBucketRateLimiter::AcquireAsyncCore(int p) {
+std::future<RateLimitLease> RedisApproximateTokenBucketRateLimiter::AcquireAsyncCore(int p, const CancellationToken &ct) {
     check_limit(p, core_->options().TokenLimit);
     core_->ThrowIfDisposed();  // A:124
-    return core_->Submit(0, p, kApproxWait);
+    return core_->Submit(0, p, kApproxWait, ct);
 }
 void RedisApproximateTokenBucketRateLimiter::DisposeCore() { core_->Dispose(); }
 

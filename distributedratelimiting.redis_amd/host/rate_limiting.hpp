@@ -72,6 +72,42 @@ struct RateLimiterEngineException : std::runtime_error {
         : std::runtime_error(msg), Status(st) {}
 };
 
+// TaskCanceledException of a canceled queued wait (CancelQueueState.TrySetCanceled,
+// Q:480-506, A:531-557).
+struct OperationCanceledException : std::runtime_error {
+    OperationCanceledException() : std::runtime_error("The operation was canceled.") {}
+};
+
+// System.Threading.CancellationToken / CancellationTokenSource, reduced to what the
+// limiters use: CanBeCanceled, IsCancellationRequested and Register (callbacks run once,
+// on the thread that calls Cancel, or at once when registered after it).
+class CancellationToken {
+public:
+    CancellationToken() = default;  // CancellationToken.None
+    bool CanBeCanceled() const { return (bool)s_; }
+    bool IsCancellationRequested() const;
+    void Register(std::function<void()> fn) const;
+private:
+    friend class CancellationTokenSource;
+    struct State {
+        std::mutex mu;
+        bool canceled = false;
+        std::vector<std::function<void()>> callbacks;
+    };
+    explicit CancellationToken(std::shared_ptr<State> s) : s_(std::move(s)) {}
+    std::shared_ptr<State> s_;
+};
+
+class CancellationTokenSource {
+public:
+    CancellationTokenSource() : s_(std::make_shared<CancellationToken::State>()) {}
+    CancellationToken Token() const { return CancellationToken(s_); }
+    bool IsCancellationRequested() const { return Token().IsCancellationRequested(); }
+    void Cancel();
+private:
+    std::shared_ptr<CancellationToken::State> s_;
+};
+
 enum class QueueProcessingOrder { OldestFirst = 0, NewestFirst = 1 };
 
 // RateLimitLease (the reference's private Lease classes, e.g. A:559-598).  Token-bucket
@@ -145,11 +181,13 @@ public:
     virtual int GetAvailablePermits() = 0;
     // Base-class argument validation: permitCount < 0 -> ArgumentOutOfRangeException.
     RateLimitLease AttemptAcquire(int permitCount = 1);
-    std::future<RateLimitLease> AcquireAsync(int permitCount = 1);
+    // A queued request whose token is canceled completes with OperationCanceledException
+    // (A:166-175); a request decided at once ignores the token, as in the reference.
+    std::future<RateLimitLease> AcquireAsync(int permitCount = 1, CancellationToken ct = {});
     void Dispose() { DisposeCore(); }
 protected:
     virtual RateLimitLease AttemptAcquireCore(int permitCount) = 0;
-    virtual std::future<RateLimitLease> AcquireAsyncCore(int permitCount) = 0;
+    virtual std::future<RateLimitLease> AcquireAsyncCore(int permitCount, const CancellationToken &ct) = 0;
     virtual void DisposeCore() = 0;
 };
 
@@ -162,14 +200,16 @@ public:
         if (permitCount < 0) throw ArgumentOutOfRangeException("permitCount must be >= 0", "permitCount");
         return AttemptAcquireCore(resource, permitCount);
     }
-    std::future<RateLimitLease> AcquireAsync(const TResource &resource, int permitCount = 1) {
+    std::future<RateLimitLease> AcquireAsync(const TResource &resource, int permitCount = 1,
+                                             CancellationToken ct = {}) {
         if (permitCount < 0) throw ArgumentOutOfRangeException("permitCount must be >= 0", "permitCount");
-        return AcquireAsyncCore(resource, permitCount);
+        return AcquireAsyncCore(resource, permitCount, ct);
     }
     void Dispose() { DisposeCore(); }
 protected:
     virtual RateLimitLease AttemptAcquireCore(const TResource &resource, int permitCount) = 0;
-    virtual std::future<RateLimitLease> AcquireAsyncCore(const TResource &resource, int permitCount) = 0;
+    virtual std::future<RateLimitLease> AcquireAsyncCore(const TResource &resource, int permitCount,
+                                                         const CancellationToken &ct) = 0;
     virtual void DisposeCore() = 0;
 };
 
@@ -188,7 +228,7 @@ public:
     int GetAvailablePermits() override;                                               // TB:48-51
 protected:
     RateLimitLease AttemptAcquireCore(int permitCount) override;
-    std::future<RateLimitLease> AcquireAsyncCore(int permitCount) override;          // TB:58-82
+    std::future<RateLimitLease> AcquireAsyncCore(int permitCount, const CancellationToken &ct) override;          // TB:58-82
     void DisposeCore() override;                                                      // TB:85-109
 private:
     std::unique_ptr<detail::LimiterCore> core_;
@@ -204,7 +244,8 @@ public:
     int GetAvailablePermits(const std::string &resourceID) override;
 protected:
     RateLimitLease AttemptAcquireCore(const std::string &resourceID, int permitCount) override;
-    std::future<RateLimitLease> AcquireAsyncCore(const std::string &resourceID, int permitCount) override;
+    std::future<RateLimitLease> AcquireAsyncCore(const std::string &resourceID, int permitCount,
+                                                 const CancellationToken &ct) override;
     void DisposeCore() override;
 private:
     std::unique_ptr<detail::LimiterCore> core_;
@@ -223,7 +264,7 @@ public:
     bool TryReplenish();  // one replenish tick now; false when AutoReplenishment is on
 protected:
     RateLimitLease AttemptAcquireCore(int permitCount) override;
-    std::future<RateLimitLease> AcquireAsyncCore(int permitCount) override;          // Q:67-134
+    std::future<RateLimitLease> AcquireAsyncCore(int permitCount, const CancellationToken &ct) override;          // Q:67-134
     void DisposeCore() override;
 private:
     std::unique_ptr<detail::LimiterCore> core_;
@@ -243,7 +284,7 @@ public:
     std::string ToString();                                                           // A:510-513
 protected:
     RateLimitLease AttemptAcquireCore(int permitCount) override;                     // A:84-113
-    std::future<RateLimitLease> AcquireAsyncCore(int permitCount) override;          // A:116-183
+    std::future<RateLimitLease> AcquireAsyncCore(int permitCount, const CancellationToken &ct) override;          // A:116-183
     void DisposeCore() override;                                                      // A:274-300
 private:
     std::unique_ptr<detail::LimiterCore> core_;

@@ -244,6 +244,73 @@ static void test_queueing_limiter() {
     CHECK(throws<ObjectDisposedException>([&] { lim.AcquireAsync(1); }));
 }
 
+template <class F>
+static bool canceled(F &f) {  // completes with OperationCanceledException within 5 s
+    if (f.wait_for(std::chrono::seconds(5)) != std::future_status::ready) return false;
+    try {
+        f.get();
+    } catch (const OperationCanceledException &) {
+        return true;
+    }
+    return false;
+}
+
+static void test_queueing_cancel() {
+    // CancelQueueState (Q:480-506) with the build's removal-at-once decision:
+    // TokenLimit 2, 1 token/s, QueueLimit 3, OldestFirst, manual replenishment.
+    FakeClock clk;
+    RedisQueueingTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(2, 1, 1.0);
+    o.TimeSource = clk.fn();
+    o.QueueLimit = 3;
+    o.AutoReplenishment = false;
+    RedisQueueingTokenBucketRateLimiter lim(o);
+    CHECK(lim.AcquireAsync(2).get().IsAcquired());
+    CancellationTokenSource c1, c2, c3, c4;
+    auto q1 = lim.AcquireAsync(1, c1.Token());              // queued (qsum 1)
+    auto q2 = lim.AcquireAsync(2, c2.Token());              // queued (qsum 3)
+    c1.Cancel();
+    CHECK(canceled(q1));                                    // qsum 2, q2 is the head now
+    auto q3 = lim.AcquireAsync(1);                          // fits only because of the cancel
+    CHECK(q3.wait_for(std::chrono::milliseconds(50)) == std::future_status::timeout);
+    clk.advance(2000000);
+    CHECK(lim.TryReplenish());                              // 2 tokens: q2 granted, q3 waits
+    CHECK(q2.get().IsAcquired());
+    c2.Cancel();                                            // after completion: no effect
+    c3.Cancel();
+    auto q4 = lim.AcquireAsync(1, c3.Token());              // canceled before the call: queues,
+    auto q5 = lim.AcquireAsync(2);                          // then leaves before q5 is decided
+    CHECK(canceled(q4));
+    CHECK(q5.wait_for(std::chrono::milliseconds(50)) == std::future_status::timeout);  // queued, not failed
+    auto g = lim.AttemptAcquire(0);                         // p = 0 still leases (script, x >= 0)
+    CHECK(g.IsAcquired());
+    auto q6 = lim.AcquireAsync(1, c4.Token());              // queue full (1 + 2): failed at once
+    CHECK(!q6.get().IsAcquired());
+    c4.Cancel();
+    lim.Dispose();                                          // fails q3 and q5
+    CHECK(!q3.get().IsAcquired());
+    CHECK(!q5.get().IsAcquired());
+}
+
+static void test_approximate_cancel() {
+    FakeClock clk;
+    RedisApproximateTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(4, 4, 1.0);
+    o.TimeSource = clk.fn();
+    o.QueueLimit = 5;
+    o.AutoReplenishment = false;
+    RedisApproximateTokenBucketRateLimiter lim(o);
+    CHECK(lim.AttemptAcquire(3).IsAcquired());
+    CancellationTokenSource c;
+    auto q = lim.AcquireAsync(2, c.Token());                // queued (available 1)
+    CHECK(!lim.AttemptAcquire(1).IsAcquired());             // OldestFirst: never leases past the queue
+    c.Cancel();
+    CHECK(canceled(q));
+    CHECK(lim.GetAvailablePermits() == 1);                  // the canceled count is not consumed
+    CHECK(lim.AttemptAcquire(1).IsAcquired());              // queue empty again
+    CHECK(lim.GetAvailablePermits() == 0);
+}
+
 static void test_approximate_limiter() {
     // Expected values from oracle/semantics.py (ApproxClient + ApproxGlobalTable):
     //   lease 3 ok, lease 2 fails, wait 2 queues (available 1);
@@ -319,7 +386,9 @@ int main(int argc, char **argv) {
         test_tb_sequence();
         test_partitioned_concurrent();
         test_queueing_limiter();
+        test_queueing_cancel();
         test_approximate_limiter();
+        test_approximate_cancel();
         test_auto_replenishment();
         test_registration();
     }
