@@ -13,12 +13,15 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <shared_mutex>
 #include <thread>
+#include <unordered_set>
 #include <variant>
 
 namespace tbe::rate_limiting {
@@ -170,17 +173,88 @@ public:
     const RedisQueueingTokenBucketRateLimiterOptions &options() const { return opt_; }
 
     // InstanceName + resourceID -> dense key (PTB:42).  Exact strings, never hashed.
-    uint64_t KeyOf(const std::string &resource) {
+    // When all PartitionLimit keys are taken, the keys whose Redis hash would have expired
+    // (TB:232-235: EXPIRE after the last grant, or never granted) are reclaimed: their
+    // bucket is absent, exactly what a new string's bucket is.  The directory lookup and
+    // the enqueue happen under a shared lock that the reclaim takes exclusively, and keys
+    // with requests still in the submitter's queue are kept, so no request of an old
+    // string can land on a reassigned key.
+    std::future<RateLimitLease> SubmitResource(const std::string &resource, int32_t permits, int mode) {
+        for (int attempt = 0;; ++attempt) {
+            {
+                std::shared_lock<std::shared_mutex> g(reclaim_mu_);
+                uint64_t k;
+                if (TryKeyOf(resource, k)) return Submit(k, permits, mode);
+            }
+            if (attempt)
+                throw RateLimiterEngineException(TBE_ERANGE, "PartitionLimit reached: no key left for '" +
+                                                                 opt_.InstanceName + resource + "'");
+            ThrowIfDisposed();
+            Run([this] { Reclaim(); });
+        }
+    }
+
+    bool TryKeyOf(const std::string &resource, uint64_t &key) {
         const std::string bucket = opt_.InstanceName + resource;
         std::lock_guard<std::mutex> g(dir_mu_);
         auto it = dir_.find(bucket);
-        if (it != dir_.end()) return it->second;
-        if (dir_.size() >= opt_.PartitionLimit)
-            throw RateLimiterEngineException(TBE_ERANGE, "PartitionLimit reached: no key left for '" + bucket + "'");
-        const uint64_t k = dir_.size();
-        dir_.emplace(bucket, k);
-        return k;
+        if (it != dir_.end()) {
+            key = it->second;
+            return true;
+        }
+        if (!free_ids_.empty()) {
+            key = free_ids_.back();
+            free_ids_.pop_back();
+        } else if (names_.size() < opt_.PartitionLimit) {
+            key = names_.size();
+            names_.emplace_back();
+        } else {
+            return false;
+        }
+        names_[key] = bucket;
+        dir_.emplace(bucket, key);
+        return true;
     }
+
+    // Submitter thread (so every request enqueued before it has been decided).
+    uint64_t Reclaim() {
+        std::unique_lock<std::shared_mutex> x(reclaim_mu_);
+        std::unordered_set<uint64_t> busy;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (auto &v : q_)
+                if (auto *r = std::get_if<Req>(&v)) busy.insert(r->key);
+        }
+        std::lock_guard<std::mutex> g(dir_mu_);
+        const uint64_t n = names_.size();
+        if (n == 0) return 0;
+        std::vector<double> v(n);
+        std::vector<int64_t> t(n);
+        Check(tbe_export_state(eng_, 0, n, v.data(), t.data()));
+        // TB:234: EXPIRE ceil(min(max(capacity / fill_rate, 1), 31536000)) seconds; the
+        // engine's expiry test is tbe_query's (millisecond resolution).
+        double q = (double)opt_.TokenLimit / opt_.FillRatePerSecond();
+        q = (1.0 > q) ? 1.0 : q;
+        q = (31536000.0 < q) ? 31536000.0 : q;
+        const int64_t ttl_ms = (int64_t)std::ceil(q) * 1000;
+        const int64_t now_ms = clock_() / 1000;
+        std::vector<uint8_t> is_free(n, 0);
+        for (uint64_t k : free_ids_) is_free[k] = 1;
+        uint64_t freed = 0;
+        for (uint64_t k = 0; k < n; ++k) {
+            if (is_free[k] || busy.count(k)) continue;
+            if (t[k] != INT64_MIN && now_ms <= t[k] / 1000 + ttl_ms) continue;  // still present
+            dir_.erase(names_[k]);
+            names_[k].clear();
+            last_reply_.erase(k);
+            free_ids_.push_back(k);
+            ++freed;
+        }
+        reclaimed_ += freed;
+        return freed;
+    }
+
+    uint64_t Reclaimed() const { return reclaimed_.load(); }
 
     bool KnownKey(const std::string &resource, uint64_t &key) {
         std::lock_guard<std::mutex> g(dir_mu_);
@@ -576,6 +650,10 @@ private:
 
     std::mutex dir_mu_;
     std::unordered_map<std::string, uint64_t> dir_;
+    std::vector<std::string> names_;       // key -> bucket string
+    std::vector<uint64_t> free_ids_;       // reclaimed keys, reused first
+    std::shared_mutex reclaim_mu_;
+    std::atomic<uint64_t> reclaimed_{0};
     std::unordered_map<uint64_t, int32_t> last_reply_;
     std::atomic<int> estimated_{0};
     std::atomic<int64_t> idle_since_ns_{-1};
@@ -623,14 +701,18 @@ int PartitionedRedisTokenBucketRateLimiter::GetAvailablePermits(const std::strin
 }
 RateLimitLease PartitionedRedisTokenBucketRateLimiter::AttemptAcquireCore(const std::string &id, int p) {
     core_->ThrowIfDisposed();
-    return core_->Submit(core_->KeyOf(id), p, kTbAcquire).get();
+    return core_->SubmitResource(id, p, kTbAcquire).get();
 }
 std::future<RateLimitLease> PartitionedRedisTokenBucketRateLimiter::AcquireAsyncCore(const std::string &id, int p,
                                                                                      const CancellationToken &) {
     core_->ThrowIfDisposed();
-    return core_->Submit(core_->KeyOf(id), p, kTbAcquire);
+    return core_->SubmitResource(id, p, kTbAcquire);
 }
 void PartitionedRedisTokenBucketRateLimiter::DisposeCore() { core_->Dispose(); }
+uint64_t PartitionedRedisTokenBucketRateLimiter::ReclaimExpired() {
+    core_->ThrowIfDisposed();
+    return core_->Run([this] { return core_->Reclaim(); });
+}
 
 // ------------------------------------------------------------------ queueing
 static void check_limit(int p, int limit) {  // Q:70-73, A:87-90, A:119-122

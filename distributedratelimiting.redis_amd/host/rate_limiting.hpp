@@ -242,6 +242,9 @@ public:
     explicit PartitionedRedisTokenBucketRateLimiter(const RedisTokenBucketRateLimiterOptions &options);
     ~PartitionedRedisTokenBucketRateLimiter() override;
     int GetAvailablePermits(const std::string &resourceID) override;
+    // Frees the keys of buckets Redis would have expired (TB:232-235) for new resource
+    // ids; runs by itself when all PartitionLimit keys are taken.  Returns the number freed.
+    uint64_t ReclaimExpired();
 protected:
     RateLimitLease AttemptAcquireCore(const std::string &resourceID, int permitCount) override;
     std::future<RateLimitLease> AcquireAsyncCore(const std::string &resourceID, int permitCount,

@@ -311,6 +311,34 @@ static void test_approximate_cancel() {
     CHECK(lim.GetAvailablePermits() == 0);
 }
 
+static void test_partition_reclaim() {
+    // TokenLimit 2, 1 token/s: EXPIRE ceil(max(2 / 1, 1)) = 2 s after the last grant
+    // (TB:232-235).  Two keys only: a third resource id needs an expired bucket's key.
+    FakeClock clk;
+    RedisTokenBucketRateLimiterOptions o = tb_options(2, 1, 1.0);
+    o.TimeSource = clk.fn();
+    o.PartitionLimit = 2;
+    PartitionedRedisTokenBucketRateLimiter lim(o);
+    CHECK(lim.AttemptAcquire("a", 1).IsAcquired());
+    CHECK(lim.AttemptAcquire("b", 2).IsAcquired());
+    CHECK(throws<RateLimiterEngineException>([&] { lim.AttemptAcquire("c", 1); }));  // nothing expired
+    CHECK(lim.ReclaimExpired() == 0);
+    clk.advance(1000000);
+    CHECK(lim.AttemptAcquire("b", 1).IsAcquired());         // refilled 1 -> 0 left, b lives on
+    clk.advance(1500000);                                   // a: 2.5 s since its grant, b: 1.5 s
+    CHECK(lim.AttemptAcquire("c", 2).IsAcquired());         // takes a's key: fresh bucket, 2 tokens
+    CHECK(lim.GetAvailablePermits("c") == 0);
+    CHECK(lim.GetAvailablePermits("a") == 2);               // unknown again (an absent bucket is full)
+    CHECK(!lim.AttemptAcquire("c", 1).IsAcquired());        // c's state is its own
+    CHECK(!lim.AttemptAcquire("b", 2).IsAcquired());        // b kept its bucket: 1.5 tokens
+    CHECK(throws<RateLimiterEngineException>([&] { lim.AttemptAcquire("a", 1); }));
+    clk.advance(2100000);                                   // b: 3.6 s, c: 2.1 s since their grants
+    CHECK(lim.ReclaimExpired() == 2);
+    CHECK(lim.AttemptAcquire("a", 2).IsAcquired());         // fresh again
+    CHECK(lim.AttemptAcquire("b", 2).IsAcquired());
+    CHECK(lim.ReclaimExpired() == 0);
+}
+
 static void test_approximate_limiter() {
     // Expected values from oracle/semantics.py (ApproxClient + ApproxGlobalTable):
     //   lease 3 ok, lease 2 fails, wait 2 queues (available 1);
@@ -385,6 +413,7 @@ int main(int argc, char **argv) {
     if (gpu) {
         test_tb_sequence();
         test_partitioned_concurrent();
+        test_partition_reclaim();
         test_queueing_limiter();
         test_queueing_cancel();
         test_approximate_limiter();
