@@ -355,30 +355,48 @@ def workload_name(args, n: int) -> str:
 def cpu_baseline(args, n_keys: int, zkeys=(), seed_b: int = SEED_B):
     """The C restatement of the reference script (oracle/tb_ref.c, serial like Redis'
     single script thread) timed on the same trace: the first `sample` requests of each
-    batch, batches in order, until ~args.cpu_seconds of CPU work."""
+    batch, batches in order, until ~args.cpu_seconds of CPU work.  Beside it, the same
+    restatement key-sharded over CPU_THREADS host threads (SURVEY.md §8d "all host
+    cores"; 16 = the GPU box's CPU share), on a fresh table and a shorter sample."""
     from oracle import cref  # CPU baseline leg (checker library), never the product path
     from distributedratelimiting.redis_amd import fill_rate
 
-    ref = cref.CTokenBucket(n_keys, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks))
     sample = min(args.batch, 1 << 22)
     seed = SEED_C if zkeys else seed_b
-    done, spent, b = 0, 0.0, 0
-    while spent < args.cpu_seconds and b < 64:
-        k, p, t = cref.gen_batch(seed, n_keys, b, args.batch, args.interval_us)
-        if zkeys:
-            k = zkeys[b % len(zkeys)]
-        k, p, t = k[:sample], p[:sample], t[:sample]
-        t0 = time.perf_counter()
-        ref.acquire_batch(k, p, t, threads=1)
-        spent += time.perf_counter() - t0
-        done += sample
-        b += 1
-    ref.close()
+
+    def timed(threads: int, seconds: float):
+        ref = cref.CTokenBucket(n_keys, args.token_limit, fill_rate(args.tokens_per_period, args.period_ticks))
+        done, spent, b = 0, 0.0, 0
+        while spent < seconds and b < 64:
+            k, p, t = cref.gen_batch(seed, n_keys, b, args.batch, args.interval_us)
+            if zkeys:
+                k = zkeys[b % len(zkeys)]
+            k, p, t = k[:sample], p[:sample], t[:sample]
+            t0 = time.perf_counter()
+            ref.acquire_batch(k, p, t, threads=threads)
+            spent += time.perf_counter() - t0
+            done += sample
+            b += 1
+        ref.close()
+        return done, spent, b
+
+    done, spent, b = timed(1, args.cpu_seconds)
     what = "config-C (Zipf)" if zkeys else ("config-A (TestApp)" if seed_b == SEED_A else "config-B")
-    return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} requests of each of {b} {what} batches "
-                      f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
-            "host_cpus": os.cpu_count()}
+    out = {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+           "sample": f"first {sample} requests of each of {b} {what} batches "
+                     f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
+           "host_cpus": os.cpu_count()}
+    if CPU_THREADS > 1 and args.cpu_seconds > 0:
+        done_t, spent_t, b_t = timed(CPU_THREADS, min(args.cpu_seconds, 4.0))
+        out["sharded"] = {"value": round(done_t / spent_t, 1), "unit": "decisions/s", "cores": CPU_THREADS,
+                          "kind": "port",
+                          "sample": f"first {sample} requests of each of {b_t} {what} batches "
+                                    f"({done_t} decisions, {spent_t:.1f} s), oracle/tb_ref.c "
+                                    f"key-sharded (key % {CPU_THREADS}) over {CPU_THREADS} threads"}
+    return out
+
+
+CPU_THREADS = 16
 
 
 if __name__ == "__main__":
