@@ -9,6 +9,8 @@ the token-bucket paths need no collective at all when ingest is already partitio
   its owner (ordered by source rank, then arrival index) and a reverse all-to-all
   returns the replies.  The combined order is a valid serial order of the reference:
   per key, rank 0's requests of this step precede rank 1's, and so on.
+* ``route_cancel``: cancellations of queued requests travel to the key's owner the
+  same way (one all-to-all of (key, request id), one of the hits back).
 * ``approx_epoch``: the ApproximateTokenBucket global tier.  Each rank is one client
   (A:9-599) holding a local tier for every shared key; at every refresh epoch the
   per-key consumed counts are exchanged -- all-gather for exact per-client prefix
@@ -62,9 +64,11 @@ def shard_batch(keys, permits, ts_us, world: int):
 def route_batch(decide: Callable, keys, permits, ts_us, group=None, device=None):
     """Decide a batch whose requests arrived at this rank but may belong to any rank.
 
-    ``decide(local_keys, permits, ts) -> (granted u8, remaining i32)`` runs this rank's
-    engine on the requests it owns.  Returns (granted, remaining) for this rank's own
-    requests in their arrival order.  Two all-to-alls (requests out, replies back)."""
+    ``decide(local_keys, permits, ts) -> (granted u8, remaining i32[, extra...])`` runs
+    this rank's engine on the requests it owns.  Returns (granted, remaining) for this
+    rank's own requests in their arrival order, plus any extra int64 reply column
+    ``decide`` returns (a queueing engine's request ids, which the owner assigns and a
+    later ``route_cancel`` needs).  Two all-to-alls (requests out, replies back)."""
     import torch
     import torch.distributed as dist
 
@@ -88,17 +92,56 @@ def route_batch(decide: Callable, keys, permits, ts_us, group=None, device=None)
     dist.all_to_all_single(recv, to(payload), output_split_sizes=recv_counts.tolist(),
                            input_split_sizes=send_counts.tolist(), group=group)
     r = recv.cpu().numpy()
-    g, rem = decide(r[:, 0].astype(np.uint64), r[:, 1].astype(np.int32), r[:, 2])
-    reply = np.stack([np.asarray(g, dtype=np.int64), np.asarray(rem, dtype=np.int64)], axis=1)
-    back = torch.empty((n, 2), dtype=torch.int64, device=device)
+    outs = decide(r[:, 0].astype(np.uint64), r[:, 1].astype(np.int32), r[:, 2])
+    cols = len(outs)
+    reply = np.stack([np.asarray(x, dtype=np.int64).reshape(-1) for x in outs], axis=1) \
+        if r.shape[0] else np.zeros((0, cols), dtype=np.int64)
+    back = torch.empty((n, cols), dtype=torch.int64, device=device)
     dist.all_to_all_single(back, to(reply), output_split_sizes=send_counts.tolist(),
                            input_split_sizes=recv_counts.tolist(), group=group)
     b = back.cpu().numpy()
-    granted = np.empty(n, dtype=np.uint8)
-    remaining = np.empty(n, dtype=np.int32)
-    granted[order] = b[:, 0]
-    remaining[order] = b[:, 1]
-    return granted, remaining
+    res = [np.empty(n, dtype=dt) for dt in [np.uint8, np.int32] + [np.int64] * (cols - 2)]
+    for c in range(cols):
+        res[c][order] = b[:, c]
+    return tuple(res)
+
+
+def route_cancel(cancel: Callable, keys, request_ids, group=None, device=None):
+    """Cancel queued requests (CancelQueueState.TrySetCanceled, Q:480-506 / A:531-557)
+    that may be queued on any rank: ``keys`` are global key ids, ``request_ids`` the ids
+    their owners assigned (``route_batch``'s extra reply column).  ``cancel(local_keys,
+    request_ids) -> u8`` runs on the owner (``QueueingTokenBucketEngine.cancel``).
+    Returns the u8 hits in this rank's order.  Per owner, the cancels apply by source
+    rank, then call order.  Two all-to-alls."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    keys = np.asarray(keys, dtype=np.uint64)
+    n = keys.shape[0]
+    owner = key_owner(keys, world)
+    order = np.argsort(owner, kind="stable")
+    send_counts = np.bincount(owner, minlength=world).astype(np.int64)
+    to = (lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)) if device else \
+        (lambda a: torch.from_numpy(np.ascontiguousarray(a)))
+    sc = to(send_counts)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = rc.cpu().numpy()
+    payload = np.stack([local_key(keys[order], world).astype(np.int64),
+                        np.asarray(request_ids, dtype=np.int64)[order]], axis=1)
+    recv = torch.empty((int(recv_counts.sum()), 2), dtype=torch.int64, device=device)
+    dist.all_to_all_single(recv, to(payload), output_split_sizes=recv_counts.tolist(),
+                           input_split_sizes=send_counts.tolist(), group=group)
+    r = recv.cpu().numpy()
+    hit = np.asarray(cancel(r[:, 0].astype(np.uint64), r[:, 1]), dtype=np.int64) if r.shape[0] \
+        else np.zeros(0, dtype=np.int64)
+    back = torch.empty(n, dtype=torch.int64, device=device)
+    dist.all_to_all_single(back, to(hit), output_split_sizes=send_counts.tolist(),
+                           input_split_sizes=recv_counts.tolist(), group=group)
+    out = np.empty(n, dtype=np.uint8)
+    out[order] = back.cpu().numpy()
+    return out
 
 
 # ------------------------------------------------------------------ approximate global tier

@@ -128,3 +128,62 @@ def ap_epoch_worker(rank: int, world: int, port: int, out_dir: str, mode: str):
              state=state)
     dist.barrier()
     dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ queued waits + cancels
+Q = dict(n_keys=40, token_limit=4, tokens_per_period=1, period_ticks=10_000_000, queue_limit=5, order=0)
+Q_STEPS, Q_N, Q_T0 = 3, 300, 1_760_000_000_000_000
+
+
+def q_batch(rank: int, step: int):
+    rng = np.random.default_rng(555 + 100 * rank + step)
+    keys = rng.integers(0, Q["n_keys"], Q_N, dtype=np.uint64)
+    permits = rng.choice([0, 1, 1, 2, 3], Q_N).astype(np.int32)
+    ts = Q_T0 + step * 700_000 + np.sort(rng.integers(0, 1_000, Q_N))
+    return keys, permits, ts.astype(np.int64)
+
+
+def q_cancel_pick(status) -> np.ndarray:
+    """A third of the queued requests, plus a few that are not queued."""
+    return np.array([i for i in range(Q_N) if (i % 3 == 0 and status[i] == 2) or i % 17 == 5],
+                    dtype=np.int64)
+
+
+def q_refresh_ts(step: int) -> int:
+    return Q_T0 + step * 700_000 + 500_000
+
+
+def q_route_worker(rank: int, world: int, port: int, out_dir: str):
+    dist = _init(rank, world, port)
+    from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
+    from distributedratelimiting.redis_amd import cluster
+
+    tab = QueueingTokenBucketTable(TokenBucketConfig.from_options(
+        Q["token_limit"], Q["tokens_per_period"], Q["period_ticks"]), Q["queue_limit"], Q["order"])
+    next_id = [0]
+
+    def wait(lk, lp, lt):   # the owner's engine: WaitAsync, ids assigned in arrival order
+        st, rem, ids = [], [], []
+        for k, p, t in zip(lk.tolist(), lp.tolist(), lt.tolist()):
+            s, r, _ = tab.acquire(k, p, t, next_id[0])
+            st.append(s)
+            rem.append(r)
+            ids.append(next_id[0])
+            next_id[0] += 1
+        return np.array(st), np.array(rem), np.array(ids)
+
+    def cancel(lk, ids):
+        return np.array([int(tab.cancel(int(k), int(i))) for k, i in zip(lk.tolist(), ids.tolist())])
+
+    out = {}
+    for s in range(Q_STEPS):
+        k, p, t = q_batch(rank, s)
+        st, rem, ids = cluster.route_batch(wait, k, p, t)
+        pick = q_cancel_pick(st)
+        hit = cluster.route_cancel(cancel, k[pick], ids[pick])
+        log = tab.refresh(q_refresh_ts(s))
+        out[f"st{s}"], out[f"rem{s}"], out[f"ids{s}"], out[f"hit{s}"] = st, rem, ids, hit
+        out[f"log{s}"] = np.array(log, dtype=np.int64).reshape(-1, 3)
+    np.savez(os.path.join(out_dir, f"q_{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()

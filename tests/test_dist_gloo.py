@@ -114,3 +114,39 @@ def test_approx_epoch_node_mode_sums_counts(tmp_path):
     # both ranks replay identical sync calls -> identical global scores and estimates
     assert np.array_equal(res[0]["state"][:, 1:3], res[1]["state"][:, 1:3])
     assert res[0]["state"][:, 1].max() > 0
+
+
+def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
+    """Queued waits routed to their owners, then cancels of some of them routed the same
+    way (cluster.route_cancel), then a replenish tick on every rank.  Expected = one
+    serial queueing table: per step rank 0's batch, rank 1's, the cancels, the tick."""
+    from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
+    _spawn(W.q_route_worker, str(tmp_path))
+    res = [np.load(tmp_path / f"q_{r}.npz") for r in range(WORLD)]
+    Q = W.Q
+    ref = QueueingTokenBucketTable(TokenBucketConfig.from_options(
+        Q["token_limit"], Q["tokens_per_period"], Q["period_ticks"]), Q["queue_limit"], Q["order"])
+    ref_id = lambda s, src, i: (s * WORLD + src) * W.Q_N + i   # noqa: E731
+    owner_id = {}   # (owner rank, owner-assigned id) -> reference id
+    total_hits = 0
+    for s in range(W.Q_STEPS):
+        batches = [W.q_batch(r, s) for r in range(WORLD)]
+        for src, (k, p, t) in enumerate(batches):
+            exp = [ref.acquire(int(k[i]), int(p[i]), int(t[i]), ref_id(s, src, i)) for i in range(W.Q_N)]
+            assert res[src][f"st{s}"].tolist() == [e[0] for e in exp], (s, src)
+            assert res[src][f"rem{s}"].tolist() == [e[1] for e in exp], (s, src)
+            for i, x in enumerate(res[src][f"ids{s}"].tolist()):
+                owner_id[(int(k[i]) % WORLD, x)] = ref_id(s, src, i)
+        for src, (k, _, _) in enumerate(batches):
+            pick = W.q_cancel_pick(res[src][f"st{s}"])
+            want = [int(ref.cancel(int(k[i]), ref_id(s, src, int(i)))) for i in pick]
+            assert res[src][f"hit{s}"].tolist() == want, (s, src)
+            total_hits += sum(want)
+        exp_log = ref.refresh(W.q_refresh_ts(s))
+        got = []
+        for r in range(WORLD):
+            for lk, x, rem in res[r][f"log{s}"].tolist():
+                got.append((lk * WORLD + r, owner_id[(r, x)], rem))
+        got.sort(key=lambda e: e[0])   # stable: per-key drain order kept
+        assert got == exp_log, s
+    assert total_hits > 0
