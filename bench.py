@@ -240,9 +240,12 @@ def main():
     # config A is the reference's own per-request deployment: also time the host-buffer
     # entry point (the P/Invoke path: copy in, decide, copy out, synchronise) on the same
     # batches, after the timed region.  Reported beside `value`, never as it.
+    # Config B gets the same check on three of its batches (pageable host buffers: the
+    # PCIe-inclusive rate DESIGN.md §6 discusses).
     host_rate = None
-    if args.workload == "testapp":
-        host = [tuple(x.cpu().numpy() for x in b) for b in bufs[args.warmup:]]
+    if args.workload in ("testapp", "uniform") and rank == 0 and world == 1:
+        timed_bufs = bufs[args.warmup:] if args.workload == "testapp" else bufs[args.warmup:args.warmup + 3]
+        host = [tuple(x.cpu().numpy() for x in b) for b in timed_bufs]
         hb = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period, args.period_ticks,
                                device=dev.index, max_batch=n)
         for k, p, t in host[:1]:
