@@ -242,7 +242,7 @@ def main():
     # batches, after the timed region.  Reported beside `value`, never as it.
     # Config B gets the same check on three of its batches (pageable host buffers: the
     # PCIe-inclusive rate DESIGN.md §6 discusses).
-    host_rate = None
+    host_rate = host_rate_pinned = None
     if args.workload in ("testapp", "uniform") and rank == 0 and world == 1:
         timed_bufs = bufs[args.warmup:] if args.workload == "testapp" else bufs[args.warmup:args.warmup + 3]
         host = [tuple(x.cpu().numpy() for x in b) for b in timed_bufs]
@@ -254,6 +254,19 @@ def main():
         for k, p, t in host[1:]:
             hb.acquire_batch(k.view(np.uint64), p, t)
         host_rate = round(n * (len(host) - 1) / (time.perf_counter() - t1), 1) if len(host) > 1 else None
+        if len(host) > 1:
+            # the same batches from page-locked buffers (tbe_alloc_host): DMA, no staging copy
+            from distributedratelimiting.redis_amd.engine import PinnedArray
+            pk, pp, pt = PinnedArray(n, np.uint64), PinnedArray(n, np.int32), PinnedArray(n, np.int64)
+            spent = 0.0
+            for k, p, t in host[1:]:
+                pk.array[:], pp.array[:], pt.array[:] = k.view(np.uint64), p, t
+                t1 = time.perf_counter()
+                hb.acquire_batch(pk.array, pp.array, pt.array)
+                spent += time.perf_counter() - t1
+            host_rate_pinned = round(n * (len(host) - 1) / spent, 1)
+            for a in (pk, pp, pt):
+                a.free()
         hb.close()
 
     cpu = None
@@ -285,6 +298,8 @@ def main():
                        "layout": layout},
             "grant_rate_last_batch": round(grant_rate, 4),
             **({"host_buffer_decisions_per_s": host_rate} if host_rate is not None else {}),
+            **({"host_buffer_pinned_decisions_per_s": host_rate_pinned}
+               if host_rate_pinned is not None else {}),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}

@@ -32,7 +32,7 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
             "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
             "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device",
-            "tbe_import_state", "tbe_queue_cancel")
+            "tbe_import_state", "tbe_queue_cancel", "tbe_alloc_host", "tbe_free_host")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -104,6 +104,10 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_refresh_log.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]
     lib.tbe_queue_of.restype = c_int32
     lib.tbe_queue_of.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint32)]
+    lib.tbe_alloc_host.restype = c_int32
+    lib.tbe_alloc_host.argtypes = [c_uint64, POINTER(c_void_p)]
+    lib.tbe_free_host.restype = None
+    lib.tbe_free_host.argtypes = [c_void_p]
     lib.tbe_queue_cancel.restype = c_int32
     lib.tbe_queue_cancel.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, POINTER(c_uint64)]
     lib.tbe_approx_acquire_batch.restype = c_int32

@@ -2880,6 +2880,22 @@ tbe_status tbe_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys, const
     return run_batch(e, d_keys, d_permits, d_ts_us, n, d_granted, d_remaining, (hipStream_t)stream);
 }
 
+tbe_status tbe_alloc_host(uint64_t bytes, void **out) {
+    if (!out) return TBE_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return TBE_OK;
+    const hipError_t rc = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (rc != hipSuccess) {
+        *out = nullptr;
+        return rc == hipErrorOutOfMemory ? TBE_ENOMEM : TBE_EDEVICE;
+    }
+    return TBE_OK;
+}
+
+void tbe_free_host(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 tbe_status tbe_synchronize(tbe_engine *e) {
     if (!e) return TBE_EINVAL;
     HIP_TRY(e, hipSetDevice(e->device));

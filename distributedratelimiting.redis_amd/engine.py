@@ -22,6 +22,36 @@ def fill_rate(tokens_per_period: int, period_ticks: int) -> float:
     return _capi.load().tbe_fill_rate(tokens_per_period, period_ticks)
 
 
+class PinnedArray:
+    """A numpy array over page-locked host memory from ``tbe_alloc_host`` (the host-buffer
+    calls copy it by DMA).  ``.array`` is valid until ``free()`` or collection of this
+    object; keep the object alive while the array (or a view of it) is in use."""
+
+    def __init__(self, n: int, dtype):
+        self._lib = _capi.load()
+        dt = np.dtype(dtype)
+        nbytes = max(1, int(n) * dt.itemsize)
+        p = c_void_p()
+        st = self._lib.tbe_alloc_host(nbytes, byref(p))
+        if st != 0 or not p.value:
+            raise TbeError(st, f"tbe_alloc_host({nbytes}) failed")
+        self._ptr = p.value
+        buf = (ctypes.c_uint8 * nbytes).from_address(self._ptr)
+        self.array = np.frombuffer(buf, dtype=np.uint8)[: int(n) * dt.itemsize].view(dt)
+
+    def free(self) -> None:
+        if self._ptr:
+            self.array = None
+            self._lib.tbe_free_host(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class TokenBucketEngine:
     KIND = _capi.TBE_KIND_TOKEN_BUCKET
 

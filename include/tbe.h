@@ -120,6 +120,14 @@ tbe_status tbe_acquire_batch_device(tbe_engine *engine, const uint64_t *d_keys,
                                     uint64_t n, uint8_t *d_granted, int32_t *d_remaining,
                                     void *stream);
 
+/* Page-locked host memory for the host-buffer calls' arrays (the caller
+ * owns its buffers, pinning recommended).  Copies from it run as direct DMA, without the
+ * staging copy a pageable buffer needs; the C# host pins its batch arrays this way
+ * instead of GCHandle-pinning managed arrays.  bytes == 0 gives NULL.  Free with
+ * tbe_free_host (NULL is ignored). */
+tbe_status tbe_alloc_host(uint64_t bytes, void **out);
+void tbe_free_host(void *p);
+
 /* Waits for every enqueued batch; TBE_EINVAL if any of them was invalid since the
  * last call (the sticky flag is then cleared). */
 tbe_status tbe_synchronize(tbe_engine *engine);
