@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate CPU-baseline budget (0 disables)")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--no-host-buffer", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) rate, e.g. under rocprofv3 so the "
+                         "kernel statistics cover the timed batches only")
     ap.add_argument("--no-pack", action="store_true",
                     help="wide pass records even where the packed 8-byte form applies (A/B)")
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
@@ -243,7 +246,7 @@ def main():
     # Config B gets the same check on three of its batches (pageable host buffers: the
     # PCIe-inclusive rate DESIGN.md §6 discusses).
     host_rate = host_rate_pinned = None
-    if args.workload in ("testapp", "uniform") and rank == 0 and world == 1:
+    if args.workload in ("testapp", "uniform") and rank == 0 and world == 1 and not args.no_host_buffer:
         timed_bufs = bufs[args.warmup:] if args.workload == "testapp" else bufs[args.warmup:args.warmup + 3]
         host = [tuple(x.cpu().numpy() for x in b) for b in timed_bufs]
         hb = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period, args.period_ticks,

@@ -24,7 +24,7 @@ step bench 420 python -u bench.py --steps "$STEPS" --warmup 2 --cpu-seconds 8
 if [ "${PROFILE:-1}" = "1" ]; then
     cd /tmp && export TMPDIR=/tmp
     step rocprof 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline
+        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer
     cd "$ROOT"
 fi
 echo done

@@ -28,7 +28,7 @@ if [ "${PROFILE:-1}" = "1" ]; then
     cd /tmp && export TMPDIR=/tmp
     for W in ${WORKLOADS:-uniform zipf queue approx}; do
         step rocprof_$W 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$W" -o run -- \
-            python3 "$ROOT/bench.py" --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-stage-timing --no-pipeline
+            python3 "$ROOT/bench.py" --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer
     done
     cd "$ROOT"
 fi
