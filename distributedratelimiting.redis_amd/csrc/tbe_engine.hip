@@ -88,8 +88,6 @@ constexpr int kUnItems = 8;
 constexpr int kUnTile = kUnBlock * kUnItems;
 constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
 constexpr int kMaxHistBlocks = 1024;
-constexpr int kFoldItems = 8;                          // requests per thread per chunk
-constexpr int kChunk = kBlock * kFoldItems;            // 2048
 constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
 constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
