@@ -87,3 +87,30 @@ def test_approx_cancel_hand_case():
     assert s.qcount == 2 and [e.request_id for e in s.queue] == [2]
     # the count is not added back to the local score (the A:489 double count)
     assert s.local == 4
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+def test_cancel_invariants(order):
+    """Random waits, cancels and ticks: qsum always equals the queued permits and stays
+    within QueueLimit, a cancel never touches the bucket, and a canceled id never drains."""
+    rng = np.random.default_rng(4242 + order)
+    q = QueueingTokenBucketTable(TokenBucketConfig.from_options(4, 1, 10_000_000), 5, order)
+    t, rid, canceled = S_US, 0, set()
+    for step in range(40):
+        for _ in range(30):
+            k = int(rng.integers(0, 6))
+            q.acquire(k, int(rng.choice([0, 1, 1, 2, 3])), t, rid)
+            rid += 1
+            t += int(rng.integers(0, 20_000))
+        for k in range(6):
+            for e in list(q.queues.get(k, [])):
+                if rng.random() < 0.3:
+                    before = q.tb.query(k)
+                    assert q.cancel(k, e.request_id)
+                    assert q.tb.query(k) == before
+                    canceled.add(e.request_id)
+        for k, ents in q.queues.items():
+            assert q.qsum.get(k, 0) == sum(e.permits for e in ents) <= 5
+        t += int(rng.integers(0, 900_000))
+        assert not canceled & {x for _, x, _ in q.refresh(t)}
+    assert canceled
