@@ -110,3 +110,32 @@ def test_approx_cancel(engine_lib, gpu, order):
             s = cli.st(key)
             assert (lo, gl, est, a, q) == (s.local, s.global_, s.est, cli.available(s), len(s.queue))
             assert [x for x, _ in eng.queue_of(key)] == [e.request_id for e in s.queue]
+
+
+def test_queue_cancel_config_d_scale(engine_lib, gpu):
+    """Config D's shape (QueueLimit 16, TokenLimit 4, 1M keys, 1M-request batch): cancel
+    30% of the queued requests in one call (~1e5 key runs).  Size-independent checks:
+    every one hits once, sampled queues lose exactly the canceled ids in order, a second
+    cancel finds nothing, and the next tick never grants a canceled id."""
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine
+    from oracle import trace
+    n_keys, n = 1 << 20, 1 << 20
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, 16, OLDEST_FIRST, device=0)
+    for b in range(2):
+        k, p, ts = trace.make_batch(0x5EED000D, n_keys, b, n, 1_000)
+        st, _, _ = eng.wait_batch(k, p, ts, b * n)
+    queued = np.flatnonzero(st == 2)
+    assert queued.size > 1000
+    rng = np.random.default_rng(9)
+    pick = rng.choice(queued, queued.size * 3 // 10, replace=False)
+    ck, ci = k[pick].astype(np.uint64), (n + pick).astype(np.int64)
+    sample = np.unique(ck)[:: max(1, np.unique(ck).size // 200)]
+    before = {int(x): eng.queue_of(int(x)) for x in sample}
+    hit = eng.cancel(ck, ci)
+    assert hit.all()
+    gone = set(ci.tolist())
+    for x, q in before.items():
+        assert eng.queue_of(x) == [e for e in q if e[0] not in gone]
+    assert not eng.cancel(ck, ci).any()
+    _, ids, _ = eng.refresh(trace.T0_US + 3 * 1_000_000)
+    assert ids.size > 0 and not gone & set(ids.tolist())
