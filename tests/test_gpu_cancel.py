@@ -139,3 +139,34 @@ def test_queue_cancel_config_d_scale(engine_lib, gpu):
     assert not eng.cancel(ck, ci).any()
     _, ids, _ = eng.refresh(trace.T0_US + 3 * 1_000_000)
     assert ids.size > 0 and not gone & set(ids.tolist())
+
+
+def test_approx_cancel_scale(engine_lib, gpu):
+    """Approximate kind, 1M keys and 2M waits over 2 batches (caps exhausted, queues in
+    use): cancel a third of the queued requests in one call; sampled queues lose exactly
+    those ids, local state (qsum via `queued`) follows, and the next refresh never
+    completes a canceled id."""
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    n_keys, n = 1 << 20, 1 << 20
+    eng = ApproximateEngine(n_keys, 4, 4, 10_000_000, 8, OLDEST_FIRST, device=0)
+    rng = np.random.default_rng(31)
+    for b in range(2):
+        k = rng.integers(0, n_keys, n).astype(np.uint64)
+        p = rng.choice([1, 1, 2, 3], n).astype(np.int32)
+        st, _, _ = eng.acquire_batch(k, p, wait=True, id_base=b * n)
+    queued = np.flatnonzero(st == 2)
+    assert queued.size > 1000
+    pick = rng.choice(queued, queued.size // 3, replace=False)
+    ck, ci = k[pick], (n + pick).astype(np.int64)
+    uk = np.unique(ck)
+    sample = uk[:: max(1, uk.size // 200)]
+    before = {int(x): eng.queue_of(int(x)) for x in sample}
+    assert eng.cancel(ck, ci).all()
+    gone = set(ci.tolist())
+    for x, q in before.items():
+        left = [e for e in q if e[0] not in gone]
+        assert eng.queue_of(x) == left
+        assert eng.local_state(x)[4] == len(left)
+    assert not eng.cancel(ck, ci).any()
+    _, ids, _ = eng.refresh(S_US + 5_000_000)
+    assert not gone & set(ids.tolist())
