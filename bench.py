@@ -184,6 +184,12 @@ def main():
         elapsed = float(tt.item())
     stages_overlapped = eng.stage_times()
     grant_rate = float(granted.float().mean().item())
+    # SURVEY.md §8(d) B_alg of the last timed batch, measured: U = its distinct keys, W =
+    # the distinct keys it wrote (granted at least once; a deny writes nothing, TB:225-236)
+    last_keys = bufs[total_steps - 1][0]
+    u_meas = int(torch.unique(last_keys).numel())
+    w_meas = int(torch.unique(last_keys[granted.bool()]).numel())
+    step_alg = int(n * 25 + u_meas * 16 + w_meas * 16)
 
     decisions = n * args.steps * world
     value = decisions / elapsed
@@ -225,12 +231,25 @@ def main():
         distinct = None
         if zkeys:   # distinct keys per batch, measured (the uniform estimate does not apply)
             distinct = float(np.mean([np.unique(zk).size for zk, _ in zkeys]))
-        alg_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct,
+        own_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct,
                                       1 if layout.get("narrow") else 4)
+        # achieved: §8(d)'s B_alg of one step (one batch = one launch of the dominant
+        # kernel's stage) over that kernel's launch time; step_frac: over the whole step
+        alg_bytes = step_alg if launches[name] == 1 else step_alg // launches[name]
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+        step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": pmc_traffic(name, args.workload), "alg_bytes_per_launch": alg_bytes,
+                    "alg_bytes_note": "SURVEY.md §8(d): 25 B per request + 16 B per distinct key read "
+                                      "+ 16 B per distinct key written, U and W measured on the last "
+                                      "timed batch",
+                    "distinct_keys_U": u_meas, "written_keys_W": w_meas,
+                    "step_alg_bytes": step_alg, "step_achieved": round(step_achieved, 1),
+                    "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
+                    "step_traffic": pmc_step_traffic(args.workload),
+                    "kernel_own_bytes_per_launch": own_bytes,
+                    "kernel_own_frac": round(own_bytes / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "avg_launch_ms": round(per_launch_ms, 4),
                     "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
                                "engine stream" if replay_check is not None else
@@ -361,6 +380,17 @@ def pmc_traffic(stage: str, workload: str = "uniform"):
         return None
     # the fold stage is two launches (summed); other stages one per pass (averaged)
     return round(sum(v) if stage == "fold" else sum(v) / len(v), 1)
+
+
+def pmc_step_traffic(workload: str = "uniform"):
+    """HBM bytes of one whole step (every kernel of one batch), from the committed PMC
+    summary's per-step total for `workload` (tools/pmc_summary.py --write), if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("step_hbm_bytes", {}).get(workload)
+    except (OSError, ValueError):
+        return None
 
 
 def workload_name(args, n: int) -> str:

@@ -32,7 +32,8 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_approx_acquire_batch", "tbe_approx_collect", "tbe_approx_sync", "tbe_approx_refresh",
             "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
             "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device",
-            "tbe_import_state", "tbe_queue_cancel", "tbe_alloc_host", "tbe_free_host")
+            "tbe_import_state", "tbe_queue_cancel", "tbe_alloc_host", "tbe_free_host",
+            "tbe_approx_export_state", "tbe_approx_import_state")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -49,6 +50,8 @@ class TbeConfig(Structure):
         ("device", c_int32),
         ("flags", c_uint32),
         ("max_batch", c_uint64),
+        ("zero_wait_slots", c_int32),
+        ("reserved", c_int32),
     ]
 
 
@@ -139,6 +142,17 @@ def load(path: str = None) -> ctypes.CDLL:
                                                     c_int64, c_void_p, c_void_p, c_void_p]
     lib.tbe_import_state.restype = c_int32
     lib.tbe_import_state.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]
+    lib.tbe_approx_export_state.restype = c_int32
+    lib.tbe_approx_export_state.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]
+    lib.tbe_approx_import_state.restype = c_int32
+    lib.tbe_approx_import_state.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]
+    lib.tbe_gen_zipf_keys_device.restype = c_int32
+    lib.tbe_gen_zipf_keys_device.argtypes = [c_uint64, c_uint64, c_double, c_uint64, c_uint64, c_void_p,
+                                             c_void_p]
+    lib.tbe_gen_batch_device.restype = c_int32
+    lib.tbe_gen_batch_device.argtypes = [c_uint64] * 4 + [c_int32] * 2 + [c_int64] * 2 + [c_void_p] * 4
+    lib.tbe_numfmt_device.restype = c_int32
+    lib.tbe_numfmt_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p]
     lib.tbe_layout.restype = c_int32
     lib.tbe_layout.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]
     lib.tbe_stage_times.restype = c_int32
@@ -149,6 +163,8 @@ def load(path: str = None) -> ctypes.CDLL:
 
 def make_config(n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
                 kind: int = TBE_KIND_TOKEN_BUCKET, queue_limit: int = 0, queue_order: int = 0,
-                device: int = -1, flags: int = 0, max_batch: int = 0) -> TbeConfig:
+                device: int = -1, flags: int = 0, max_batch: int = 0,
+                zero_wait_slots: int = 0) -> TbeConfig:
     return TbeConfig(ctypes.sizeof(TbeConfig), kind, n_keys, token_limit, tokens_per_period,
-                     period_ticks, queue_limit, queue_order, device, flags, max_batch)
+                     period_ticks, queue_limit, queue_order, device, flags, max_batch,
+                     zero_wait_slots, 0)

@@ -660,6 +660,17 @@ __device__ __forceinline__ void put_reply(uint32_t *res, uint32_t q, uint32_t re
         res[q] = rep;
 }
 
+// Write-back filter of a dense slice: a deny writes nothing (TB:225-236), so only the
+// 128-byte lines holding a modified row go back to HBM, each whole (8 rows of 16 B;
+// `dirty` has one bit per row, and a bucket's first row starts a line).  A sparse slice
+// writes its modified rows one by one (the rows beside them were never loaded).
+__device__ __forceinline__ bool row_line_dirty(const uint32_t *dirty, uint32_t j) {
+    return ((dirty[j >> 5] >> (j & 24u)) & 0xFFu) != 0;
+}
+__device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
+    return (dirty[j >> 5] >> (j & 31u)) & 1u;
+}
+
 // Full buckets (>= R/2 requests, uniform traffic): 512-thread workgroups with the rows'
 // field t cached in LDS (74.5 KB, two workgroups per CU), one chunk of 2048 requests.
 // k_fold below takes the other buckets.
@@ -700,6 +711,9 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
     Slot *__restrict__ rows = table + row0;
     // Buckets with >= R/2 requests only (k_fold takes the others): nearly every line of
     // the slice is touched, so the whole slice is pulled in and written back.
+#ifdef TBE_FOLD_NARROW_ONLY
+    return;   // A/B: k_fold takes every bucket
+#endif
     if (e - s < (R >> 1)) return;
     const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
@@ -828,7 +842,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
                 } else if (o == tag) {
                     row[kl[r]] = nrow[r];           // the row this round's evaluation produced
                     ft[kl[r]] = rq[r].new_t;        // its field t (unused while absent)
-                    if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                    atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     pend &= ~(1u << r);
                 }
             }
@@ -888,7 +902,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
                     } else if (o == tag) {
                         row[tkl] = nr;
                         ft[tkl] = trq.new_t;
-                        if (!dense) atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
+                        atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
                         tp = false;
                     }
                     if (!tp) put_reply(res, c + tlid, trep, narrow);
@@ -911,9 +925,9 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
         }
     }
     __syncthreads();
-    // the slice streams out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log)
+    // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log)
     for (uint32_t j = tid; j < nrows; j += kFoldBlock)
-        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) ST_S(rows + j, row[j]);
+        if (row_line_dirty(dirty, j)) ST_S(rows + j, row[j]);
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
         for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
@@ -974,7 +988,9 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
+#ifndef TBE_FOLD_NARROW_ONLY
     if (e - s >= (R >> 1)) return;   // k_fold_wide's
+#endif
     // Whole slice (dense) or touched rows only (sparse), decided below.
     bool dense = false;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
@@ -1117,7 +1133,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
                     pend &= ~(1u << r);             // before the key's first modifier: decided
                 } else if (o == tag) {
                     row[kl[r]] = nrow[r];           // the row this round's evaluation produced
-                    if (!dense) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                    atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     pend &= ~(1u << r);
                 }
             }
@@ -1189,7 +1205,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
                         tp[i] = false;
                     } else if (o == tag) {
                         row[tkl[i]] = nr[i];
-                        if (!dense) atomicOr(&dirty[tkl[i] >> 5], 1u << (tkl[i] & 31));
+                        atomicOr(&dirty[tkl[i] >> 5], 1u << (tkl[i] & 31));
                         tp[i] = false;
                     }
                     if (!tp[i]) put_reply(res, c + tlid[i], trep[i], narrow);
@@ -1213,9 +1229,10 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
         }
     }
     __syncthreads();
-    // the slice streams out (non-temporal: 12% faster fold, profiles/r01_v10_ablate_nt_variants.log)
+    // modified rows (sparse) or dirty lines (dense) stream out (non-temporal: 12% faster
+    // fold, profiles/r01_v10_ablate_nt_variants.log)
     for (uint32_t j = tid; j < nrows; j += kTbBlock)
-        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) ST_S(rows + j, row[j]);
+        if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, row[j]);
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
         for (uint32_t j = tid; j < nrows; j += kTbBlock) {
@@ -1778,11 +1795,11 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
         }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < nrows; j += kQBlock)
-        if (dense || (dirty[j >> 5] & (1u << (j & 31)))) {
-            ST_S(rows + j, slot[j]);
-            ST_U(hrows + j, qh[j]);
-        }
+    // dense: whole dirty lines of rows (8 per line) and of headers (16 per line)
+    for (uint32_t j = tid; j < nrows; j += kQBlock) {
+        if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
+        if (dense ? ((dirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(dirty, j)) ST_U(hrows + j, qh[j]);
+    }
 }
 
 // One replenish tick (Q:237-271) over every key: drain the head (OldestFirst) or tail
@@ -1850,7 +1867,8 @@ __global__ __launch_bounds__(kBlock) void k_drain(
 struct ALocal {
     int32_t cap;     // (int)Math.Ceiling((TokenLimit - _globalThrottleScore) / _instanceCountEstimate)
     int32_t local;   // _localThrottleScore
-    int32_t qsum;    // _queueCount
+    uint16_t qsum;   // _queueCount (<= QueueLimit <= 65535)
+    uint16_t zc;     // zero-permit registrations in the queue (<= AParams.zero_slots)
     uint32_t hc;     // ring head (bits 0-15) | count (bits 16-31)
 };
 struct AClient {
@@ -1862,10 +1880,10 @@ struct AParams {
     int32_t token_limit;
     int32_t queue_limit;
     int32_t order;          // 0 OldestFirst, 1 NewestFirst
-    uint32_t cap;           // ring entries per key
+    uint32_t cap;           // ring entries per key: max(1, QueueLimit) + zero_slots
     int64_t id_base;
     int32_t wait;           // 1: WaitAsyncCore (A:116-183), 0: AcquireCore (A:84-113)
-    int32_t pad;
+    int32_t zero_slots;     // ring entries a key may give to zero-permit registrations
     double decay_rate;      // FillRatePerSecond (A:224 decay_rate)
     double period_s;        // ReplenishmentPeriod.TotalSeconds (A:443)
 };
@@ -1909,8 +1927,26 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     ALocal *__restrict__ rows = alocal + row0;
+#ifdef TBE_APPROX_DENSE
+    // Experiment ("streaming hints"): dense buckets pull the whole local-tier
+    // slice and write it back whole, with streaming hints unless TBE_APPROX_DENSE_PLAIN.
+    const bool dense = (e - s) >= (R >> 3);
+    if (dense) {
+        for (uint32_t j = tid; j < R; j += kFoldBlock) {
+            const ALocal *src = rows + (j < nrows ? j : nrows - 1);
+#ifdef TBE_APPROX_DENSE_PLAIN
+            sl[j] = *src;
+#else
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+            __builtin_memcpy(&sl[j], &v, sizeof v);
+#endif
+        }
+    }
+#else
+    constexpr bool dense = false;
+#endif
     for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
-        loaded[j] = 0;
+        loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
     for (uint32_t c = s; c < e; c += kFoldChunk) {
@@ -1942,7 +1978,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
             ALocal tmp[kFoldPer];
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
-                tmp[r] = ALocal{0, 0, 0, 0u};
+                tmp[r] = ALocal{0, 0, 0, 0, 0u};
                 if (mine & (1u << r)) tmp[r] = rows[kl[r]];
             }
 #pragma unroll
@@ -1969,8 +2005,27 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                 if (p > A.token_limit) {                                   // A:87-90 / A:119-122
                     status = TBE_WAIT_REJECTED;
                     evaluated = false;
-                } else if (p == 0) {                                       // A:93-102 / A:127-130
+                } else if (p == 0 && (avail > 0 || !A.wait)) {            // A:93-102 / A:127-130
                     status = (avail > 0) ? TBE_WAIT_GRANTED : TBE_WAIT_FAILED;
+                } else if (p == 0) {
+                    // WaitAsync(0) while throttled: TryLease fails (A:191, availableTokens
+                    // != 0) and QueueLimit - _queueCount < 0 never holds (A:141), so the
+                    // registration queues with Count 0 (A:166-181) and completes at the
+                    // next drain that reaches it (A:474: AvailableTokens >= 0).  The
+                    // reference bounds such registrations by nothing; the ring gives each
+                    // key zero_slots of them, beyond which the wait fails.
+                    if (a.zc < A.zero_slots) {
+                        uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
+                        uint32_t tail = head + cnt;
+                        if (tail >= A.cap) tail -= A.cap;
+                        ring[(row0 + kl[r]) * (uint64_t)A.cap + tail] = (uint64_t)(A.id_base + ai[r]) << 16;
+                        a.hc = (head & 0xFFFFu) | ((cnt + 1) << 16);
+                        a.zc = (uint16_t)(a.zc + 1);
+                        modified = true;
+                        status = TBE_WAIT_QUEUED;
+                    } else {
+                        status = TBE_WAIT_FAILED;
+                    }
                 } else if (avail >= p && avail != 0 && (a.qsum == 0 || A.order == 1)) {  // A:191-209
                     a.local = (int32_t)((uint32_t)a.local + (uint32_t)p);
                     modified = true;
@@ -1990,7 +2045,8 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                                     ev_cause[at] = ai[r];
                                     ev_id[at] = (int64_t)(ent >> 16);
                                 }
-                                a.qsum -= (int32_t)(ent & 0xFFFFu);
+                                a.qsum = (uint16_t)(a.qsum - (uint32_t)(ent & 0xFFFFu));
+                                if ((ent & 0xFFFFu) == 0) a.zc = (uint16_t)(a.zc - 1);   // DequeueHead takes it too
                                 head = (head + 1 == A.cap) ? 0 : head + 1;
                                 --cnt;
                             }
@@ -2005,7 +2061,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                         if (tail >= A.cap) tail -= A.cap;
                         kr[tail] = ((uint64_t)(A.id_base + ai[r]) << 16) | (uint32_t)p;
                         ++cnt;
-                        a.qsum += p;
+                        a.qsum = (uint16_t)(a.qsum + (uint32_t)p);
                         status = TBE_WAIT_QUEUED;
                     }
                     a.hc = (head & 0xFFFFu) | (cnt << 16);
@@ -2027,8 +2083,19 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
         }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < nrows; j += kFoldBlock)
-        if (dirty[j >> 5] & (1u << (j & 31))) rows[j] = sl[j];
+    for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
+        if (dense) {
+#if defined(TBE_APPROX_DENSE) && !defined(TBE_APPROX_DENSE_PLAIN)
+            u32x4 v;
+            __builtin_memcpy(&v, &sl[j], sizeof v);
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(rows + j));
+#else
+            rows[j] = sl[j];
+#endif
+        } else if (dirty[j >> 5] & (1u << (j & 31))) {
+            rows[j] = sl[j];
+        }
+    }
 }
 
 // A:430-435: count = _localThrottleScore; _localThrottleScore = 0, for every key.
@@ -2106,8 +2173,9 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
             }
             const uint64_t ent = kr[idx];
             const int32_t c = (int32_t)(ent & 0xFFFFu);
-            if (avail_of(a) < c) break;
-            a.qsum -= c;
+            if (avail_of(a) < c) break;                                  // A:474 (Count 0: always)
+            a.qsum = (uint16_t)(a.qsum - (uint32_t)c);
+            if (c == 0) a.zc = (uint16_t)(a.zc - 1);
             a.local = (int32_t)((uint32_t)a.local + (uint32_t)c);
             if (A.order == 0) head = (head + 1 == A.cap) ? 0 : head + 1;
             --cnt;
@@ -2129,7 +2197,7 @@ __global__ void k_init_approx(uint64_t n_keys, ALocal *__restrict__ alocal, ACli
                               int32_t token_limit) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += stride) {
-        alocal[k] = ALocal{token_limit, 0, 0, 0u};     // global 0, est 1 -> cap = TokenLimit
+        alocal[k] = ALocal{token_limit, 0, 0, 0, 0u};  // global 0, est 1 -> cap = TokenLimit
         aclient[k] = AClient{1.0, 0, 0};
         gv[k] = 0.0;
         gp[k] = 0.0;
@@ -2672,6 +2740,10 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
             return create_fail(TBE_EINVAL, "QueueProcessingOrder must be OldestFirst (0) or NewestFirst (1)");
         if (c.token_limit >= (int32_t)kRemNone)                                     // reply packing
             return create_fail(TBE_EINVAL, "TokenLimit must be < 2^30 - 1 for queueing limiters");
+        if (c.zero_wait_slots < 0 || (c.kind == TBE_KIND_QUEUEING && c.zero_wait_slots != 0) ||
+            std::max(1, c.queue_limit) + c.zero_wait_slots > 0xFFFF)
+            return create_fail(TBE_EINVAL, "zero_wait_slots must be >= 0 (approximate kind only) with "
+                                           "max(1, QueueLimit) + zero_wait_slots <= 65535");
     }
     if (c.n_keys == 0 || c.n_keys > (1ull << 32))
         return create_fail(TBE_EINVAL, "n_keys must lie in [1, 2^32]");
@@ -2777,7 +2849,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->ap.token_limit = c.token_limit;
         e->ap.queue_limit = c.queue_limit;
         e->ap.order = c.queue_order;
-        e->ap.cap = (uint32_t)std::max(1, c.queue_limit);
+        e->ap.zero_slots = c.zero_wait_slots;
+        e->ap.cap = (uint32_t)(std::max(1, c.queue_limit) + c.zero_wait_slots);
         e->ap.decay_rate = rate;
         e->ap.period_s = (double)c.replenishment_period_ticks / 10000000.0;
         if (hipMalloc(&e->alocal, c.n_keys * sizeof(ALocal)) != hipSuccess) return bail(TBE_ENOMEM);
@@ -3360,6 +3433,46 @@ tbe_status tbe_approx_query(tbe_engine *e, uint64_t key, int32_t *local, int32_t
     return TBE_OK;
 }
 
+tbe_status tbe_approx_export_state(tbe_engine *e, uint64_t first, uint64_t count, double *v, double *p,
+                                   int64_t *t_us) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    if (first > e->cfg.n_keys || count > e->cfg.n_keys - first)
+        return fail(e, TBE_EINVAL, "range out of bounds");
+    if (count == 0) return TBE_OK;
+    if (!v || !p || !t_us) return fail(e, TBE_EINVAL, "null buffer");
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());   // after every enqueued batch and sync, whatever its stream
+    HIP_TRY(e, hipMemcpy(v, e->gv + first, count * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(p, e->gp + first, count * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(t_us, e->gt + first, count * sizeof(int64_t), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < count; ++i)
+        if (t_us[i] == kAbsent) v[i] = p[i] = 0.0;   // absent: the sync script's default {0, 0}
+    return TBE_OK;
+}
+
+tbe_status tbe_approx_import_state(tbe_engine *e, uint64_t first, uint64_t count, const double *v,
+                                   const double *p, const int64_t *t_us) {
+    if (!e) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
+    if (first > e->cfg.n_keys || count > e->cfg.n_keys - first)
+        return fail(e, TBE_EINVAL, "range out of bounds");
+    if (count == 0) return TBE_OK;
+    if (!v || !p || !t_us) return fail(e, TBE_EINVAL, "null buffer");
+    std::vector<double> tv(count), tp(count);
+    for (uint64_t i = 0; i < count; ++i) {
+        if (t_us[i] != kAbsent && t_us[i] < 0) return fail(e, TBE_EINVAL, "t_us < 0");
+        tv[i] = t_us[i] == kAbsent ? 0.0 : v[i];
+        tp[i] = t_us[i] == kAbsent ? 0.0 : p[i];
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());
+    HIP_TRY(e, hipMemcpy(e->gv + first, tv.data(), count * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(e->gp + first, tp.data(), count * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(e, hipMemcpy(e->gt + first, t_us, count * sizeof(int64_t), hipMemcpyHostToDevice));
+    return TBE_OK;
+}
+
 tbe_status tbe_refresh_log(tbe_engine *e, uint64_t *keys, int64_t *request_id, int32_t *remaining,
                            uint64_t capacity, uint64_t *n_written) {
     if (!e || !n_written) return TBE_EINVAL;
@@ -3449,6 +3562,7 @@ __global__ __launch_bounds__(256) void k_cancel(
             continue;
         }
         qsum -= (int64_t)(kr[(head + j) % cap] & 0xFFFFu);
+        if (approx && (kr[(head + j) % cap] & 0xFFFFu) == 0) a.zc = (uint16_t)(a.zc - 1);
         for (; j + 1 < cnt; ++j) kr[(head + j) % cap] = kr[(head + j + 1) % cap];
         --cnt;
         hit[c] = 1;
@@ -3456,7 +3570,7 @@ __global__ __launch_bounds__(256) void k_cancel(
     }
     if (!changed) return;
     if (approx) {
-        a.qsum = (int32_t)qsum;
+        a.qsum = (uint16_t)qsum;
         a.hc = (head & 0xFFFFu) | (cnt << 16);
         alocal[key] = a;
     } else {

@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 #include "../../include/tbe_tools.h"
+#include "tbe_numfmt.hpp"
 
 namespace {
 
@@ -40,7 +43,112 @@ __global__ void k_gen_batch(uint64_t seed, uint64_t n_keys, uint64_t g0, uint64_
     }
 }
 
+// The engine's `%.14g` + double.Parse round trip (tbe_numfmt.hpp, used by k_approx_sync
+// for A:270 -> A:442) over an array, so tests can check the gfx950 build of it directly.
+__global__ void k_numfmt(const double *__restrict__ in, double *__restrict__ out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = tbe::round_trip_14g(in[i]);
+}
+
+// ---------------------------------------------------------------- Zipf key streams
+// Bounded Zipf(s) ranks by rejection-inversion (Hormann & Derflinger 1996) with the same
+// constants, counters and rank -> key bijection as distributedratelimiting.redis_amd/
+// workloads.py (draw g of attempt a uses U[0,1) from stream STREAM_ZIPF + a at counter g).
+// The law is the same; ranks can differ from the numpy version where device and host
+// libm round log/exp differently right at an acceptance boundary, so tests copy the
+// device keys to the host instead of regenerating them there.
+constexpr uint64_t kStreamZipf = 0x3C3C3C3C3C3C3C3Cull;
+
+struct ZipfParams {
+    double s, h_x1, h_n, sq;
+    uint64_t n_items;
+    uint64_t mask;      // bijection domain [0, 2^bits)
+    uint32_t sh;        // xorshift of the bijection
+    uint32_t pad;
+};
+
+__device__ __forceinline__ double zipf_helper1(double x) {
+    return fabs(x) > 1e-8 ? log1p(x) / x : 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x));
+}
+__device__ __forceinline__ double zipf_helper2(double x) {
+    return fabs(x) > 1e-8 ? expm1(x) / x : 1.0 + x * 0.5 * (1.0 + x * (1.0 / 3.0) * (1.0 + 0.25 * x));
+}
+__device__ __forceinline__ double zipf_h(double x, double s) { return exp(-s * log(x)); }
+__device__ __forceinline__ double zipf_hint(double x, double s) {
+    const double lx = log(x);
+    return zipf_helper2((1.0 - s) * lx) * lx;
+}
+__device__ __forceinline__ double zipf_hinv(double x, double s) {
+    const double t = fmax(x * (1.0 - s), -1.0);
+    return exp(zipf_helper1(t) * x);
+}
+__device__ __forceinline__ uint64_t zipf_scramble(uint64_t x, uint64_t mask, uint32_t sh) {
+    x = (x * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) & mask;
+    x ^= x >> sh;
+    x = (x * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull) & mask;
+    x ^= x >> sh;
+    x = (x * 0xAEF17502108EF2D9ull + 0x2545F4914F6CDD1Dull) & mask;
+    x ^= x >> sh;
+    return x;
+}
+
+__global__ void k_gen_zipf(uint64_t seed, ZipfParams Z, uint64_t g0, uint64_t n, uint64_t *__restrict__ keys) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t g = g0 + i;
+        double k = 1.0;
+        for (uint64_t a = 0; a < 64; ++a) {   // acceptance > 0.9 per attempt
+            const uint64_t r = mix64((seed ^ (kStreamZipf + a)) + g * kGamma);
+            const double u01 = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+            const double u = Z.h_n + u01 * (Z.h_x1 - Z.h_n);
+            const double x = zipf_hinv(u, Z.s);
+            k = fmin(fmax(floor(x + 0.5), 1.0), (double)Z.n_items);
+            if (k - x <= Z.sq || u >= zipf_hint(k + 0.5, Z.s) - zipf_h(k, Z.s)) break;
+        }
+        uint64_t key = zipf_scramble((uint64_t)k - 1, Z.mask, Z.sh);
+        while (key >= Z.n_items) key = zipf_scramble(key, Z.mask, Z.sh);   // cycle walking
+        keys[i] = key;
+    }
+}
+
 }  // namespace
+
+static double host_helper1(double x) {
+    return std::fabs(x) > 1e-8 ? std::log1p(x) / x : 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x));
+}
+static double host_helper2(double x) {
+    return std::fabs(x) > 1e-8 ? std::expm1(x) / x : 1.0 + x * 0.5 * (1.0 + x * (1.0 / 3.0) * (1.0 + 0.25 * x));
+}
+
+extern "C" int tbe_gen_zipf_keys_device(uint64_t seed, uint64_t n_items, double s, uint64_t g0, uint64_t n,
+                                        uint64_t *d_keys, void *stream) {
+    if (n == 0) return 0;
+    if (n_items == 0 || n_items > (1ull << 40) || !(s > 0.0) || s == 1.0 || !d_keys) return 1;
+    auto hint = [&](double x) { const double lx = std::log(x); return host_helper2((1.0 - s) * lx) * lx; };
+    auto hinv = [&](double x) { return std::exp(host_helper1(std::fmax(x * (1.0 - s), -1.0)) * x); };
+    auto h = [&](double x) { return std::exp(-s * std::log(x)); };
+    ZipfParams Z{};
+    Z.s = s;
+    Z.h_x1 = hint(1.5) - 1.0;
+    Z.h_n = hint((double)n_items + 0.5);
+    Z.sq = 2.0 - hinv(hint(2.5) - h(2.0));
+    Z.n_items = n_items;
+    int bits = 1;
+    while (bits < 64 && ((n_items - 1) >> bits) != 0) ++bits;
+    Z.mask = (bits >= 64) ? ~0ull : ((1ull << bits) - 1);
+    Z.sh = (uint32_t)(bits / 2 > 1 ? bits / 2 : 1);
+    const unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+    k_gen_zipf<<<blocks, 256, 0, (hipStream_t)stream>>>(seed, Z, g0, n, d_keys);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+extern "C" int tbe_numfmt_device(const double *d_in, double *d_out, uint64_t n, void *stream) {
+    if (n == 0) return 0;
+    const unsigned blocks = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    k_numfmt<<<blocks, 256, 0, (hipStream_t)stream>>>(d_in, d_out, n);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 extern "C" int tbe_gen_batch_device(uint64_t seed, uint64_t n_keys, uint64_t g0, uint64_t n,
                                     int32_t p_lo, int32_t p_hi, int64_t ts0_us, int64_t interval_us,

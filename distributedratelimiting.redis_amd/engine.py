@@ -58,7 +58,7 @@ class TokenBucketEngine:
     def __init__(self, n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
                  device: int = -1, stage_timing: bool = False, max_batch: int = 0,
                  queue_limit: int = 0, queue_order: int = 0, pack: bool = True, hot: bool = True,
-                 pipeline: bool = True, narrow: bool = True):
+                 pipeline: bool = True, narrow: bool = True, zero_wait_slots: int = 0):
         self._lib = _capi.load()
         flags = _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0
         if not pack:
@@ -72,7 +72,7 @@ class TokenBucketEngine:
         self.config = _capi.make_config(n_keys, token_limit, tokens_per_period, period_ticks,
                                         kind=self.KIND, queue_limit=queue_limit,
                                         queue_order=queue_order, device=device, flags=flags,
-                                        max_batch=max_batch)
+                                        max_batch=max_batch, zero_wait_slots=zero_wait_slots)
         h = c_void_p()
         st = self._lib.tbe_create(byref(self.config), byref(h))
         if st != _capi.TBE_OK:
@@ -273,7 +273,7 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
         return keys, ids, rem
 
     def queue_of(self, key: int):
-        cap = max(1, self.queue_limit)
+        cap = max(1, self.queue_limit) + getattr(self, "zero_wait_slots", 0)
         ids = np.empty(cap, dtype=np.int64)
         ps = np.empty(cap, dtype=np.int32)
         cnt = c_uint32()
@@ -305,6 +305,13 @@ class ApproximateEngine(QueueingTokenBucketEngine):
     all-reduce for one node-wide client) -> ``sync`` (A:439-508)."""
 
     KIND = _capi.TBE_KIND_APPROXIMATE
+
+    def __init__(self, n_keys: int, token_limit: int, tokens_per_period: int, period_ticks: int,
+                 queue_limit: int, queue_order: int = 0, zero_wait_slots: int = 4, **kw):
+        """zero_wait_slots: queue entries per key for zero-permit waits (tbe.h)."""
+        super().__init__(n_keys, token_limit, tokens_per_period, period_ticks, queue_limit,
+                         queue_order, zero_wait_slots=zero_wait_slots, **kw)
+        self.zero_wait_slots = zero_wait_slots
 
     def acquire_batch(self, keys, permits, wait: bool = True, id_base: int = 0):
         """Returns (status u8, available i32, evicted (cause index, request id))."""
@@ -359,6 +366,28 @@ class ApproximateEngine(QueueingTokenBucketEngine):
             self._check(self._lib.tbe_refresh_log(self.handle, keys.ctypes.data, ids.ctypes.data,
                                                   rem.ctypes.data, m, byref(nw)))
         return keys, ids, rem
+
+    def export_global(self, first: int = 0, count: Optional[int] = None):
+        """Replica of the global tier (tbe_approx_export_state): (v, p, t_us), t_us =
+        INT64_MIN for absent keys."""
+        if count is None:
+            count = self.n_keys - first
+        v = np.empty(count, dtype=np.float64)
+        p = np.empty(count, dtype=np.float64)
+        t = np.empty(count, dtype=np.int64)
+        self._check(self._lib.tbe_approx_export_state(self.handle, first, count, v.ctypes.data,
+                                                      p.ctypes.data, t.ctypes.data))
+        return v, p, t
+
+    def import_global(self, v, p, t_us, first: int = 0) -> None:
+        """Restore rows of the global-tier replica (tbe_approx_import_state)."""
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        t_us = np.ascontiguousarray(t_us, dtype=np.int64)
+        if not (v.shape == p.shape == t_us.shape):
+            raise ValueError("v, p and t_us must have the same length")
+        self._check(self._lib.tbe_approx_import_state(self.handle, first, v.shape[0], v.ctypes.data,
+                                                      p.ctypes.data, t_us.ctypes.data))
 
     def local_state(self, key: int):
         """(local, global, est, available, queued) of one key."""

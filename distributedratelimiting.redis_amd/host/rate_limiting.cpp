@@ -159,6 +159,7 @@ public:
         c.queue_order = (int32_t)o.QueueProcessingOrder;
         c.device = o.Device;
         c.max_batch = o.MaxBatch;
+        c.zero_wait_slots = kind == TBE_KIND_APPROXIMATE ? o.ZeroWaitSlots : 0;
         const tbe_status st = tbe_create(&c, &eng_);
         if (st == TBE_EINVAL) throw ArgumentException(std::string("invalid limiter options: ") + tbe_last_error(nullptr), "options");
         if (st != TBE_OK) throw RateLimiterEngineException(st, std::string("tbe_create failed: ") + tbe_last_error(nullptr));

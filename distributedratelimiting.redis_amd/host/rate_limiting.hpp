@@ -168,6 +168,9 @@ struct RedisQueueingTokenBucketRateLimiterOptions : RedisTokenBucketRateLimiterO
     // Timer-driven replenishment every ReplenishmentPeriod (the reference's timer);
     // false: call TryReplenish() yourself (as System.Threading.RateLimiting allows).
     bool AutoReplenishment = true;
+    // Approximate limiter only: queue entries per key kept for zero-permit waits, which
+    // the reference queues without bound while throttled (A:127-181; include/tbe.h).
+    int ZeroWaitSlots = 4;
 };
 
 // RedisApproximateTokenBucketRateLimiterOptions (ApproximateTokenBucket/...Options.cs).

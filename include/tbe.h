@@ -64,6 +64,11 @@ typedef struct tbe_config {
     int32_t device;                       /* HIP device ordinal; -1 = current device */
     uint32_t flags;                       /* TBE_FLAG_* */
     uint64_t max_batch;                   /* expected largest batch (workspace pre-sizing); 0 = grow on demand */
+    int32_t zero_wait_slots;              /* approximate kind: queue entries per key for zero-permit
+                                             waits (A:127-181; see tbe_approx_acquire_batch); 0 for
+                                             the other kinds.  max(1, queue_limit) + zero_wait_slots
+                                             <= 65535 */
+    int32_t reserved;                     /* 0 */
 } tbe_config;
 
 #define TBE_FLAG_STAGE_TIMING 0x1u        /* record per-stage HIP events (tbe_stage_times) */
@@ -244,7 +249,12 @@ tbe_status tbe_queue_cancel(tbe_engine *engine, const uint64_t *keys, const int6
  * decision (-1 for REJECTED). */
 
 /* wait = 0: AcquireCore (A:84-113, never queues); wait = 1: WaitAsyncCore (A:116-183).
- * A zero-permit request that cannot lease is FAILED, never queued. */
+ * A zero-permit wait while AvailableTokens is 0 queues with Count 0 (A:127-181: TryLease
+ * fails on `availableTokens != 0` and `QueueLimit - _queueCount < 0` never holds), holds
+ * no queue permits, completes at the first drain that reaches it (A:474: AvailableTokens
+ * >= 0) and is evicted from the head like any registration (A:145-156).  The reference
+ * queues any number of them; a key holds at most tbe_config.zero_wait_slots, beyond which
+ * the wait is FAILED. */
 tbe_status tbe_approx_acquire_batch(tbe_engine *engine, const uint64_t *keys, const int32_t *permits,
                                     uint64_t n, int32_t wait, int64_t id_base, uint8_t *status,
                                     int32_t *available, uint64_t *n_evicted);
@@ -279,6 +289,18 @@ tbe_status tbe_approx_refresh(tbe_engine *engine, int64_t ts_us, uint64_t *n_gra
  * _instanceCountEstimate, AvailableTokens (GetAvailablePermits, A:81), queued requests. */
 tbe_status tbe_approx_query(tbe_engine *engine, uint64_t key, int32_t *local, int32_t *global_score,
                             double *est, int32_t *available, uint32_t *queued);
+
+/* Snapshot/restore of the approximate kind's replica of the global tier: per key the
+ * Redis hash {v, p, t} that the sync script writes with a one-day TTL (A:265-268);
+ * t_us[k] is the injected TIME of the key's last sync, INT64_MIN when absent (then v = p
+ * = 0, the script's default, A:250-252).  The local tier is in-process state in the
+ * reference (A:36-40) and is not part of it.  Import: t_us must be INT64_MIN or >= 0;
+ * both calls are ordered after every batch and sync enqueued before them.  Every rank of
+ * a node imports the same snapshot so that the replicas stay identical. */
+tbe_status tbe_approx_export_state(tbe_engine *engine, uint64_t first, uint64_t count, double *v,
+                                   double *p, int64_t *t_us);
+tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t count, const double *v,
+                                   const double *p, const int64_t *t_us);
 
 /* How the engine lays a batch out (for reports and tests): *passes = 8-bit partition
  * passes over the bucket id, *r_bits = log2 of the keys per bucket (one workgroup

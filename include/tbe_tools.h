@@ -24,6 +24,17 @@ int tbe_gen_batch_device(uint64_t seed, uint64_t n_keys, uint64_t g0, uint64_t n
                          int32_t p_hi, int64_t ts0_us, int64_t interval_us, uint64_t *d_keys,
                          int32_t *d_permits, int64_t *d_ts, void *stream);
 
+/* n keys of a bounded Zipf(s) stream over [0, n_items) (rank 1 hottest; ranks mapped to
+ * keys by the fixed bijection of workloads.py), draws g0 .. g0+n-1, by rejection-
+ * inversion.  s > 0, s != 1.  Enqueued on `stream`; returns 0 on success. */
+int tbe_gen_zipf_keys_device(uint64_t seed, uint64_t n_items, double s, uint64_t g0, uint64_t n,
+                             uint64_t *d_keys, void *stream);
+
+/* out[i] = the engine's device round trip of in[i] through Lua tostring ("%.14g") and
+ * C# double.Parse (csrc/tbe_numfmt.hpp; A:270 -> A:442), for parity tests of the gfx950
+ * build.  Enqueued on `stream`; returns 0 on success. */
+int tbe_numfmt_device(const double *d_in, double *d_out, uint64_t n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -362,8 +362,11 @@ class QueueingTokenBucketTable:
 #   WaitAsyncCore          A:116-183 (async: may queue)
 #   TryLeaseUnsynchronized A:185-214
 #   RefreshAsync           A:412-508 (swap local -> count, sync script, drain)
-# Decision: a zero-permit WaitAsync that cannot lease is FAILED instead
-# of queued (the reference would queue it with no bound).
+# Zero-permit WaitAsync while throttled (A:127-181): TryLease fails (availableTokens != 0)
+# and `QueueLimit - _queueCount < 0` never holds, so the registration queues with Count 0,
+# holds no queue permits and completes at the first drain that reaches it (A:474:
+# AvailableTokens >= 0).  The reference queues any number of them;
+# the build gives each key `zero_slots` of them, beyond which the wait FAILS.
 AP_FAILED, AP_GRANTED, AP_QUEUED, AP_REJECTED = 0, 1, 2, 3
 INT32_MIN, INT32_MAX = -(2 ** 31), 2 ** 31 - 1
 
@@ -394,7 +397,7 @@ class ApproxClient:
     """One client process's local tier for every key (A:9-599)."""
 
     def __init__(self, token_limit: int, tokens_per_period: int, period_ticks: int,
-                 queue_limit: int, order: int):
+                 queue_limit: int, order: int, zero_slots: int = 4):
         if token_limit <= 0 or tokens_per_period <= 0:
             raise ValueError("Both TokenLimit and TokensPerPeriod must be set to values greater than 0.")
         if queue_limit < 0:
@@ -404,6 +407,7 @@ class ApproxClient:
         self.token_limit = token_limit
         self.queue_limit = queue_limit
         self.order = order
+        self.zero_slots = zero_slots
         self.period_seconds = float(period_ticks) / float(TICKS_PER_SECOND)
         self.decay_rate = fill_rate_per_second(tokens_per_period, period_ticks)
         self.keys: Dict[int, ApproxLocal] = {}
@@ -457,7 +461,11 @@ class ApproxClient:
         if self.try_lease(s, p):
             return AP_GRANTED, []
         if p == 0:
-            return AP_FAILED, []          # build decision: zero permits never queue
+            # queued with Count 0 (A:141 never fails for 0); bounded by zero_slots per key
+            if sum(1 for e in s.queue if e.permits == 0) >= self.zero_slots:
+                return AP_FAILED, []
+            s.queue.append(QueueEntry(request_id, 0))
+            return AP_QUEUED, []
         evicted = []
         if self.queue_limit - s.qcount < p:
             if self.order == NEWEST_FIRST and p <= self.queue_limit:

@@ -60,3 +60,164 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait):
                 lo, gl, est, av, q = engines[r].local_state(key)
                 s = clients[r].st(key)
                 assert (lo, gl, est, av, q) == (s.local, s.global_, s.est, clients[r].available(s), len(s.queue))
+
+
+GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
+                                    "golden")
+
+
+@pytest.mark.parametrize("name", ["approx_one_client", "approx_eight_clients", "approx_slow_decay"])
+def test_golden_sync_trace_on_gpu(engine_lib, gpu, name):
+    """The reference's sync script replayed by Lua (tests/golden/make_golden.py): each
+    recorded ScriptEvaluateAsync(_syncScript, {BucketId, LocalCount}) call (A:439) runs as
+    one tbe_approx_sync on the device; _globalThrottleScore (A:441) and the estimate built
+    from the "%.14g" period string (A:442-443) must match after every call, and the
+    replica's final {v, p, t} must equal the script's hash (A:265)."""
+    import os
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    from oracle.semantics import instance_count_estimate, new_t_of
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    ticks = int(g["period_ticks"])
+    eng = ApproximateEngine(1, 1000, int(g["tokens_per_period"]), ticks, 0, 0, device=0)
+    from distributedratelimiting.redis_amd import fill_rate
+    assert fill_rate(int(g["tokens_per_period"]), ticks) == float(g["decay_rate"])
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    for i in range(len(g["counts"])):
+        cnt.fill_(int(g["counts"][i]))
+        eng.sync(cnt, 1, 0, int(g["ts_us"][i]), 0)
+        _, gl, est, _, _ = eng.local_state(0)
+        assert gl == int(g["global_score"][i]), i
+        want = instance_count_estimate(ticks / 1e7, float(g["period"][i]))
+        assert est == want or (est != est and want != want), (i, est, want)
+    v, p, t = eng.export_global()
+    assert (v[0], p[0], new_t_of(int(t[0]))) == (g["final_v"], g["final_p"], g["final_t"])
+
+
+def test_numfmt_round_trip_on_device(engine_lib, gpu):
+    """round_trip_14g as compiled for gfx950 (tbe_numfmt_device) == Python float("%.14g" % x)
+    on the inputs of tests/test_numfmt.py (the CPU test compiles the same header with g++)."""
+    import importlib.util
+    import os
+    import torch
+    from distributedratelimiting.redis_amd import _capi
+    spec = importlib.util.spec_from_file_location("_numfmt_cases", os.path.join(os.path.dirname(__file__),
+                                                                                "test_numfmt.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    xs = np.array(mod.values() + [0.0, -0.0, float("inf"), 0.5e-9, 2e23, -0.3], dtype=np.float64)
+    d_in = torch.from_numpy(xs).to(gpu)
+    d_out = torch.empty_like(d_in)
+    assert _capi.load().tbe_numfmt_device(d_in.data_ptr(), d_out.data_ptr(), xs.size, None) == 0
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    inside = (np.abs(xs) >= 1e-9) & (np.abs(xs) < 1e23)
+    want = np.array([float("%.14g" % x) for x in xs[inside]])
+    bad = np.flatnonzero(got[inside].view(np.uint64) != want.view(np.uint64))
+    assert bad.size == 0, list(zip(xs[inside][bad[:5]], got[inside][bad[:5]], want[bad[:5]]))
+    assert got[~inside][:3].tolist() == [0.0, 0.0, float("inf")]   # passed through
+    assert inside.sum() > 500_000
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+def test_zero_permit_waits_queue(engine_lib, gpu, order):
+    """WaitAsync(0) while AvailableTokens is 0 queues with Count 0 (A:127-181), holds no
+    queue permits, completes at the next drain that reaches it (A:474), is evicted from the
+    head like any registration (A:145-156) and can be canceled; zero_wait_slots bounds
+    them per key.  Hand-checked, and against the Python restatement."""
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    eng = ApproximateEngine(4, 2, 2, 10_000_000, 2, order, device=0, zero_wait_slots=2)
+    cli = ApproxClient(2, 2, 10_000_000, 2, order, zero_slots=2)
+    reqs = [(1, 2), (1, 0), (1, 0), (1, 0), (1, 1), (1, 1), (1, 2), (2, 0)]
+    keys = np.array([k for k, _ in reqs], np.uint64)
+    ps = np.array([p for _, p in reqs], np.int32)
+    st, av, (cause, ids) = eng.acquire_batch(keys, ps, wait=True, id_base=100)
+    exp = [cli.wait(k, p, 100 + i) for i, (k, p) in enumerate(reqs)]
+    assert st.tolist() == [e[0] for e in exp]
+    assert list(zip(cause.tolist(), ids.tolist())) == [(i, x) for i, e in enumerate(exp) for x in e[1]]
+    # key 1: granted 2, two zero waits queue, the third finds no zero slot; p=1, p=1 queue
+    # (qsum 2); p=2: OldestFirst fails, NewestFirst evicts the head run (zeros included)
+    # until 2 permits fit; key 2 has tokens: a zero wait is granted at once
+    if order == OLDEST_FIRST:
+        assert st.tolist() == [1, 2, 2, 0, 2, 2, 0, 1]
+    else:
+        assert st.tolist() == [1, 2, 2, 0, 2, 2, 2, 1] and ids.tolist() == [101, 102, 104, 105]
+    assert [q for q in eng.queue_of(1)] == [(e.request_id, e.permits) for e in cli.st(1).queue]
+    # a cancel of a queued zero wait (OldestFirst only has one left to cancel here)
+    if order == OLDEST_FIRST:
+        assert eng.cancel(np.array([1], np.uint64), np.array([102], np.int64)).tolist() == [1]
+        assert cli.cancel(1, 102)
+    counts = torch.zeros(4, dtype=torch.int32, device=gpu)
+    tbl = ApproxGlobalTable(cli.decay_rate)
+    ts = S_US
+    for epoch in range(3):
+        ts += 1_000_000
+        eng.collect(counts)
+        log = eng.sync(counts, 1, 0, ts, 0)
+        exp_log = approx_refresh_all([cli], tbl, ts, 0, range(4))[0]
+        assert list(zip(log[0].tolist(), log[1].tolist())) == exp_log
+        for key in range(4):
+            lo, gl, est, a, q = eng.local_state(key)
+            s = cli.st(key)
+            assert (lo, gl, est, a, q) == (s.local, s.global_, s.est, cli.available(s), len(s.queue))
+
+
+def test_global_tier_snapshot_restore(engine_lib, gpu):
+    """tbe_approx_export_state -> tbe_approx_import_state (the Redis hash {v, p, t} with
+    its one-day TTL, A:265-268): a replica restored into a fresh engine continues the
+    sync replay exactly like the original; absent rows of a snapshot (t = INT64_MIN) read
+    back as the script's default {0, 0} and behave like never-synced keys."""
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine, TbeError
+    ABS = np.iinfo(np.int64).min
+    n_keys, half = 5000, 2500
+    mk = lambda: ApproximateEngine(n_keys, 50, 10, 10_000_000, 0, 0, device=0)
+    a = mk()
+    rng = np.random.default_rng(8)
+    counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    v0, p0, t0 = a.export_global()
+    assert (t0 == ABS).all() and (v0 == 0).all() and (p0 == 0).all()
+    ts = S_US
+    for epoch in range(3):
+        keys = rng.integers(0, n_keys, 20_000).astype(np.uint64)
+        a.acquire_batch(keys, rng.integers(0, 4, keys.size).astype(np.int32), wait=False)
+        ts += 700_000
+        a.collect(counts)
+        a.sync(counts, 1, 0, ts, 0)
+    v, p, t = a.export_global()
+    assert (t == ts).all() and (p > 0).any()          # every key syncs every epoch (A:412-508)
+    b = mk()                                          # restored in two ranges
+    b.import_global(v[:100], p[:100], t[:100])
+    b.import_global(v[100:], p[100:], t[100:], first=100)
+    for x, y in zip(b.export_global(), (v, p, t)):
+        assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+    c = mk()                                          # upper half absent in the snapshot
+    t2 = t.copy()
+    t2[half:] = ABS
+    c.import_global(np.full(n_keys, 7.0), np.full(n_keys, 3.0), t2)
+    c.import_global(v[:half], p[:half], t[:half])
+    vc, pc, tc = c.export_global()
+    assert (tc[half:] == ABS).all() and (vc[half:] == 0).all() and (pc[half:] == 0).all()
+    d = mk()                                          # lower half restored, upper never synced
+    d.import_global(v[:half], p[:half], t[:half])
+    for epoch in range(2):
+        cn = torch.from_numpy(rng.integers(0, 30, n_keys).astype(np.int32)).to(gpu)
+        ts += 900_000
+        for e in (a, b, c, d):
+            e.sync(cn, 1, 0, ts, 0)
+        for x, y in zip(a.export_global(), b.export_global()):
+            assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+        for x, y in zip(c.export_global(), d.export_global()):
+            assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+        for key in range(0, n_keys, 37):
+            assert a.local_state(key)[1:3] == b.local_state(key)[1:3]
+            assert c.local_state(key)[1:3] == d.local_state(key)[1:3]
+    # past the one-day TTL every key is absent again: the next sync starts from {0, 0, now}
+    day = 86_400 * 1_000_000
+    b.sync(torch.zeros(n_keys, dtype=torch.int32, device=gpu), 1, 0, ts + day + 2_000, 0)
+    vb, pb, _ = b.export_global()
+    assert (pb == 0.0).all() and (vb == 0.0).all()
+    with pytest.raises(TbeError):
+        b.import_global(v[:10], p[:10], t[:10], first=n_keys - 5)

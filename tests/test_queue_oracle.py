@@ -114,3 +114,34 @@ def test_cancel_invariants(order):
         t += int(rng.integers(0, 900_000))
         assert not canceled & {x for _, x, _ in q.refresh(t)}
     assert canceled
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+def test_c_queue_multithreaded_matches_serial(oracle_lib, order):
+    """tbrq_*_mt (key-sharded, used by the full-size GPU parity tests) == serial tbrq_*:
+    statuses, remaining, eviction logs (sorted by cause, id), tick logs and final state."""
+    from distributedratelimiting.redis_amd import fill_rate
+    n_keys, n = 3000, 40_000
+    rate = fill_rate(2, 10_000_000)
+    a = cref.CQueueingTokenBucket(n_keys, 4, rate, 6, order)
+    b = cref.CQueueingTokenBucket(n_keys, 4, rate, 6, order)
+    rng = np.random.default_rng(order + 5)
+    t = S_US
+    for r in range(4):
+        k = rng.integers(0, n_keys, n).astype(np.uint64)
+        p = rng.choice([0, 1, 1, 2, 3, 5], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 400_000, n))).astype(np.int64)
+        t += 400_000
+        sa, ra, ca, ia = a.acquire_batch(k, p, ts, r * n)
+        sb, rb, cb, ib = b.acquire_batch(k, p, ts, r * n, threads=5)
+        o = np.lexsort((ia, ca))
+        assert np.array_equal(sa, sb) and np.array_equal(ra, rb)
+        assert np.array_equal(ca[o], cb) and np.array_equal(ia[o], ib)
+        la = a.refresh(t)
+        lb = b.refresh(t, threads=7)
+        for x, y in zip(la, lb):
+            assert np.array_equal(x, y)
+    for x, y in zip(a.bucket_state(), b.bucket_state()):
+        assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+    for key in range(0, n_keys, 97):
+        assert a.queue_of(key) == b.queue_of(key)

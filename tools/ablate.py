@@ -15,10 +15,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
-    # name: (build defines, extra bench args)
-    "base": ([], []),
-    "slice_load_cached": (["TBE_SLICE_LOAD_CACHED"], []),
-    "zipf": ([], ["--workload", "zipf", "--zipf-batches", "1"]),
+    # name: (build defines, extra bench args); steady state: 15 warm-up batches age the
+    # table into config B's denial-dominated regime before the timed ones
+    "base_steady": ([], ["--warmup", "15"]),
+    "narrow_only_steady": (["TBE_FOLD_NARROW_ONLY"], ["--warmup", "15"]),
+    "approx_base": ([], ["--workload", "approx"]),
+    "approx_dense_nt": (["TBE_APPROX_DENSE"], ["--workload", "approx"]),
+    "approx_dense_plain": (["TBE_APPROX_DENSE", "TBE_APPROX_DENSE_PLAIN"], ["--workload", "approx"]),
 }
 
 
@@ -42,16 +45,19 @@ def run(rounds: int, steps: int):
         for name, (_, extra) in VARIANTS.items():
             defs = VARIANTS[name][0]
             env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs) or 'base'}.so"))
-            out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps),
-                                  "--warmup", "2", "--cpu-seconds", "0"] + extra, env=env, capture_output=True,
-                                 text=True, timeout=300)
+            args = ["--steps", str(steps), "--cpu-seconds", "0", "--no-host-buffer"]
+            if "--warmup" not in extra:
+                args += ["--warmup", "2"]
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + extra, env=env,
+                                 capture_output=True, text=True, timeout=300)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")]
             if not line:
                 print(name, "FAILED", out.stderr[-2000:])
                 continue
             d = json.loads(line[0])
             results.setdefault(name, []).append(d["stage_ms_per_step"])
-            print(r, name, d["ms_per_step"], d["stage_ms_per_step"], flush=True)
+            print(r, name, d["ms_per_step"], d["stage_ms_per_step"],
+                  (d.get("roofline") or {}).get("avg_launch_ms"), flush=True)
     print(json.dumps(results))
 
 

@@ -44,6 +44,7 @@ def main():
             # median per dispatch: robust to warm-up dispatches (a Zipf run's first batches
             # fold hot keys in their buckets before the hot set exists)
             d = {c: sorted(v)[len(v) // 2] for c, v in agg[w][k].items()}
+            d["dispatches"] = max(len(v) for v in agg[w][k].values())
             if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
                 d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
             out[k] = d
@@ -60,12 +61,30 @@ def main():
         # summed; other stages are one kernel per pass, averaged over the passes
         if st != "fold":
             e["hbm_bytes_per_launch"] /= len(e["kernels"])
+    # whole-step HBM bytes: every pipeline kernel's median bytes per launch times its
+    # average launches per batch (dispatches / dispatches of the fold kernel)
+    step = {}
+    marker = {"uniform": "k_fold_wide<true>", "zipf": "k_fold_wide<true>", "queue": "k_fold_q",
+              "approx": "k_fold_a"}
+    skip = ("k_gen_batch", "k_init_table", "k_init_approx", "k_count_queued", "k_gen_zipf")
+    for w, kern in by_w.items():
+        m = kern.get(marker.get(w, ""), {}).get("dispatches")
+        if not m:
+            continue
+        tot = 0.0
+        for k, d in kern.items():
+            if k.split("<")[0] in skip or "hbm_bytes_per_launch" not in d:
+                continue
+            tot += d["hbm_bytes_per_launch"] * d["dispatches"] / m
+        step[w] = round(tot, 1)
+        print(w, "step HBM bytes", f"{tot:.4g}")
     if "--write" in sys.argv:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
             json.dump({"note": "per-launch medians; HBM bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB "
                                "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section); "
                                "stages = the token-bucket (uniform) path",
-                       **stages, "kernels": by_w.get("uniform", {}), "workloads": by_w}, f, indent=1)
+                       **stages, "step_hbm_bytes": step, "kernels": by_w.get("uniform", {}),
+                       "workloads": by_w}, f, indent=1)
 
 
 if __name__ == "__main__":
