@@ -746,6 +746,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
             }
         }
     };
+
     load_chunk(s);   // in flight together with the dense slice
     if (dense) {
         constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
@@ -765,6 +766,19 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
         loaded[j] = 0;
         dirty[j] = 0;
     }
+#ifdef TBE_FOLD_COPY_ONLY
+    // A/B floor (not a decision path): the fold's memory traffic without its rounds --
+    // records and slice in, the whole slice and one reply per request out
+    __syncthreads();
+    for (uint32_t c = s; c < e; c += kFoldChunk) {
+        if (c != s) load_chunk(c);
+#pragma unroll
+        for (int r = 0; r < kFoldPer; ++r)
+            if (pend & (1u << r)) put_reply(res, c + r * kFoldBlock + tid, kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
+    }
+    for (uint32_t j = tid; j < nrows; j += kFoldBlock) ST_S(rows + j, row[j]);
+    return;
+#endif
 
     for (uint32_t c = s; c < e; c += kFoldChunk) {
         if (c != s) load_chunk(c);

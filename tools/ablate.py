@@ -17,11 +17,11 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args); steady state: 15 warm-up batches age the
     # table into config B's denial-dominated regime before the timed ones
-    "base_steady": ([], ["--warmup", "15"]),
-    "narrow_only_steady": (["TBE_FOLD_NARROW_ONLY"], ["--warmup", "15"]),
-    "approx_base": ([], ["--workload", "approx"]),
-    "approx_dense_nt": (["TBE_APPROX_DENSE"], ["--workload", "approx"]),
-    "approx_dense_plain": (["TBE_APPROX_DENSE", "TBE_APPROX_DENSE_PLAIN"], ["--workload", "approx"]),
+    "walk": ([], []),
+    "rounds": ([], ["--no-walk"]),
+    "walk_steady": ([], ["--warmup", "15"]),
+    "rounds_steady": ([], ["--warmup", "15", "--no-walk"]),
+    "copy_only": (["TBE_FOLD_COPY_ONLY"], []),
 }
 
 

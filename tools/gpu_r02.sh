@@ -11,6 +11,11 @@ export PYTHONUNBUFFERED=1
 stop() { echo "[stop] $1 rc=$2"; exit "$2"; }
 fatal() { case "$1" in 124|134|137|139|-6|-11) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
 
+if [ "${WALK_FIRST:-0}" = 1 ]; then
+timeout -k 10 300 python -u -m pytest tests/test_gpu_walk.py -x -q --timeout 200 --timeout-method thread \
+    > "$OUT/r02_walk.log" 2>&1
+rc=$?; tail -3 "$OUT/r02_walk.log"; [ $rc -ne 0 ] && stop walk $rc
+fi
 if [ "${SKIP_SUITE:-0}" != 1 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     --ignore=tests/test_gpu_fullshape.py > "$OUT/r02_pytest_gpu.log" 2>&1
