@@ -51,8 +51,12 @@ def parse():
     ap.add_argument("--keys", type=int, default=None,
                     help="total keys (uniform, default 1e8) / keys per GPU (zipf, default 1.25e8)")
     ap.add_argument("--zipf-s", type=float, default=1.1)
-    ap.add_argument("--zipf-batches", type=int, default=2,
-                    help="distinct Zipf key batches drawn on the host, reused in turn")
+    ap.add_argument("--route", choices=("pre", "timed"), default="pre",
+                    help="N > 1: route each step's global requests to their owners before the timed "
+                         "region (ingest partitioned) or inside every timed step")
+    ap.add_argument("--approx-mode", choices=("clients", "node"), default="clients",
+                    help="config E with N > 1: every rank a client (all-gather) or the node as one "
+                         "client (all-reduce of the counts)")
     ap.add_argument("--batch", type=int, default=None, help="requests per batch (default 2^26; testapp 1M)")
     ap.add_argument("--interval-us", type=int, default=None,
                     help="injected time per batch (default 10 ms; 1 ms for queue)")
@@ -121,50 +125,79 @@ def main():
             td.destroy_process_group()
         return
 
-    # Hash partition: this rank owns keys_local = ceil(K / world) dense local ids.  The
-    # synthetic stream is generated directly in the rank's local id space (uniform keys
-    # stay uniform under a hash partition); seeds differ per rank.  Zipf (config C): each
-    # rank owns 1.25e8 keys (1e9 over 8 GPUs) and draws its own Zipf(1.1) stream over them.
+    # Key space and ownership.  One GPU owns every key, so the generated
+    # ids are its bucket ids.  With N ranks, every rank draws its share of ONE global
+    # request stream (uniform over 1e8 keys, or Zipf(1.1) over 1.25e8 * N keys for config C),
+    # and the requests go to their owners, owner = mix64(key) >> (64 - log2 N), whose key
+    # directories turn them into dense bucket ids (cluster.route_requests: stable
+    # partition + RCCL all-to-all + directory, all in HBM).  --route pre (default) routes
+    # before the timed region, i.e. ingest arrives partitioned (the benchmark mode of
+    # §8e); --route timed keeps the exchange, the directory and the replies' way back in
+    # every timed step.  Either way the hot keys of a Zipf stream load their owners
+    # unevenly, and the slowest rank sets the time.
     if args.workload == "zipf":
-        keys_local = args.keys or 125_000_000
-        keys_total = keys_local * world
+        keys_total = (args.keys or 125_000_000) * world
     else:
         keys_total = args.keys or (10_000 if args.workload == "testapp" else 100_000_000)
-        keys_local = (keys_total + world - 1) // world
+    from distributedratelimiting.redis_amd import cluster
+    keys_local = cluster.keys_per_rank(keys_total, world)
     n = args.batch
-    eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
-                            args.period_ticks, device=dev.index,
-                            stage_timing=not args.no_stage_timing, max_batch=n,
-                            pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
-                            pipeline=not args.no_pipeline)
-    layout = eng.layout()
     total_steps = args.warmup + args.steps
-    seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B) + 7919 * rank
-    zkeys = []
-    if args.workload == "zipf":
-        from distributedratelimiting.redis_amd import workloads
-        zs = workloads.ZipfSampler(keys_local, args.zipf_s)
-        for d in range(args.zipf_batches):
-            zk = workloads.zipf_keys(seed, keys_local, d * n, n, sampler=zs)
-            zkeys.append((zk, torch.from_numpy(zk.view(np.int64)).to(dev)))
-    bufs = []
+    routed = dist and args.workload != "testapp"
+    seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B)
+    directory = cluster.DeviceDirectory(keys_local, device=dev.index) if routed else None
+    bufs, raw = [], []
     for s in range(total_steps):
+        g0 = (s * world + rank) * n          # this rank's share of the global stream
         k = torch.empty(n, dtype=torch.int64, device=dev)
         p = torch.empty(n, dtype=torch.int32, device=dev)
         t = torch.empty(n, dtype=torch.int64, device=dev)
-        rc = lib.tbe_gen_batch_device(seed, keys_local, s * n, n, 1, 1, T0_US + s * args.interval_us,
+        rc = lib.tbe_gen_batch_device(seed, keys_total, g0, n, 1, 1, T0_US + s * args.interval_us,
                                       args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), None)
         assert rc == 0
-        if zkeys:
-            k.copy_(zkeys[s % len(zkeys)][1])
-        bufs.append((k, p, t))
-    granted = torch.empty(n, dtype=torch.uint8, device=dev)
-    remaining = torch.empty(n, dtype=torch.int32, device=dev)
+        if args.workload == "zipf":
+            assert lib.tbe_gen_zipf_keys_device(seed, keys_total, args.zipf_s, g0, n, k.data_ptr(), None) == 0
+        if routed and args.route == "pre":
+            (lk, lp, lt), _ = cluster.route_requests(k, p, t, directory)
+            bufs.append((lk, lp, lt))
+        elif routed:
+            raw.append((k, p, t))
+        else:
+            bufs.append((k, p, t))
     torch.cuda.synchronize()
+    sizes = [b[0].numel() for b in bufs] or [n]
+    m_max = max(sizes)
+    eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
+                            args.period_ticks, device=dev.index,
+                            stage_timing=not args.no_stage_timing, max_batch=m_max,
+                            pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
+                            pipeline=not args.no_pipeline)
+    layout = eng.layout()
+    granted = torch.empty(m_max if not raw else n, dtype=torch.uint8, device=dev)
+    remaining = torch.empty(m_max if not raw else n, dtype=torch.int32, device=dev)
+    zkeys = [bufs[s][0].cpu().numpy().view(np.uint64) for s in range(min(2, len(bufs)))] \
+        if args.workload == "zipf" and not routed else []
+    cur = torch.cuda.current_stream(dev).cuda_stream
+
+    def decide(lk, lp, lt):   # --route timed: the owner's engine on the routed requests
+        g = torch.empty(lk.numel(), dtype=torch.uint8, device=dev)
+        r = torch.empty(lk.numel(), dtype=torch.int32, device=dev)
+        eng.acquire_batch_device(lk, lp, lt, g, r, stream=cur)
+        return g, r
+
+    def step(s):
+        if raw:
+            g, r = cluster.route_batch(decide, *raw[s], directory)
+            granted.copy_(g)
+            remaining.copy_(r)
+        else:
+            m = bufs[s][0].numel()
+            eng.acquire_batch_device(*bufs[s], granted[:m], remaining[:m])
 
     for s in range(args.warmup):
-        eng.acquire_batch_device(*bufs[s], granted, remaining)
+        step(s)
     eng.synchronize()
+    torch.cuda.synchronize()
     eng.stage_times()  # discard warm-up stage times
 
     if dist:
@@ -172,24 +205,33 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_steps):
-        eng.acquire_batch_device(*bufs[s], granted, remaining)
+        step(s)
     eng.synchronize()
     torch.cuda.synchronize()
     if dist:
         td.barrier()
     elapsed = time.perf_counter() - t0
+    load = None
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # requests each owner decided in the timed steps: max / mean = the hash partition's
+        # imbalance (Zipf: the hot keys' owners)
+        mine = torch.tensor([float(sum(sizes[args.warmup:]))], dtype=torch.float64, device=dev)
+        every = torch.empty(world, dtype=torch.float64, device=dev)
+        td.all_gather_into_tensor(every, mine)
+        ev = every.cpu().numpy()
+        load = {"per_rank_requests": ev.tolist(), "max_over_mean": round(float(ev.max() / ev.mean()), 4)}
     stages_overlapped = eng.stage_times()
-    grant_rate = float(granted.float().mean().item())
+    m_last = (raw[-1][0] if raw else bufs[total_steps - 1][0]).numel()
+    grant_rate = float(granted[:m_last].float().mean().item())
     # SURVEY.md §8(d) B_alg of the last timed batch, measured: U = its distinct keys, W =
     # the distinct keys it wrote (granted at least once; a deny writes nothing, TB:225-236)
-    last_keys = bufs[total_steps - 1][0]
+    last_keys = raw[-1][0] if raw else bufs[total_steps - 1][0]
     u_meas = int(torch.unique(last_keys).numel())
-    w_meas = int(torch.unique(last_keys[granted.bool()]).numel())
-    step_alg = int(n * 25 + u_meas * 16 + w_meas * 16)
+    w_meas = int(torch.unique(last_keys[granted[:m_last].bool()]).numel())
+    step_alg = int(m_last * 25 + u_meas * 16 + w_meas * 16)
 
     decisions = n * args.steps * world
     value = decisions / elapsed
@@ -201,7 +243,7 @@ def main():
     # stream, pipeline off) of exactly the same warm-up + timed batches on a second engine,
     # right after the timed region; its replies must equal the pipelined run's.
     stages, replay_check = stages_overlapped, None
-    if layout.get("pipeline") and not args.no_stage_timing:
+    if layout.get("pipeline") and not args.no_stage_timing and not raw:
         eng.close()
         ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                                 args.period_ticks, device=dev.index, stage_timing=True,
@@ -210,14 +252,15 @@ def main():
         g2 = torch.empty_like(granted)
         r2 = torch.empty_like(remaining)
         for s in range(args.warmup):
-            ser.acquire_batch_device(*bufs[s], g2, r2)
+            ser.acquire_batch_device(*bufs[s], g2[:sizes[s]], r2[:sizes[s]])
         ser.synchronize()
         ser.stage_times()
         for s in range(args.warmup, total_steps):
-            ser.acquire_batch_device(*bufs[s], g2, r2)
+            ser.acquire_batch_device(*bufs[s], g2[:sizes[s]], r2[:sizes[s]])
         ser.synchronize()
         stages = ser.stage_times()
-        replay_check = bool(torch.equal(g2, granted) and torch.equal(r2, remaining))
+        replay_check = bool(torch.equal(g2[:m_last], granted[:m_last]) and
+                            torch.equal(r2[:m_last], remaining[:m_last]))
         eng = ser
 
     # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
@@ -230,7 +273,7 @@ def main():
         per_launch_ms = stages[name] / (args.steps * launches[name])
         distinct = None
         if zkeys:   # distinct keys per batch, measured (the uniform estimate does not apply)
-            distinct = float(np.mean([np.unique(zk).size for zk, _ in zkeys]))
+            distinct = float(np.mean([np.unique(zk).size for zk in zkeys]))
         own_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct,
                                       1 if layout.get("narrow") else 4)
         # achieved: §8(d)'s B_alg of one step (one batch = one launch of the dominant
@@ -280,20 +323,21 @@ def main():
             # the same batches from page-locked buffers (tbe_alloc_host): DMA, no staging copy
             from distributedratelimiting.redis_amd.engine import PinnedArray
             pk, pp, pt = PinnedArray(n, np.uint64), PinnedArray(n, np.int32), PinnedArray(n, np.int64)
+            pg, pr = PinnedArray(n, np.uint8), PinnedArray(n, np.int32)
             spent = 0.0
             for k, p, t in host[1:]:
                 pk.array[:], pp.array[:], pt.array[:] = k.view(np.uint64), p, t
                 t1 = time.perf_counter()
-                hb.acquire_batch(pk.array, pp.array, pt.array)
+                hb.acquire_batch(pk.array, pp.array, pt.array, pg.array, pr.array)   # chunked, overlapped
                 spent += time.perf_counter() - t1
             host_rate_pinned = round(n * (len(host) - 1) / spent, 1)
-            for a in (pk, pp, pt):
+            for a in (pk, pp, pt, pg, pr):
                 a.free()
         hb.close()
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, keys_local, [zk for zk, _ in zkeys],
+        cpu = cpu_baseline(args, keys_local, zkeys,
                            SEED_A if args.workload == "testapp" else SEED_B)
 
     if rank == 0:
@@ -309,16 +353,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("synthetic (Zipf keys drawn on the host, copied to HBM before timing; "
-                     "timestamps generated in HBM)" if zkeys else
+            "data": ("synthetic (Zipf(1.1) keys by rejection-inversion, splitmix64 counters, "
+                     "generated in HBM)" if args.workload == "zipf" else
                      "synthetic (splitmix64 seeded trace generated in HBM)"),
             "config": {"workload": workload_name(args, n),
                        "keys_total": keys_total, "keys_per_gpu": keys_local, "batch_per_gpu": n,
                        "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
                        "period_ticks": args.period_ticks, "interval_us": args.interval_us,
-                       "partitioning": f"key-hash x{world}, no data-path collective",
+                       "partitioning": ("one GPU owns every key" if world == 1 else
+                                        f"owner = mix64(key) >> (64 - log2 {world}); each rank draws its "
+                                        f"share of one global stream, routed to the owners "
+                                        + ("before the timed region (ingest partitioned, no "
+                                           "data-path collective timed)" if args.route == "pre" else
+                                           "inside every timed step (RCCL all-to-all both ways)")),
                        "layout": layout},
             "grant_rate_last_batch": round(grant_rate, 4),
+            **({"owner_load": load} if load is not None else {}),
             **({"host_buffer_decisions_per_s": host_rate} if host_rate is not None else {}),
             **({"host_buffer_pinned_decisions_per_s": host_rate_pinned}
                if host_rate_pinned is not None else {}),

@@ -257,11 +257,17 @@ def run_approx(args, lib, dev, world, rank, dist):
             torch.cuda.synchronize()
         t1 = time.perf_counter()
         eng.collect(counts)             # A:430-435
-        if dist:
+        if dist and args.approx_mode == "node":
             import torch.distributed as td
-            td.all_gather_into_tensor(allc, counts)   # RCCL over xGMI
-            torch.cuda.current_stream(dev).synchronize()   # the sync replay reads allc
-        eng.sync(allc, world, rank, T0_US + (s + 1) * args.interval_us, stagger)
+            td.all_reduce(counts)                     # RCCL over xGMI: the node is ONE client
+            torch.cuda.current_stream(dev).synchronize()
+            eng.sync(counts, 1, 0, T0_US + (s + 1) * args.interval_us, 0)
+        else:
+            if dist:
+                import torch.distributed as td
+                td.all_gather_into_tensor(allc, counts)   # RCCL over xGMI
+                torch.cuda.current_stream(dev).synchronize()   # the sync replay reads allc
+            eng.sync(allc, world, rank, T0_US + (s + 1) * args.interval_us, stagger)
         if timed:
             refresh_s[0] += time.perf_counter() - t1
 
@@ -310,7 +316,10 @@ def run_approx(args, lib, dev, world, rank, dist):
                    "keys_shared": kshared, "batch_per_gpu": n, "token_limit": args.token_limit,
                    "tokens_per_period": args.tokens_per_period, "period_ticks": args.period_ticks,
                    "interval_us": args.interval_us, "clients": world,
-                   "exchange": "RCCL all-gather of int32 counts" if dist else "none (one client)"},
+                   "exchange": ("none (one client)" if not dist else
+                                "RCCL all-reduce of int32 counts (the node is one client, SURVEY.md §8e option 1)"
+                                if args.approx_mode == "node" else
+                                "RCCL all-gather of int32 counts (every rank a client, §8e option 2)")},
         "granted_frac_last_batch": round(granted, 4),
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
         "refresh_ms_per_step_wall": round(refresh_s[0] / steps * 1e3, 4),

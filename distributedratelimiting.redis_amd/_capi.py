@@ -151,6 +151,27 @@ def load(path: str = None) -> ctypes.CDLL:
                                              c_void_p]
     lib.tbe_gen_batch_device.restype = c_int32
     lib.tbe_gen_batch_device.argtypes = [c_uint64] * 4 + [c_int32] * 2 + [c_int64] * 2 + [c_void_p] * 4
+    # multi-GPU path (include/tbe_cluster.h)
+    lib.tbe_key_owner.restype = c_uint32
+    lib.tbe_key_owner.argtypes = [c_uint64, c_uint32]
+    lib.tbe_route_workspace_bytes.restype = c_uint64
+    lib.tbe_route_workspace_bytes.argtypes = [c_uint64, c_uint32]
+    lib.tbe_route_plan_device.restype = c_int32
+    lib.tbe_route_plan_device.argtypes = [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.tbe_route_pack_device.restype = c_int32
+    lib.tbe_route_pack_device.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.tbe_route_gather_device.restype = c_int32
+    lib.tbe_route_gather_device.argtypes = [c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_void_p]
+    lib.tbe_dir_create.restype = c_int32
+    lib.tbe_dir_create.argtypes = [c_uint64, c_int32, POINTER(c_void_p)]
+    lib.tbe_dir_destroy.restype = None
+    lib.tbe_dir_destroy.argtypes = [c_void_p]
+    lib.tbe_dir_assign_device.restype = c_int32
+    lib.tbe_dir_assign_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
+    lib.tbe_dir_lookup_device.restype = c_int32
+    lib.tbe_dir_lookup_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
+    lib.tbe_dir_size.restype = c_int32
+    lib.tbe_dir_size.argtypes = [c_void_p, POINTER(c_uint64)]
     lib.tbe_numfmt_device.restype = c_int32
     lib.tbe_numfmt_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p]
     lib.tbe_layout.restype = c_int32

@@ -29,24 +29,46 @@ def hipcc() -> str:
     raise FileNotFoundError("hipcc not found")
 
 
-def up_to_date(target: str, deps) -> bool:
-    if not os.path.exists(target):
+def _digest(deps, flags) -> str:
+    import hashlib
+    h = hashlib.sha256(" ".join(flags).encode())
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def up_to_date(target: str, deps, flags=()) -> bool:
+    """The library was built from exactly these sources and flags: a SHA-256 of both is
+    stored beside it (target + ".sha256"), so copying the tree (file times change, e.g.
+    on the GPU box) neither forces a rebuild nor hides a stale one."""
+    stamp = target + ".sha256"
+    if not (os.path.exists(target) and os.path.exists(stamp)):
         return False
-    t = os.path.getmtime(target)
-    return all(os.path.getmtime(d) <= t for d in deps)
+    with open(stamp) as f:
+        return f.read().strip() == _digest(deps, flags)
+
+
+def _stamp(target: str, deps, flags=()) -> None:
+    with open(target + ".sha256", "w") as f:
+        f.write(_digest(deps, flags) + "\n")
 
 
 def build_engine(force: bool = False, verbose: bool = False, defines=(), out: str = LIB) -> str:
     """Build libtbe.so (or, for ablation experiments, a variant with extra -D defines
     written to `out`)."""
-    if not force and not defines and up_to_date(out, DEPS):
+    flags = HIPCC_FLAGS + [f"-D{d}" for d in defines]
+    if not force and up_to_date(out, DEPS, flags):
+        if verbose:
+            print(f"build: {os.path.basename(out)} up to date (sources sha256 {_digest(DEPS, flags)[:12]})",
+                  file=sys.stderr)
         return out
-    cmd = [hipcc()] + HIPCC_FLAGS + [f"-D{d}" for d in defines] + \
-        ["-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SOURCES
+    cmd = [hipcc()] + flags + ["-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    _stamp(out, DEPS, flags)
     return out
 
 
@@ -59,7 +81,7 @@ CXX_FLAGS = ["-O2", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "
 def build_host(force: bool = False, verbose: bool = False) -> str:
     """libtbe_host.so: the C++ limiter classes (host/) over libtbe.so."""
     build_engine(verbose=verbose)
-    if not force and up_to_date(HOST_LIB, HOST_DEPS + [LIB]):
+    if not force and up_to_date(HOST_LIB, HOST_DEPS + [LIB], CXX_FLAGS):
         return HOST_LIB
     cmd = ["g++"] + CXX_FLAGS + ["-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
                                  "-o", HOST_LIB + ".tmp", HOST_SRC, "-L", HERE, "-ltbe",
@@ -68,6 +90,7 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(HOST_LIB + ".tmp", HOST_LIB)
+    _stamp(HOST_LIB, HOST_DEPS + [LIB], CXX_FLAGS)
     return HOST_LIB
 
 

@@ -1,118 +1,308 @@
 """Multi-GPU layer: one engine per GPU (one process per rank), keys hash-partitioned.
 
 The reference distributes by letting many client processes share one Redis key space
-(SURVEY.md §2).  Here every key has exactly one owner GPU holding its bucket state, so
-the token-bucket paths need no collective at all when ingest is already partitioned
-(the benchmark mode).  Two exchanges exist:
+(the bucket key is ``InstanceName + resourceID``, PTB:42).  Here every key
+has exactly one owner GPU holding its bucket state:
 
-* ``route_batch``: when requests arrive at arbitrary ranks, one all-to-all sends each to
-  its owner (ordered by source rank, then arrival index) and a reverse all-to-all
-  returns the replies.  The combined order is a valid serial order of the reference:
-  per key, rank 0's requests of this step precede rank 1's, and so on.
-* ``route_cancel``: cancellations of queued requests travel to the key's owner the
-  same way (one all-to-all of (key, request id), one of the hits back).
+    owner(key) = ((mix64(key) >> 32) * world) >> 32      (= mix64(key) >> (64 - log2 world))
+
+and the owner's key directory (``tbe_dir_*``, device-resident and collision-free: it
+stores whole keys) turns the keys it owns into dense bucket ids.  The token-bucket paths
+need no collective when ingest is already partitioned (the benchmark's default mode).
+Exchanges:
+
+* ``route_requests`` / ``route_replies`` (``route_batch`` = both around a ``decide``):
+  requests that arrive at any rank travel to their owner in one all-to-all (grouped by a
+  stable partition, so a key's requests reach the owner in (source rank, arrival) order,
+  a valid serial order of the reference) and the replies come back in a reverse
+  all-to-all.  On GPUs everything stays in HBM (``tbe_route_*`` kernels + RCCL); only the
+  world group sizes go through the host, as the all-to-all's split sizes.
+* ``route_cancel``: cancellations of queued requests travel to the key's owner the same
+  way (one all-to-all each way).
 * ``approx_epoch``: the ApproximateTokenBucket global tier.  Each rank is one client
   (A:9-599) holding a local tier for every shared key; at every refresh epoch the
   per-key consumed counts are exchanged -- all-gather for exact per-client prefix
   semantics (client r's sync call sees clients 0..r-1, SURVEY.md §8e option 2), or
-  all-reduce when the node acts as ONE client (option 1) -- and every rank replays
-  the same sync calls on its replica of the global tier.
+  all-reduce when the node acts as ONE client (option 1) -- and every rank replays the
+  same sync calls on its replica of the global tier.
 
-With backend "nccl" (RCCL on ROCm) the collectives run over xGMI on device tensors;
-tests drive the same code with "gloo" on CPU tensors.
+Inputs as CUDA tensors take the device path (backend "nccl" = RCCL over xGMI); numpy
+arrays take a host path with identical semantics (backend "gloo", the CPU tests).
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Optional, Tuple
 
 import numpy as np
 
+GAMMA = 0x9E3779B97F4A7C15
+MASK64 = (1 << 64) - 1
+NO_ID = np.uint64(MASK64)
+
 
 # ------------------------------------------------------------------ key partitioning
-def key_owner(keys: np.ndarray, world: int) -> np.ndarray:
-    """Owner rank of each (dense) key id.  Ids are assumed scrambled by the caller's
-    string-key directory (PTB:42 builds ``InstanceName + resourceID``); with dense
-    uniform ids ``key % world`` balances exactly."""
-    return (np.asarray(keys, dtype=np.uint64) % np.uint64(world)).astype(np.int64)
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = np.asarray(z, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z
 
 
-def local_key(keys: np.ndarray, world: int) -> np.ndarray:
-    """Dense id of a key inside its owner's table: ``key // world``."""
-    return np.asarray(keys, dtype=np.uint64) // np.uint64(world)
+def key_owner(keys, world: int) -> np.ndarray:
+    """Owner rank of each key (csrc/tbe_hash.hpp key_owner): ((mix64(key) >> 32) * world)
+    >> 32, i.e. the top log2(world) bits of mix64(key) for a power-of-two world."""
+    h = _mix64(keys) >> np.uint64(32)
+    with np.errstate(over="ignore"):
+        return ((h * np.uint64(world)) >> np.uint64(32)).astype(np.int64)
 
 
-def keys_per_rank(n_keys: int, world: int) -> int:
-    return (n_keys + world - 1) // world
+def _scramble_params(n: int):
+    bits = max(1, int(n - 1).bit_length())
+    return np.uint64((1 << bits) - 1), np.uint64(max(1, bits // 2))
 
 
-def shard_batch(keys, permits, ts_us, world: int):
-    """Stable split of one batch by owner: for each rank r, (arrival indices, local keys,
-    permits, ts).  Arrival order is preserved inside every shard."""
-    keys = np.asarray(keys, dtype=np.uint64)
-    owner = key_owner(keys, world)
-    order = np.argsort(owner, kind="stable")
-    bounds = np.searchsorted(owner[order], np.arange(world + 1))
-    out = []
-    for r in range(world):
-        idx = order[bounds[r]:bounds[r + 1]]
-        out.append((idx, local_key(keys[idx], world), np.asarray(permits)[idx],
-                    np.asarray(ts_us)[idx]))
-    return out
+def _scramble(x: np.ndarray, mask, sh) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        for a, c in ((0x9E3779B97F4A7C15, 0x632BE59BD9B4E019),
+                     (0xD1B54A32D192ED03, 0x8CB92BA72F3D8DD7),
+                     (0xAEF17502108EF2D9, 0x2545F4914F6CDD1D)):
+            x = (x * np.uint64(a) + np.uint64(c)) & mask
+            x ^= x >> sh
+    return x
+
+
+def scramble_walk(x, n: int) -> np.ndarray:
+    """The fixed bijection of [0, n) the directory applies to its counters
+    (csrc/tbe_hash.hpp scramble_walk)."""
+    mask, sh = _scramble_params(n)
+    x = _scramble(np.asarray(x, dtype=np.uint64), mask, sh)
+    bad = x >= np.uint64(n)
+    while bad.any():
+        x[bad] = _scramble(x[bad], mask, sh)
+        bad = x >= np.uint64(n)
+    return x
+
+
+class HostDirectory:
+    """Host mirror of the device key directory (tbe_dir_*): keys new to it get counters in
+    order of first occurrence, id = scramble_walk(counter, capacity).  Used by the gloo
+    path and the tests."""
+
+    def __init__(self, capacity: int):
+        self.capacity = int(capacity)
+        self.ids = {}
+        self.overflow = False
+
+    def assign(self, keys) -> np.ndarray:
+        keys = np.asarray(keys, dtype=np.uint64)
+        if keys.size == 0:
+            return np.zeros(0, dtype=np.uint64)
+        uniq, first = np.unique(keys, return_index=True)
+        new = [(f, k) for k, f in zip(uniq.tolist(), first.tolist()) if k not in self.ids]
+        new.sort()
+        base = len(self.ids)
+        room = max(0, self.capacity - base)
+        if len(new) > room:
+            self.overflow = True
+        if new[:room]:
+            ctr = np.arange(base, base + len(new[:room]), dtype=np.uint64)
+            for (_, k), i in zip(new[:room], scramble_walk(ctr, self.capacity).tolist()):
+                self.ids[k] = i
+        return self.lookup(keys)
+
+    def lookup(self, keys) -> np.ndarray:
+        get = self.ids.get
+        return np.array([get(k, MASK64) for k in np.asarray(keys, dtype=np.uint64).tolist()], dtype=np.uint64)
+
+    def size(self) -> int:
+        return len(self.ids)
+
+
+class DeviceDirectory:
+    """The owner's key directory in HBM (include/tbe_cluster.h tbe_dir_*)."""
+
+    def __init__(self, capacity: int, device: int = -1):
+        import ctypes
+        from . import _capi
+        self._lib = _capi.load()
+        h = ctypes.c_void_p()
+        st = self._lib.tbe_dir_create(int(capacity), device, ctypes.byref(h))
+        if st != _capi.TBE_OK:
+            raise _capi.TbeError(st, f"tbe_dir_create({capacity}) failed")
+        self._h = h
+        self.capacity = int(capacity)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.tbe_dir_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _run(self, fn, d_keys):
+        import torch
+        from . import _capi
+        d_keys = d_keys.contiguous()
+        ids = torch.empty(d_keys.numel(), dtype=torch.int64, device=d_keys.device)
+        st = fn(self._h, d_keys.data_ptr(), d_keys.numel(), ids.data_ptr(),
+                torch.cuda.current_stream(d_keys.device).cuda_stream)
+        if st != _capi.TBE_OK:
+            raise _capi.TbeError(st, "directory call failed")
+        return ids
+
+    def assign(self, d_keys):
+        """int64 device tensor of keys -> int64 device tensor of ids (assigning new ones)."""
+        return self._run(self._lib.tbe_dir_assign_device, d_keys)
+
+    def lookup(self, d_keys):
+        """ids of known keys, -1 (UINT64_MAX) for others; assigns nothing."""
+        return self._run(self._lib.tbe_dir_lookup_device, d_keys)
+
+    def size(self) -> int:
+        import ctypes
+        from . import _capi
+        n = ctypes.c_uint64()
+        st = self._lib.tbe_dir_size(self._h, ctypes.byref(n))
+        if st != _capi.TBE_OK:
+            raise _capi.TbeError(st, "directory over capacity" if st == _capi.TBE_ERANGE else "tbe_dir_size failed")
+        return n.value
+
+
+def keys_per_rank(n_keys: int, world: int, slack: float = 0.01) -> int:
+    """Table capacity per rank for n_keys hash-partitioned keys: the expected share plus
+    a margin far above the binomial spread of the owner counts."""
+    share = -(-n_keys // world)
+    return n_keys if world == 1 else min(n_keys, int(share * (1.0 + slack)) + 1024)
 
 
 # ------------------------------------------------------------------ all-to-all routing
-def route_batch(decide: Callable, keys, permits, ts_us, group=None, device=None):
+class RoutePlan:
+    """What route_replies needs to send replies back: the arrival -> grouped permutation
+    and the all-to-all split sizes of both directions."""
+
+    def __init__(self, order, send_counts, recv_counts, n):
+        self.order, self.send_counts, self.recv_counts, self.n = order, send_counts, recv_counts, n
+
+
+def _is_cuda(x) -> bool:
+    return hasattr(x, "is_cuda") and x.is_cuda
+
+
+def route_requests(keys, permits, ts_us, directory, group=None):
+    """Send this rank's requests to their owners.  Returns ((local ids, permits, ts) of
+    the requests this rank owns, in (source rank, arrival) order, and the RoutePlan for
+    route_replies).  CUDA tensors: device kernels + RCCL; numpy: host path + gloo."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    if _is_cuda(keys):
+        from . import _capi
+        lib = _capi.load()
+        dev = keys.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        keys = keys.contiguous()
+        n = keys.numel()
+        pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        counts = torch.zeros(world, dtype=torch.int64, device=dev)
+        work = torch.empty(max(1, lib.tbe_route_workspace_bytes(n, world)), dtype=torch.uint8, device=dev)
+        _check(lib.tbe_route_plan_device(keys.data_ptr(), n, world, work.data_ptr(), pos.data_ptr(),
+                                         counts.data_ptr(), stream))
+        send = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        _check(lib.tbe_route_pack_device(pos.data_ptr(), n, keys.data_ptr(), permits.contiguous().data_ptr(),
+                                         ts_us.contiguous().data_ptr(), send.data_ptr(), stream))
+        rc = torch.empty_like(counts)
+        dist.all_to_all_single(rc, counts, group=group)
+        sc_l, rc_l = counts.tolist(), rc.tolist()
+        recv = torch.empty((sum(rc_l), 3), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, send, output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
+        local = directory.assign(recv[:, 0])
+        return (local, recv[:, 2].to(torch.int32), recv[:, 1].contiguous()), RoutePlan(pos, sc_l, rc_l, n)
+    keys = np.asarray(keys, dtype=np.uint64)
+    n = keys.shape[0]
+    owner = key_owner(keys, world)
+    order = np.argsort(owner, kind="stable")
+    send_counts = np.bincount(owner, minlength=world).astype(np.int64)
+    sc = torch.from_numpy(send_counts)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = rc.numpy()
+    payload = np.stack([keys[order].view(np.int64), np.asarray(ts_us, dtype=np.int64)[order],
+                        np.asarray(permits, dtype=np.int64)[order]], axis=1)
+    recv = torch.empty((int(recv_counts.sum()), 3), dtype=torch.int64)
+    dist.all_to_all_single(recv, torch.from_numpy(np.ascontiguousarray(payload)),
+                           output_split_sizes=recv_counts.tolist(), input_split_sizes=send_counts.tolist(),
+                           group=group)
+    r = recv.numpy()
+    local = directory.assign(r[:, 0].view(np.uint64))
+    return (local, r[:, 2].astype(np.int32), r[:, 1].copy()), RoutePlan(order, send_counts.tolist(),
+                                                                        recv_counts.tolist(), n)
+
+
+def route_replies(plan: RoutePlan, cols, group=None):
+    """Send the owner's reply columns (one int64-convertible array/tensor per column, in
+    route_requests' received order) back; returns them in this rank's arrival order."""
+    import torch
+    import torch.distributed as dist
+
+    if cols and _is_cuda(cols[0]):
+        from . import _capi
+        lib = _capi.load()
+        dev = cols[0].device
+        reply = torch.stack([c.to(torch.int64) for c in cols], dim=1).contiguous()
+        k = reply.shape[1]
+        back = torch.empty((plan.n, k), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(back, reply, output_split_sizes=plan.send_counts,
+                               input_split_sizes=plan.recv_counts, group=group)
+        out = torch.empty_like(back)
+        _check(lib.tbe_route_gather_device(plan.order.data_ptr(), plan.n, back.data_ptr(), k, out.data_ptr(),
+                                           torch.cuda.current_stream(dev).cuda_stream))
+        return tuple(out[:, c] for c in range(k))
+    k = len(cols)
+    m = sum(plan.recv_counts)
+    reply = np.stack([np.asarray(c, dtype=np.int64).reshape(-1) for c in cols], axis=1) if m \
+        else np.zeros((0, k), dtype=np.int64)
+    back = torch.empty((plan.n, k), dtype=torch.int64)
+    dist.all_to_all_single(back, torch.from_numpy(np.ascontiguousarray(reply)),
+                           output_split_sizes=plan.send_counts, input_split_sizes=plan.recv_counts, group=group)
+    b = back.numpy()
+    out = np.empty_like(b)
+    out[plan.order] = b
+    return tuple(out[:, c] for c in range(k))
+
+
+def route_batch(decide: Callable, keys, permits, ts_us, directory, group=None):
     """Decide a batch whose requests arrived at this rank but may belong to any rank.
 
-    ``decide(local_keys, permits, ts) -> (granted u8, remaining i32[, extra...])`` runs
-    this rank's engine on the requests it owns.  Returns (granted, remaining) for this
-    rank's own requests in their arrival order, plus any extra int64 reply column
-    ``decide`` returns (a queueing engine's request ids, which the owner assigns and a
-    later ``route_cancel`` needs).  Two all-to-alls (requests out, replies back)."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    keys = np.asarray(keys, dtype=np.uint64)
-    n = keys.shape[0]
-    owner = key_owner(keys, world)
-    order = np.argsort(owner, kind="stable")
-    send_counts = np.bincount(owner, minlength=world).astype(np.int64)
-    to = (lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)) if device else \
-        (lambda a: torch.from_numpy(np.ascontiguousarray(a)))
-    sc = to(send_counts)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = rc.cpu().numpy()
-    # one int64 record per field keeps the exchange to three all-to-alls of one dtype
-    payload = np.stack([local_key(keys[order], world).astype(np.int64),
-                        np.asarray(permits, dtype=np.int64)[order],
-                        np.asarray(ts_us, dtype=np.int64)[order]], axis=1)
-    recv = torch.empty((int(recv_counts.sum()), 3), dtype=torch.int64, device=device)
-    dist.all_to_all_single(recv, to(payload), output_split_sizes=recv_counts.tolist(),
-                           input_split_sizes=send_counts.tolist(), group=group)
-    r = recv.cpu().numpy()
-    outs = decide(r[:, 0].astype(np.uint64), r[:, 1].astype(np.int32), r[:, 2])
-    cols = len(outs)
-    reply = np.stack([np.asarray(x, dtype=np.int64).reshape(-1) for x in outs], axis=1) \
-        if r.shape[0] else np.zeros((0, cols), dtype=np.int64)
-    back = torch.empty((n, cols), dtype=torch.int64, device=device)
-    dist.all_to_all_single(back, to(reply), output_split_sizes=send_counts.tolist(),
-                           input_split_sizes=recv_counts.tolist(), group=group)
-    b = back.cpu().numpy()
-    res = [np.empty(n, dtype=dt) for dt in [np.uint8, np.int32] + [np.int64] * (cols - 2)]
-    for c in range(cols):
-        res[c][order] = b[:, c]
-    return tuple(res)
+    ``decide(local_ids, permits, ts) -> (col0, col1[, ...])`` runs this rank's engine on
+    the requests it owns (e.g. granted and remaining; a queueing engine adds the request
+    ids it assigns, which a later ``route_cancel`` needs).  Returns the columns for this
+    rank's own requests in their arrival order: granted/status as u8, remaining as i32,
+    further columns as i64 (host path) or the int64 device tensors (device path)."""
+    (lk, lp, lt), plan = route_requests(keys, permits, ts_us, directory, group)
+    cols = decide(lk, lp, lt)
+    out = route_replies(plan, cols, group)
+    if _is_cuda(out[0]):
+        import torch
+        return (out[0].to(torch.uint8), out[1].to(torch.int32)) + tuple(out[2:])
+    return (out[0].astype(np.uint8), out[1].astype(np.int32)) + tuple(out[2:])
 
 
-def route_cancel(cancel: Callable, keys, request_ids, group=None, device=None):
+def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
     """Cancel queued requests (CancelQueueState.TrySetCanceled, Q:480-506 / A:531-557)
-    that may be queued on any rank: ``keys`` are global key ids, ``request_ids`` the ids
-    their owners assigned (``route_batch``'s extra reply column).  ``cancel(local_keys,
-    request_ids) -> u8`` runs on the owner (``QueueingTokenBucketEngine.cancel``).
-    Returns the u8 hits in this rank's order.  Per owner, the cancels apply by source
-    rank, then call order.  Two all-to-alls."""
+    that may be queued on any rank: ``keys`` are global keys, ``request_ids`` the ids
+    their owners assigned (``route_batch``'s extra reply column).  ``cancel(local_ids,
+    request_ids) -> u8`` runs on the owner; a key unknown to the owner's directory has
+    nothing queued.  Returns the hits in this rank's order.  Per owner, the cancels apply
+    by source rank, then call order."""
     import torch
     import torch.distributed as dist
 
@@ -122,26 +312,34 @@ def route_cancel(cancel: Callable, keys, request_ids, group=None, device=None):
     owner = key_owner(keys, world)
     order = np.argsort(owner, kind="stable")
     send_counts = np.bincount(owner, minlength=world).astype(np.int64)
-    to = (lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)) if device else \
-        (lambda a: torch.from_numpy(np.ascontiguousarray(a)))
-    sc = to(send_counts)
+    sc = torch.from_numpy(send_counts)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = rc.cpu().numpy()
-    payload = np.stack([local_key(keys[order], world).astype(np.int64),
-                        np.asarray(request_ids, dtype=np.int64)[order]], axis=1)
-    recv = torch.empty((int(recv_counts.sum()), 2), dtype=torch.int64, device=device)
-    dist.all_to_all_single(recv, to(payload), output_split_sizes=recv_counts.tolist(),
-                           input_split_sizes=send_counts.tolist(), group=group)
-    r = recv.cpu().numpy()
-    hit = np.asarray(cancel(r[:, 0].astype(np.uint64), r[:, 1]), dtype=np.int64) if r.shape[0] \
-        else np.zeros(0, dtype=np.int64)
-    back = torch.empty(n, dtype=torch.int64, device=device)
-    dist.all_to_all_single(back, to(hit), output_split_sizes=send_counts.tolist(),
+    recv_counts = rc.numpy()
+    payload = np.stack([keys[order].view(np.int64), np.asarray(request_ids, dtype=np.int64)[order]], axis=1)
+    recv = torch.empty((int(recv_counts.sum()), 2), dtype=torch.int64)
+    dist.all_to_all_single(recv, torch.from_numpy(np.ascontiguousarray(payload)),
+                           output_split_sizes=recv_counts.tolist(), input_split_sizes=send_counts.tolist(),
+                           group=group)
+    r = recv.numpy()
+    hit = np.zeros(r.shape[0], dtype=np.int64)
+    if r.shape[0]:
+        local = directory.lookup(r[:, 0].view(np.uint64))
+        known = local != NO_ID
+        if known.any():
+            hit[known] = np.asarray(cancel(local[known], r[known, 1]), dtype=np.int64)
+    back = torch.empty(n, dtype=torch.int64)
+    dist.all_to_all_single(back, torch.from_numpy(hit), output_split_sizes=send_counts.tolist(),
                            input_split_sizes=recv_counts.tolist(), group=group)
     out = np.empty(n, dtype=np.uint8)
-    out[order] = back.cpu().numpy()
+    out[order] = back.numpy()
     return out
+
+
+def _check(st: int) -> None:
+    from . import _capi
+    if st != _capi.TBE_OK:
+        raise _capi.TbeError(st, "routing kernel launch failed")
 
 
 # ------------------------------------------------------------------ approximate global tier

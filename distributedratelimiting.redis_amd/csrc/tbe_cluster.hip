@@ -278,6 +278,31 @@ __global__ void k_dir_gather(const uint32_t *__restrict__ slot_of, uint64_t n, c
     }
 }
 
+// Read-only lookup: id, or UINT64_MAX for a key the directory has never assigned.
+__global__ __launch_bounds__(kDirBlock) void k_dir_lookup(const uint64_t *__restrict__ keys, uint64_t n,
+                                                          const uint64_t *__restrict__ skey,
+                                                          const uint32_t *__restrict__ sid, uint64_t smask,
+                                                          uint64_t *__restrict__ ids) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t key = keys[i];
+        uint64_t id = ~0ull;
+        if (key != kEmptyKey) {
+            uint64_t h = mix64(key) & smask;
+            for (uint64_t probe = 0; probe <= smask; ++probe) {
+                const uint64_t cur = skey[h];
+                if (cur == key) {
+                    if (sid[h] != kNoId) id = sid[h];
+                    break;
+                }
+                if (cur == kEmptyKey) break;
+                h = (h + 1) & smask;
+            }
+        }
+        ids[i] = id;
+    }
+}
+
 __global__ void k_dir_init(uint64_t *__restrict__ skey, uint32_t *__restrict__ sid, uint32_t *__restrict__ sfirst,
                            uint64_t nslots) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -423,6 +448,16 @@ tbe_status tbe_dir_assign_device(tbe_directory *d, const uint64_t *d_keys, uint6
     k_dir_assign<<<nblk, kDirBlock, 0, st>>>(d->slot_of, n, d->sid, d->sfirst, d->bsum, d->state, d->capacity,
                                              d->imask, d->ish);
     k_dir_gather<<<grid_for(n, 256), 256, 0, st>>>(d->slot_of, n, d->sid, d_ids);
+    return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
+}
+
+tbe_status tbe_dir_lookup_device(tbe_directory *d, const uint64_t *d_keys, uint64_t n, uint64_t *d_ids, void *stream) {
+    if (!d) return TBE_EINVAL;
+    if (n == 0) return TBE_OK;
+    if (!d_keys || !d_ids) return TBE_EINVAL;
+    if (hipSetDevice(d->device) != hipSuccess) return TBE_EDEVICE;
+    k_dir_lookup<<<grid_for(n, kDirBlock), kDirBlock, 0, (hipStream_t)stream>>>(d_keys, n, d->skey, d->sid,
+                                                                               d->nslots - 1, d_ids);
     return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
 }
 

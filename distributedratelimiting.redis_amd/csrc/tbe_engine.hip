@@ -31,6 +31,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -958,8 +959,14 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
 // instead of two doubles its time, profiles/r01_v11_ablate_occupancy.log).  The row's
 // field t is derived per evaluation (field_t) instead of being cached in LDS.
 constexpr int kTbBlock = 256;
-constexpr int kTbPer = 4;
-constexpr int kTbTail = kTbBlock;                         // compact pending list after round 1
+#ifndef TBE_TB_PER
+#define TBE_TB_PER 4
+#endif
+#ifndef TBE_TB_TAIL
+#define TBE_TB_TAIL kTbBlock
+#endif
+constexpr int kTbPer = TBE_TB_PER;
+constexpr int kTbTail = TBE_TB_TAIL;                      // compact pending list after round 1
 constexpr int kTbChunk = kTbBlock * kTbPer;               // 1024 requests per chunk
 constexpr int kTailPer = kTbTail / kTbBlock;              // its entries per thread
 constexpr int64_t kRowWindow = (int64_t)1 << 31;          // field_t fast path: rows up to ~35 min older
@@ -2351,6 +2358,8 @@ struct tbe_engine {
     uint32_t *sticky = nullptr;      // set by any skipped batch until tbe_synchronize reads it
     uint32_t *last_err = nullptr;    // the error flag of the last enqueued batch
     // host-buffer path staging
+    hipStream_t cin = nullptr, cout = nullptr;   // chunked pinned path: copy-in / copy-out streams
+    std::vector<hipEvent_t> ev_chunk;            // per-chunk copy-in done
     uint64_t stage_cap = 0;
     uint64_t *d_keys = nullptr;
     int32_t *d_permits = nullptr;
@@ -2521,7 +2530,8 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 // batch b-1 is done) and hot[(b+1) % 3] (complete since batch b-1's hot update).
 tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                      const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
-                     hipStream_t caller, int64_t id_base = 0) {
+                     hipStream_t caller, int64_t id_base = 0, hipEvent_t in_ready = nullptr,
+                     hipStream_t out_stream = nullptr) {
     const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
     const bool wait = e->cfg.kind != TBE_KIND_TOKEN_BUCKET;   // status-packed replies
     if (n == 0) return TBE_OK;
@@ -2537,7 +2547,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (pipe) {
         sf = e->stream;
         sp = e->pstream;
-        if (caller) {
+        if (in_ready) {               // chunked host-buffer path: this chunk's copy-in
+            HIP_TRY(e, hipStreamWaitEvent(sp, in_ready, 0));
+        } else if (caller) {
             HIP_TRY(e, hipEventRecord(e->ev_in, caller));
             HIP_TRY(e, hipStreamWaitEvent(sp, e->ev_in, 0));
         }
@@ -2710,9 +2722,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (pipe) {
         HIP_TRY(e, hipEventRecord(w.done, sf));
         w.used = true;
-        if (caller && caller != sf) {
+        hipStream_t outs = out_stream ? out_stream : caller;
+        if (outs && outs != sf) {
             HIP_TRY(e, hipEventRecord(e->ev_out, sf));
-            HIP_TRY(e, hipStreamWaitEvent(caller, e->ev_out, 0));
+            HIP_TRY(e, hipStreamWaitEvent(outs, e->ev_out, 0));
         }
         e->ws_cur ^= 1;
     }
@@ -2889,6 +2902,8 @@ void tbe_destroy(tbe_engine *e) {
     if (!e) return;
     if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (hipStream_t s2 : {e->cin, e->cout})
+        if (s2) (void)hipStreamSynchronize(s2);
     free_workspace(e->ws[0]);
     free_workspace(e->ws[1]);
     free_staging(e);
@@ -2915,12 +2930,88 @@ void tbe_destroy(tbe_engine *e) {
     for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ws[0].done, e->ws[1].done})
         if (ev) (void)hipEventDestroy(ev);
     if (e->pstream) (void)hipStreamDestroy(e->pstream);
+    for (hipEvent_t ev : e->ev_chunk)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t s2 : {e->cin, e->cout})
+        if (s2) (void)hipStreamDestroy(s2);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
 const char *tbe_last_error(const tbe_engine *e) {
     return e ? e->last_error.c_str() : g_create_error.c_str();
+}
+
+// ---- the host-buffer path from page-locked buffers (tbe_alloc_host), chunked so that
+// PCIe copies overlap the decisions: every chunk's copy-in is enqueued up front on one
+// copy stream, each chunk is decided as a sub-batch as soon as its copy lands (sub-batches
+// in arrival order are the same serial order as one batch), and its replies go back on a
+// second copy stream while later chunks are decided.  The whole batch is validated on
+// the host first (several threads), so an invalid batch still changes nothing.
+static constexpr uint64_t kHostChunk = 1ull << 22;
+
+static bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory is not an error worth keeping
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+static bool host_validate(const tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
+                          uint64_t n) {
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    std::vector<char> bad(nt, 0);
+    const uint64_t nk = e->cfg.n_keys;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            const uint64_t a = n * t / nt, b = n * (t + 1) / nt;
+            bool x = false;
+            for (uint64_t i = a; i < b; ++i) x |= (keys[i] >= nk) | (permits[i] < 0) | (ts[i] < 0);
+            bad[t] = x;
+        });
+    for (auto &x : th) x.join();
+    for (char b : bad)
+        if (b) return false;
+    return true;
+}
+
+static tbe_status acquire_chunked(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
+                                  uint64_t n, uint8_t *granted, int32_t *remaining) {
+    if (!e->cin) {
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
+    }
+    const uint64_t nch = (n + kHostChunk - 1) / kHostChunk;
+    while (e->ev_chunk.size() < nch) {
+        hipEvent_t ev = nullptr;
+        HIP_TRY(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        e->ev_chunk.push_back(ev);
+    }
+    for (uint64_t c = 0; c < nch; ++c) {   // all copies in, in chunk order
+        const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
+        HIP_TRY(e, hipMemcpyAsync(e->d_keys + o, keys + o, m * sizeof(uint64_t), hipMemcpyHostToDevice, e->cin));
+        HIP_TRY(e, hipMemcpyAsync(e->d_permits + o, permits + o, m * sizeof(int32_t), hipMemcpyHostToDevice, e->cin));
+        HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin));
+        HIP_TRY(e, hipEventRecord(e->ev_chunk[c], e->cin));
+    }
+    if (!host_validate(e, keys, permits, ts, n)) {   // overlaps the first copies
+        HIP_TRY(e, hipStreamSynchronize(e->cin));
+        return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
+    }
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
+        tbe_status rc = run_batch(e, e->d_keys + o, e->d_permits + o, e->d_ts + o, m, e->d_granted + o,
+                                  e->d_remaining + o, nullptr, 0, e->ev_chunk[c], e->cout);
+        if (rc != TBE_OK) return rc;
+        HIP_TRY(e, hipMemcpyAsync(granted + o, e->d_granted + o, m, hipMemcpyDeviceToHost, e->cout));
+        HIP_TRY(e, hipMemcpyAsync(remaining + o, e->d_remaining + o, m * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  e->cout));
+    }
+    HIP_TRY(e, hipStreamSynchronize(e->cout));
+    return TBE_OK;
 }
 
 tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
@@ -2934,6 +3025,9 @@ tbe_status tbe_acquire_batch(tbe_engine *e, const uint64_t *keys, const int32_t 
     HIP_TRY(e, hipSetDevice(e->device));
     tbe_status rc = ensure_host_staging(e, n);
     if (rc != TBE_OK) return rc;
+    if (e->pipeline && n >= 2 * kHostChunk && host_pinned(keys) && host_pinned(permits) &&
+        host_pinned(ts_us) && host_pinned(granted) && host_pinned(remaining))
+        return acquire_chunked(e, keys, permits, ts_us, n, granted, remaining);
     hipStream_t st = e->stream;
     HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));

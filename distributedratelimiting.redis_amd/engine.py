@@ -110,16 +110,22 @@ class TokenBucketEngine:
         return self._h
 
     # ------------------------------------------------------------------ decisions
-    def acquire_batch(self, keys, permits, ts_us) -> Tuple[np.ndarray, np.ndarray]:
-        """Host arrays in, host arrays out (granted u8, remaining i32), arrival order."""
+    def acquire_batch(self, keys, permits, ts_us, granted=None, remaining=None) -> Tuple[np.ndarray, np.ndarray]:
+        """Host arrays in, host arrays out (granted u8, remaining i32), arrival order.
+        granted/remaining: optional output arrays (e.g. PinnedArray.array: with every
+        buffer page-locked, large batches take the chunked path whose copies overlap the
+        decisions)."""
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         permits = np.ascontiguousarray(permits, dtype=np.int32)
         ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
         n = keys.shape[0]
         if permits.shape[0] != n or ts_us.shape[0] != n:
             raise ValueError("keys, permits and ts_us must have the same length")
-        granted = np.empty(n, dtype=np.uint8)
-        remaining = np.empty(n, dtype=np.int32)
+        granted = np.empty(n, dtype=np.uint8) if granted is None else granted
+        remaining = np.empty(n, dtype=np.int32) if remaining is None else remaining
+        if granted.shape != (n,) or remaining.shape != (n,) or granted.dtype != np.uint8 or \
+                remaining.dtype != np.int32 or not (granted.flags.c_contiguous and remaining.flags.c_contiguous):
+            raise ValueError("granted must be u8[n] and remaining i32[n], contiguous")
         self._check(self._lib.tbe_acquire_batch(
             self.handle, keys.ctypes.data, permits.ctypes.data, ts_us.ctypes.data, n,
             granted.ctypes.data, remaining.ctypes.data))

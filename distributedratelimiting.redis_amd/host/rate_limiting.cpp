@@ -104,27 +104,41 @@ bool CancellationToken::IsCancellationRequested() const {
     return s_->canceled;
 }
 
-void CancellationToken::Register(std::function<void()> fn) const {
-    if (!s_) return;
+uint64_t CancellationToken::Register(std::function<void()> fn) const {
+    if (!s_) return 0;
     {
         std::lock_guard<std::mutex> g(s_->mu);
         if (!s_->canceled) {
-            s_->callbacks.push_back(std::move(fn));
-            return;
+            const uint64_t h = s_->next++;
+            s_->callbacks.emplace(h, std::move(fn));
+            return h;
         }
     }
     fn();  // already canceled: run at once, as CancellationToken.Register does
+    return 0;
+}
+
+void CancellationToken::Unregister(uint64_t handle) const {
+    if (!s_ || !handle) return;
+    std::lock_guard<std::mutex> g(s_->mu);
+    s_->callbacks.erase(handle);
+}
+
+size_t CancellationToken::RegisteredCount() const {
+    if (!s_) return 0;
+    std::lock_guard<std::mutex> g(s_->mu);
+    return s_->callbacks.size();
 }
 
 void CancellationTokenSource::Cancel() {
-    std::vector<std::function<void()>> fns;
+    std::map<uint64_t, std::function<void()>> fns;
     {
         std::lock_guard<std::mutex> g(s_->mu);
         if (s_->canceled) return;
         s_->canceled = true;
         fns.swap(s_->callbacks);
     }
-    for (auto &f : fns) f();
+    for (auto &f : fns) f.second();
 }
 
 // ------------------------------------------------------------------ the core
@@ -229,9 +243,6 @@ public:
         std::lock_guard<std::mutex> g(dir_mu_);
         const uint64_t n = names_.size();
         if (n == 0) return 0;
-        std::vector<double> v(n);
-        std::vector<int64_t> t(n);
-        Check(tbe_export_state(eng_, 0, n, v.data(), t.data()));
         // TB:234: EXPIRE ceil(min(max(capacity / fill_rate, 1), 31536000)) seconds; the
         // engine's expiry test is tbe_query's (millisecond resolution).
         double q = (double)opt_.TokenLimit / opt_.FillRatePerSecond();
@@ -242,14 +253,32 @@ public:
         std::vector<uint8_t> is_free(n, 0);
         for (uint64_t k : free_ids_) is_free[k] = 1;
         uint64_t freed = 0;
-        for (uint64_t k = 0; k < n; ++k) {
-            if (is_free[k] || busy.count(k)) continue;
-            if (t[k] != INT64_MIN && now_ms <= t[k] / 1000 + ttl_ms) continue;  // still present
-            dir_.erase(names_[k]);
-            names_[k].clear();
-            last_reply_.erase(k);
-            free_ids_.push_back(k);
-            ++freed;
+        // the table is read back in chunks (bounded host memory); a freed key's row is
+        // then written back absent, so a new string starts from a full bucket whatever
+        // the clock does later (a system clock may step backwards)
+        constexpr uint64_t kChunk = 1u << 20;
+        std::vector<double> v(std::min(n, kChunk));
+        std::vector<int64_t> t(std::min(n, kChunk));
+        for (uint64_t k0 = 0; k0 < n; k0 += kChunk) {
+            const uint64_t m = std::min(kChunk, n - k0);
+            Check(tbe_export_state(eng_, k0, m, v.data(), t.data()));
+            bool cleared = false;
+            for (uint64_t j = 0; j < m; ++j) {
+                const uint64_t k = k0 + j;
+                if (is_free[k] || busy.count(k)) continue;
+                if (t[j] != INT64_MIN && now_ms <= t[j] / 1000 + ttl_ms) continue;  // still present
+                dir_.erase(names_[k]);
+                names_[k].clear();
+                last_reply_.erase(k);
+                free_ids_.push_back(k);
+                if (t[j] != INT64_MIN) {
+                    t[j] = INT64_MIN;
+                    cleared = true;
+                }
+                ++freed;
+            }
+            // this thread is the engine's only submitter: the other rows go back unchanged
+            if (cleared) Check(tbe_import_state(eng_, k0, m, v.data(), t.data()));
         }
         reclaimed_ += freed;
         return freed;
@@ -346,10 +375,7 @@ public:
             uint64_t w = 0;
             Check(tbe_refresh_log(eng_, keys.data(), ids.data(), rem.data(), n, &w));
             for (uint64_t i = 0; i < w; ++i) {
-                auto it = waiting_.find(ids[i]);
-                if (it == waiting_.end()) continue;
-                it->second.set_value(RateLimitLease(true));
-                waiting_.erase(it);
+                if (!Complete(ids[i], RateLimitLease(true))) continue;
                 if (kind_ == TBE_KIND_QUEUEING) Remember(keys[i], rem[i]);
             }
         }
@@ -385,7 +411,10 @@ public:
         {
             std::lock_guard<std::mutex> g(mu_);
             q_.emplace_back(Cmd{[this] {
-                for (auto &w : waiting_) w.second.set_value(RateLimitLease(false));
+                for (auto &w : waiting_) {
+                    w.second.ct.Unregister(w.second.reg);
+                    w.second.done.set_value(RateLimitLease(false));
+                }
                 waiting_.clear();
             }});
             stop_ = true;
@@ -449,13 +478,19 @@ private:
             ids[i] = list[i].second;
         }
         uint64_t m = 0;
-        if (tbe_queue_cancel(eng_, keys.data(), ids.data(), n, hit.data(), &m) != TBE_OK) return;
+        if (tbe_queue_cancel(eng_, keys.data(), ids.data(), n, hit.data(), &m) != TBE_OK) {
+            // keep them: the next flush retries (the engine error also surfaces on the next batch)
+            std::lock_guard<std::mutex> g(inbox_->mu);
+            list.insert(list.end(), inbox_->pending.begin(), inbox_->pending.end());
+            inbox_->pending.swap(list);
+            return;
+        }
         for (uint64_t i = 0; i < n; ++i) {
             if (!hit[i]) continue;  // already completed: TrySetCanceled returns false
             auto it = waiting_.find(ids[i]);
             if (it == waiting_.end()) continue;
-            it->second.set_exception(std::make_exception_ptr(OperationCanceledException()));
-            waiting_.erase(it);
+            it->second.done.set_exception(std::make_exception_ptr(OperationCanceledException()));
+            waiting_.erase(it);   // its callback has run: nothing left registered
         }
     }
 
@@ -576,11 +611,11 @@ private:
                 r.done.set_value(RateLimitLease(true));
             } else if (s == TBE_WAIT_QUEUED) {
                 const int64_t id = id_base + (int64_t)i;
-                waiting_.emplace(id, std::move(r.done));
+                Waiter &wt = waiting_.emplace(id, Waiter{std::move(r.done), r.ct, 0}).first->second;
                 if (r.ct.CanBeCanceled()) {  // A:166-175
                     std::shared_ptr<CancelInbox> box = inbox_;
                     const uint64_t key = r.key;
-                    r.ct.Register([box, key, id] { box->Post(key, id); });
+                    wt.reg = r.ct.Register([box, key, id] { box->Post(key, id); });
                 }
             } else if (mode == kApproxWait || mode == kApproxAttempt) {
                 auto it = approx.find(r.key);
@@ -598,12 +633,7 @@ private:
             std::vector<int64_t> ids(n_ev);
             uint64_t w = 0;
             Check(tbe_evicted(eng_, cause.data(), ids.data(), n_ev, &w));
-            for (uint64_t j = 0; j < w; ++j) {
-                auto it = waiting_.find(ids[j]);
-                if (it == waiting_.end()) continue;
-                it->second.set_value(RateLimitLease(false));
-                waiting_.erase(it);
-            }
+            for (uint64_t j = 0; j < w; ++j) Complete(ids[j], RateLimitLease(false));
         }
     }
 
@@ -661,7 +691,23 @@ private:
 
     // submitter-thread state
     int64_t next_id_ = 0;
-    std::unordered_map<int64_t, std::promise<RateLimitLease>> waiting_;
+    // A queued request: its promise and its token registration, disposed when the request
+    // completes (granted, evicted, failed at dispose) so a long-lived token does not keep
+    // one callback per request it ever saw (CancellationTokenRegistration.Dispose, Q:263).
+    struct Waiter {
+        std::promise<RateLimitLease> done;
+        CancellationToken ct;
+        uint64_t reg;
+    };
+    std::unordered_map<int64_t, Waiter> waiting_;
+    bool Complete(int64_t id, RateLimitLease lease) {
+        auto it = waiting_.find(id);
+        if (it == waiting_.end()) return false;
+        it->second.ct.Unregister(it->second.reg);
+        it->second.done.set_value(std::move(lease));
+        waiting_.erase(it);
+        return true;
+    }
     std::vector<uint64_t> keys_;
     std::vector<int32_t> permits_;
     std::vector<int64_t> ts_;

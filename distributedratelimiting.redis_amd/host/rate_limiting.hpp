@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <functional>
 #include <future>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -86,13 +87,19 @@ public:
     CancellationToken() = default;  // CancellationToken.None
     bool CanBeCanceled() const { return (bool)s_; }
     bool IsCancellationRequested() const;
-    void Register(std::function<void()> fn) const;
+    // Returns a registration handle (0: nothing registered -- CancellationToken.None, or
+    // already canceled, in which case fn has run).  Unregister(handle) removes a callback
+    // that has not run (CancellationTokenRegistration.Dispose, Q:263, Q:303).
+    uint64_t Register(std::function<void()> fn) const;
+    void Unregister(uint64_t handle) const;
+    size_t RegisteredCount() const;  // diagnostics (tests)
 private:
     friend class CancellationTokenSource;
     struct State {
         std::mutex mu;
         bool canceled = false;
-        std::vector<std::function<void()>> callbacks;
+        uint64_t next = 1;
+        std::map<uint64_t, std::function<void()>> callbacks;
     };
     explicit CancellationToken(std::shared_ptr<State> s) : s_(std::move(s)) {}
     std::shared_ptr<State> s_;

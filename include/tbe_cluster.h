@@ -58,15 +58,20 @@ tbe_status tbe_route_gather_device(const uint32_t *d_pos, uint64_t n, const int6
  * first occurrence (batches in call order, arrival order inside a batch), and the id is
  * a fixed bijection of [0, capacity) applied to the counter (so hot keys, which are seen
  * first, do not crowd the first buckets).  Collision-free: the table stores whole keys.
- * When a batch would assign more than `capacity` ids, the excess keys get id UINT64_MAX
- * (an engine batch containing them is rejected as invalid) and tbe_dir_size reports
- * TBE_ERANGE from then on. */
+ * Capacity: once a batch brings more new keys than `capacity` ids remain, tbe_dir_size
+ * reports TBE_ERANGE from then on and the directory must be recreated.  In such a batch
+ * every key that gets an id keeps a unique one in [0, capacity), but which of the new
+ * keys get one is unspecified (the hash table, 2x capacity, may fill up first); the
+ * others get UINT64_MAX, and an engine batch containing them is rejected as invalid. */
 typedef struct tbe_directory tbe_directory;
 
 tbe_status tbe_dir_create(uint64_t capacity, int32_t device, tbe_directory **out);
 void tbe_dir_destroy(tbe_directory *dir);
 /* d_ids[i] = id of d_keys[i] (assigning new ones).  n < 2^32. */
 tbe_status tbe_dir_assign_device(tbe_directory *dir, const uint64_t *d_keys, uint64_t n, uint64_t *d_ids,
+                                 void *stream);
+/* d_ids[i] = id of d_keys[i], UINT64_MAX for a key never assigned (nothing changes). */
+tbe_status tbe_dir_lookup_device(tbe_directory *dir, const uint64_t *d_keys, uint64_t n, uint64_t *d_ids,
                                  void *stream);
 /* Ids assigned so far (synchronises the directory's device). */
 tbe_status tbe_dir_size(tbe_directory *dir, uint64_t *n_ids);

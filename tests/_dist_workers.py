@@ -45,14 +45,18 @@ def tb_route_worker(rank: int, world: int, port: int, out_dir: str):
     from distributedratelimiting.redis_amd import cluster
 
     rate = fill_rate_per_second(TB["tokens_per_period"], TB["period_ticks"])
-    ref = cref.CTokenBucket(cluster.keys_per_rank(TB["n_keys"], world), TB["token_limit"], rate)
+    cap = cluster.keys_per_rank(TB["n_keys"], world)
+    directory = cluster.HostDirectory(cap)
+    ref = cref.CTokenBucket(cap, TB["token_limit"], rate)
     out = {}
     for s in range(TB_STEPS):
         k, p, t = tb_batch(rank, s)
-        g, r = cluster.route_batch(lambda lk, lp, lt: ref.acquire_batch(lk, lp, lt), k, p, t)
+        g, r = cluster.route_batch(lambda lk, lp, lt: ref.acquire_batch(lk, lp, lt), k, p, t, directory)
         out[f"g{s}"], out[f"r{s}"] = g, r
     v, tt = ref.export_state()
     out["v"], out["t"] = v, tt
+    out["dir_keys"] = np.array(list(directory.ids.keys()), dtype=np.uint64)
+    out["dir_ids"] = np.array(list(directory.ids.values()), dtype=np.uint64)
     np.savez(os.path.join(out_dir, f"tb_{rank}.npz"), **out)
     ref.close()
     dist.barrier()
@@ -175,15 +179,18 @@ def q_route_worker(rank: int, world: int, port: int, out_dir: str):
     def cancel(lk, ids):
         return np.array([int(tab.cancel(int(k), int(i))) for k, i in zip(lk.tolist(), ids.tolist())])
 
+    directory = cluster.HostDirectory(Q["n_keys"])
     out = {}
     for s in range(Q_STEPS):
         k, p, t = q_batch(rank, s)
-        st, rem, ids = cluster.route_batch(wait, k, p, t)
+        st, rem, ids = cluster.route_batch(wait, k, p, t, directory)
         pick = q_cancel_pick(st)
-        hit = cluster.route_cancel(cancel, k[pick], ids[pick])
+        hit = cluster.route_cancel(cancel, k[pick], ids[pick], directory)
         log = tab.refresh(q_refresh_ts(s))
         out[f"st{s}"], out[f"rem{s}"], out[f"ids{s}"], out[f"hit{s}"] = st, rem, ids, hit
         out[f"log{s}"] = np.array(log, dtype=np.int64).reshape(-1, 3)
+    out["dir_keys"] = np.array(list(directory.ids.keys()), dtype=np.uint64)
+    out["dir_ids"] = np.array(list(directory.ids.values()), dtype=np.uint64)
     np.savez(os.path.join(out_dir, f"q_{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()

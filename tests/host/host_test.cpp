@@ -339,6 +339,49 @@ static void test_partition_reclaim() {
     CHECK(lim.ReclaimExpired() == 0);
 }
 
+static void test_token_registrations_released() {
+    // a long-lived token shared by many queued waits keeps no callback for a
+    // wait that has completed (granted here), so its registrations do not pile up.
+    FakeClock clk;
+    RedisQueueingTokenBucketRateLimiterOptions o;
+    static_cast<RedisTokenBucketRateLimiterOptions &>(o) = tb_options(1, 1, 1.0);
+    o.TimeSource = clk.fn();
+    o.QueueLimit = 3;
+    o.AutoReplenishment = false;
+    RedisQueueingTokenBucketRateLimiter lim(o);
+    CancellationTokenSource c;
+    CHECK(CancellationToken().Register([] {}) == 0);        // CancellationToken.None
+    for (int round = 0; round < 3; ++round) {
+        CHECK(lim.AttemptAcquire(1).IsAcquired());
+        auto q = lim.AcquireAsync(1, c.Token());            // queued, registered on the token
+        CHECK(q.wait_for(std::chrono::milliseconds(20)) == std::future_status::timeout);
+        CHECK(c.Token().RegisteredCount() == 1);
+        clk.advance(1000000);
+        CHECK(lim.TryReplenish());
+        CHECK(q.get().IsAcquired());
+        CHECK(c.Token().RegisteredCount() == 0);             // released on completion
+        clk.advance(1000000);
+    }
+    auto q = lim.AcquireAsync(1, c.Token());                // granted at once: never registered
+    CHECK(q.get().IsAcquired() && c.Token().RegisteredCount() == 0);
+}
+
+static void test_reclaim_survives_clock_step_back() {
+    // a reclaimed key's row is written back absent, so a new string starts from
+    // a full bucket even if the clock then steps back behind the old string's last grant.
+    FakeClock clk;
+    RedisTokenBucketRateLimiterOptions o = tb_options(2, 1, 1.0);
+    o.TimeSource = clk.fn();
+    o.PartitionLimit = 1;
+    PartitionedRedisTokenBucketRateLimiter lim(o);
+    CHECK(lim.AttemptAcquire("a", 2).IsAcquired());         // a's bucket: 0 tokens at T0
+    clk.advance(3000000);                                   // past a's 2 s TTL
+    CHECK(lim.ReclaimExpired() == 1);
+    clk.advance(-2900000);                                  // the system clock steps back
+    CHECK(lim.AttemptAcquire("b", 2).IsAcquired());         // b: fresh (absent) bucket, 2 tokens
+    CHECK(lim.GetAvailablePermits("b") == 0);
+}
+
 static void test_approximate_limiter() {
     // Expected values from oracle/semantics.py (ApproxClient + ApproxGlobalTable):
     //   lease 3 ok, lease 2 fails, wait 2 queues (available 1);
@@ -414,6 +457,8 @@ int main(int argc, char **argv) {
         test_tb_sequence();
         test_partitioned_concurrent();
         test_partition_reclaim();
+        test_reclaim_survives_clock_step_back();
+        test_token_registrations_released();
         test_queueing_limiter();
         test_queueing_cancel();
         test_approximate_limiter();

@@ -32,17 +32,29 @@ def _spawn(fn, *args):
                        start_method="spawn")
 
 
-def test_shard_batch_partition():
+def test_key_owner_and_directory():
+    """owner = top bits of mix64 for a power-of-two world, balanced; the
+    host directory assigns a bijection of [0, capacity) in first-seen order."""
     from distributedratelimiting.redis_amd import cluster
-    keys = np.array([5, 2, 7, 4, 9, 0, 3], dtype=np.uint64)
-    parts = cluster.shard_batch(keys, np.arange(7), np.arange(7) * 10, 3)
-    seen = np.concatenate([p[0] for p in parts])
-    assert sorted(seen.tolist()) == list(range(7))
-    for r, (idx, lk, pp, tt) in enumerate(parts):
-        assert np.all(keys[idx] % 3 == r)
-        assert np.all(np.diff(idx) > 0)                      # arrival order kept
-        assert np.array_equal(lk * 3 + r, keys[idx])
-        assert np.array_equal(pp, idx) and np.array_equal(tt, idx * 10)
+    keys = np.arange(200_000, dtype=np.uint64)
+    for world in (2, 4, 8):
+        own = cluster.key_owner(keys, world)
+        top = (cluster._mix64(keys) >> np.uint64(64 - (world.bit_length() - 1))).astype(np.int64)
+        assert np.array_equal(own, top)
+        cnt = np.bincount(own, minlength=world)
+        assert cnt.min() > 0.97 * keys.size / world
+    d = cluster.HostDirectory(1000)
+    a = d.assign(np.array([7, 3, 7, 9], np.uint64))
+    b = d.assign(np.array([9, 11, 3], np.uint64))
+    assert a[0] == a[2] and len({int(a[0]), int(a[1]), int(a[3]), int(b[1])}) == 4
+    assert b[0] == a[3] and b[2] == a[1]
+    assert np.array_equal(cluster.scramble_walk(np.arange(4, dtype=np.uint64), 1000), np.array(
+        [a[0], a[1], a[3], b[1]], np.uint64))                    # counters 0..3 in first-seen order
+    ids = cluster.scramble_walk(np.arange(1000, dtype=np.uint64), 1000)
+    assert np.array_equal(np.sort(ids), np.arange(1000, dtype=np.uint64))   # a bijection
+    small = cluster.HostDirectory(2)
+    out = small.assign(np.array([5, 6, 7], np.uint64))
+    assert small.overflow and out[2] == cluster.NO_ID
 
 
 def test_route_batch_matches_serial_reference(oracle_lib, tmp_path):
@@ -63,12 +75,17 @@ def test_route_batch_matches_serial_reference(oracle_lib, tmp_path):
             sl = slice(r * W.TB_N, (r + 1) * W.TB_N)
             assert np.array_equal(res[r][f"g{s}"], g[sl]), (s, r)
             assert np.array_equal(res[r][f"r{s}"], rem[sl]), (s, r)
+    from distributedratelimiting.redis_amd import cluster
     v, t = ref.export_state()
+    seen = 0
     for r in range(WORLD):
-        keys = np.arange(r, W.TB["n_keys"], WORLD)
-        n = keys.size
-        assert np.array_equal(res[r]["t"][:n], t[keys])
-        assert np.array_equal(res[r]["v"][:n].view(np.int64), v[keys].view(np.int64))
+        keys, ids = res[r]["dir_keys"].astype(np.int64), res[r]["dir_ids"].astype(np.int64)
+        assert np.all(cluster.key_owner(keys.astype(np.uint64), WORLD) == r)   # the owner's keys only
+        assert np.array_equal(res[r]["t"][ids], t[keys])
+        assert np.array_equal(res[r]["v"][ids].view(np.int64), v[keys].view(np.int64))
+        seen += keys.size
+    assert seen == np.unique(np.concatenate([W.tb_batch(r, s)[0] for r in range(WORLD)
+                                             for s in range(W.TB_STEPS)])).size
     ref.close()
 
 
@@ -121,6 +138,7 @@ def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
     way (cluster.route_cancel), then a replenish tick on every rank.  Expected = one
     serial queueing table: per step rank 0's batch, rank 1's, the cancels, the tick."""
     from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
+    from distributedratelimiting.redis_amd import cluster
     _spawn(W.q_route_worker, str(tmp_path))
     res = [np.load(tmp_path / f"q_{r}.npz") for r in range(WORLD)]
     Q = W.Q
@@ -135,8 +153,9 @@ def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
             exp = [ref.acquire(int(k[i]), int(p[i]), int(t[i]), ref_id(s, src, i)) for i in range(W.Q_N)]
             assert res[src][f"st{s}"].tolist() == [e[0] for e in exp], (s, src)
             assert res[src][f"rem{s}"].tolist() == [e[1] for e in exp], (s, src)
+            own = cluster.key_owner(k, WORLD)
             for i, x in enumerate(res[src][f"ids{s}"].tolist()):
-                owner_id[(int(k[i]) % WORLD, x)] = ref_id(s, src, i)
+                owner_id[(int(own[i]), x)] = ref_id(s, src, i)
         for src, (k, _, _) in enumerate(batches):
             pick = W.q_cancel_pick(res[src][f"st{s}"])
             want = [int(ref.cancel(int(k[i]), ref_id(s, src, int(i)))) for i in pick]
@@ -145,8 +164,9 @@ def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
         exp_log = ref.refresh(W.q_refresh_ts(s))
         got = []
         for r in range(WORLD):
+            gkey = dict(zip(res[r]["dir_ids"].tolist(), res[r]["dir_keys"].tolist()))
             for lk, x, rem in res[r][f"log{s}"].tolist():
-                got.append((lk * WORLD + r, owner_id[(r, x)], rem))
+                got.append((gkey[lk], owner_id[(r, x)], rem))
         got.sort(key=lambda e: e[0])   # stable: per-key drain order kept
         assert got == exp_log, s
     assert total_hits > 0

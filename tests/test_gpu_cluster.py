@@ -1,0 +1,129 @@
+"""The multi-GPU data path on the device (include/tbe_cluster.h): the routing partition,
+pack and gather kernels and the key directory, each against its host mirror in
+cluster.py (the code path the world-size-2 gloo tests drive), plus route_batch end to end
+through RCCL at world size 1 with the HIP engine deciding."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import cref
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(n, seed, hot=0.0):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, 1 << 40, n, dtype=np.uint64)
+    if hot:
+        pool = rng.integers(0, 1 << 40, 50, dtype=np.uint64)
+        k = np.where(rng.random(n) < hot, pool[rng.integers(0, 50, n)], k)
+    return k
+
+
+@pytest.mark.parametrize("n_owners", [1, 2, 3, 8, 64, 256])
+@pytest.mark.parametrize("n", [1, 4095, 4097, 300_000])
+def test_route_plan_matches_host(engine_lib, gpu, n_owners, n):
+    import torch
+    from distributedratelimiting.redis_amd import _capi, cluster
+    lib = _capi.load()
+    k = _keys(n, n_owners * 7 + n, hot=0.3)
+    dk = torch.from_numpy(k.view(np.int64)).to(gpu)
+    pos = torch.empty(n, dtype=torch.int32, device=gpu)
+    counts = torch.empty(n_owners, dtype=torch.int64, device=gpu)
+    work = torch.empty(lib.tbe_route_workspace_bytes(n, n_owners), dtype=torch.uint8, device=gpu)
+    assert lib.tbe_route_plan_device(dk.data_ptr(), n, n_owners, work.data_ptr(), pos.data_ptr(),
+                                     counts.data_ptr(), None) == 0
+    owner = cluster.key_owner(k, n_owners)
+    assert all(lib.tbe_key_owner(int(x), n_owners) == o for x, o in zip(k[:200].tolist(), owner[:200].tolist()))
+    order = np.argsort(owner, kind="stable")
+    want = np.empty(n, dtype=np.int64)
+    want[order] = np.arange(n)
+    torch.cuda.synchronize()
+    assert np.array_equal(pos.cpu().numpy().astype(np.int64), want)
+    assert np.array_equal(counts.cpu().numpy(), np.bincount(owner, minlength=n_owners))
+    # pack (send buffer) and gather (replies back to arrival order)
+    p = torch.from_numpy(np.arange(n, dtype=np.int32) % 7).to(gpu)
+    t = torch.from_numpy(np.arange(n, dtype=np.int64) * 3).to(gpu)
+    send = torch.empty((n, 3), dtype=torch.int64, device=gpu)
+    assert lib.tbe_route_pack_device(pos.data_ptr(), n, dk.data_ptr(), p.data_ptr(), t.data_ptr(),
+                                     send.data_ptr(), None) == 0
+    back = torch.empty_like(send)
+    assert lib.tbe_route_gather_device(pos.data_ptr(), n, send.data_ptr(), 3, back.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    s = send.cpu().numpy()
+    assert np.array_equal(s[:, 0].view(np.uint64), k[order]) and np.array_equal(s[:, 2], np.arange(n)[order] % 7)
+    b = back.cpu().numpy()
+    assert np.array_equal(b[:, 0].view(np.uint64), k) and np.array_equal(b[:, 1], np.arange(n) * 3)
+
+
+def test_directory_matches_host(engine_lib, gpu):
+    import torch
+    from distributedratelimiting.redis_amd import TbeError, cluster
+    cap = 100_000                                                   # > the 90k key space: no overflow
+    dd = cluster.DeviceDirectory(cap, device=0)
+    hd = cluster.HostDirectory(cap)
+    for b in range(5):
+        k = _keys(40_000, 100 + b, hot=0.5) % np.uint64(90_000)       # repeats within and across batches
+        got = dd.assign(torch.from_numpy(k.view(np.int64)).to(gpu)).cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, hd.assign(k)), b
+    assert dd.size() == hd.size() == len(np.unique(np.concatenate(
+        [_keys(40_000, 100 + b, hot=0.5) % np.uint64(90_000) for b in range(5)])))
+    probe = np.array([1 << 50, 3, 1 << 51], np.uint64)
+    lk = dd.lookup(torch.from_numpy(probe.view(np.int64)).to(gpu)).cpu().numpy().view(np.uint64)
+    assert np.array_equal(lk, hd.lookup(probe))
+    assert lk[0] == cluster.NO_ID and lk[2] == cluster.NO_ID
+    # capacity: exact while the new keys of a batch fit; an over-capacity batch gives
+    # unique ids in [0, capacity) to at most `capacity` keys and size() reports it
+    small = cluster.DeviceDirectory(1000, device=0)
+    hs = cluster.HostDirectory(1000)
+    k = np.arange(900, dtype=np.uint64) * np.uint64(7919)
+    first = small.assign(torch.from_numpy(k.view(np.int64)).to(gpu)).cpu().numpy().view(np.uint64)
+    assert np.array_equal(first, hs.assign(k)) and small.size() == 900
+    k = np.arange(3000, dtype=np.uint64) * np.uint64(7919) + np.uint64(5)
+    got = small.assign(torch.from_numpy(k.view(np.int64)).to(gpu)).cpu().numpy().view(np.uint64)
+    ok = got[got != cluster.NO_ID]
+    assert ok.size <= 100 and np.unique(ok).size == ok.size and (ok < 1000).all()
+    assert not set(ok.tolist()) & set(first.tolist())
+    with pytest.raises(TbeError):
+        small.size()
+
+
+def test_route_batch_device_world1(engine_lib, gpu):
+    """route_batch's device path (route kernels + RCCL all-to-all + directory + the HIP
+    engine) at world size 1, against the C restatement on the directory's dense ids."""
+    import torch
+    import torch.distributed as dist
+    from distributedratelimiting.redis_amd import TokenBucketEngine, cluster, fill_rate
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        cap = 200_000
+        eng = TokenBucketEngine(cap, 5, 2, 10_000_000, device=0)
+        dd = cluster.DeviceDirectory(cap, device=0)
+        hd = cluster.HostDirectory(cap)
+        ref = cref.CTokenBucket(cap, 5, fill_rate(2, 10_000_000))
+        rng = np.random.default_rng(2)
+
+        def decide(lk, lp, lt):
+            g = torch.empty(lk.numel(), dtype=torch.uint8, device=gpu)
+            r = torch.empty(lk.numel(), dtype=torch.int32, device=gpu)
+            eng.acquire_batch_device(lk, lp, lt, g, r, stream=torch.cuda.current_stream(gpu).cuda_stream)
+            return g, r
+
+        for b in range(3):
+            n = 150_000
+            k = (_keys(n, 9 + b, hot=0.2) % np.uint64(1 << 20)).astype(np.uint64)
+            p = rng.integers(0, 4, n).astype(np.int32)
+            t = (1_760_000_000_000_000 + b * 900_000 + np.sort(rng.integers(0, 900_000, n))).astype(np.int64)
+            g, r = cluster.route_batch(decide, torch.from_numpy(k.view(np.int64)).to(gpu), torch.from_numpy(p).to(gpu),
+                                       torch.from_numpy(t).to(gpu), dd)
+            g_ref, r_ref = ref.acquire_batch(hd.assign(k), p, t)
+            assert np.array_equal(g.cpu().numpy(), g_ref) and np.array_equal(r.cpu().numpy(), r_ref), b
+    finally:
+        dist.destroy_process_group()

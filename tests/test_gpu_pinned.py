@@ -30,3 +30,38 @@ def test_pinned_host_buffers(engine_lib, gpu):
     empty = PinnedArray(0, np.int64)
     assert empty.array.size == 0
     ref.close()
+
+
+def test_pinned_chunked_overlap(engine_lib, gpu):
+    """Batches of >= 2 chunks (4M requests each) from page-locked buffers take the chunked
+    path (copies overlapping the decisions): same replies and table as the C restatement,
+    including a ragged last chunk; an invalid request in the LAST chunk still rejects the
+    whole batch with nothing applied."""
+    from distributedratelimiting.redis_amd import TbeError, TokenBucketEngine, fill_rate
+    from distributedratelimiting.redis_amd.engine import PinnedArray
+    n_keys, n = 3_000_000, (1 << 24) + 12_345
+    eng = TokenBucketEngine(n_keys, 10, 1, 10_000_000, device=0)
+    ref = cref.CTokenBucket(n_keys, 10, fill_rate(1, 10_000_000))
+    bufs = [PinnedArray(n, d) for d in (np.uint64, np.int32, np.int64, np.uint8, np.int32)]
+    bk, bp, bt, bg, br = (b.array for b in bufs)
+    for b in range(3):
+        k, p, t = cref.gen_batch(0x5EED000B, n_keys, b, n, 10_000, 1, 3)
+        bk[:], bp[:], bt[:] = k, p, t
+        g, r = eng.acquire_batch(bk, bp, bt, bg, br)
+        g3, r3 = ref.acquire_batch(k, p, t, threads=8)
+        assert np.array_equal(g, g3) and np.array_equal(r, r3), b
+    v, tt = eng.export_state()
+    v_ref, t_ref = ref.export_state()
+    assert np.array_equal(tt, t_ref)
+    touched = t_ref != np.iinfo(np.int64).min
+    assert np.array_equal(v[touched].view(np.uint64), v_ref[touched].view(np.uint64))
+    k, p, t = cref.gen_batch(0x5EED000B, n_keys, 3, n, 10_000, 1, 3)
+    bk[:], bp[:], bt[:] = k, p, t
+    bp[n - 5] = -1
+    with pytest.raises(TbeError):
+        eng.acquire_batch(bk, bp, bt, bg, br)
+    v2, t2 = eng.export_state()
+    assert np.array_equal(t2, tt) and np.array_equal(v2.view(np.uint64), v.view(np.uint64))
+    for a in bufs:
+        a.free()
+    ref.close()

@@ -17,11 +17,11 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args); steady state: 15 warm-up batches age the
     # table into config B's denial-dominated regime before the timed ones
-    "walk": ([], []),
-    "rounds": ([], ["--no-walk"]),
-    "walk_steady": ([], ["--warmup", "15"]),
-    "rounds_steady": ([], ["--warmup", "15", "--no-walk"]),
-    "copy_only": (["TBE_FOLD_COPY_ONLY"], []),
+    "base": ([], []),
+    "base_steady": ([], ["--warmup", "15"]),
+    "narrow8": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=8", "TBE_TB_TAIL=512"], []),
+    "narrow8_steady": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=8", "TBE_TB_TAIL=512"], ["--warmup", "15"]),
+    "narrow6": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=6", "TBE_TB_TAIL=512"], []),
 }
 
 
@@ -33,7 +33,7 @@ def build():
     spec.loader.exec_module(m)
     os.makedirs(OUTDIR, exist_ok=True)
     for name, (defs, _) in VARIANTS.items():
-        lib = os.path.join(OUTDIR, f"libtbe_{'_'.join(defs) or 'base'}.so")
+        lib = os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so")
         if not os.path.exists(lib):
             m.build_engine(force=True, defines=defs, out=lib)
         print("built", name)
@@ -44,7 +44,7 @@ def run(rounds: int, steps: int):
     for r in range(rounds):
         for name, (_, extra) in VARIANTS.items():
             defs = VARIANTS[name][0]
-            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs) or 'base'}.so"))
+            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so"))
             args = ["--steps", str(steps), "--cpu-seconds", "0", "--no-host-buffer"]
             if "--warmup" not in extra:
                 args += ["--warmup", "2"]

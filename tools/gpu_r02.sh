@@ -17,7 +17,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_walk.py -x -q --timeout 200
 rc=$?; tail -3 "$OUT/r02_walk.log"; [ $rc -ne 0 ] && stop walk $rc
 fi
 if [ "${SKIP_SUITE:-0}" != 1 ]; then
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread \
     --ignore=tests/test_gpu_fullshape.py > "$OUT/r02_pytest_gpu.log" 2>&1
 rc=$?; tail -3 "$OUT/r02_pytest_gpu.log"; fatal $rc && stop suite $rc
 fi
