@@ -144,6 +144,8 @@ def main():
     n = args.batch
     total_steps = args.warmup + args.steps
     routed = dist and args.workload != "testapp"
+    if routed:   # the device path orders the engine on a real stream (cluster.device_stream)
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B)
     directory = cluster.DeviceDirectory(keys_local, device=dev.index) if routed else None
     bufs, raw = [], []

@@ -152,8 +152,7 @@ class DeviceDirectory:
         from . import _capi
         d_keys = d_keys.contiguous()
         ids = torch.empty(d_keys.numel(), dtype=torch.int64, device=d_keys.device)
-        st = fn(self._h, d_keys.data_ptr(), d_keys.numel(), ids.data_ptr(),
-                torch.cuda.current_stream(d_keys.device).cuda_stream)
+        st = fn(self._h, d_keys.data_ptr(), d_keys.numel(), ids.data_ptr(), device_stream(d_keys.device))
         if st != _capi.TBE_OK:
             raise _capi.TbeError(st, "directory call failed")
         return ids
@@ -208,7 +207,7 @@ def route_requests(keys, permits, ts_us, directory, group=None):
         from . import _capi
         lib = _capi.load()
         dev = keys.device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = device_stream(dev)
         keys = keys.contiguous()
         n = keys.numel()
         pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -264,7 +263,7 @@ def route_replies(plan: RoutePlan, cols, group=None):
                                input_split_sizes=plan.recv_counts, group=group)
         out = torch.empty_like(back)
         _check(lib.tbe_route_gather_device(plan.order.data_ptr(), plan.n, back.data_ptr(), k, out.data_ptr(),
-                                           torch.cuda.current_stream(dev).cuda_stream))
+                                           device_stream(dev)))
         return tuple(out[:, c] for c in range(k))
     k = len(cols)
     m = sum(plan.recv_counts)
@@ -334,6 +333,19 @@ def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
     out = np.empty(n, dtype=np.uint8)
     out[order] = back.numpy()
     return out
+
+
+def device_stream(dev) -> int:
+    """The current torch stream's handle for the device path.  The engine reads a NULL
+    handle as "inputs complete at the call" (include/tbe.h), which the default stream's
+    queued work is not, so the device path refuses it: run it inside
+    torch.cuda.stream(torch.cuda.Stream(...))."""
+    import torch
+    h = torch.cuda.current_stream(dev).cuda_stream
+    if not h:
+        raise ValueError("cluster device path: set a non-default torch.cuda.Stream as current "
+                         "(the default stream's NULL handle cannot order the engine's work)")
+    return h
 
 
 def _check(st: int) -> None:

@@ -1948,24 +1948,22 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     ALocal *__restrict__ rows = alocal + row0;
-#ifdef TBE_APPROX_DENSE
-    // Experiment ("streaming hints"): dense buckets pull the whole local-tier
-    // slice and write it back whole, with streaming hints unless TBE_APPROX_DENSE_PLAIN.
+    // A dense bucket (>= R/8 requests: config E has ~13,700 per bucket) pulls its whole
+    // local-tier slice with coalesced streaming loads and writes it back whole; a sparse one
+    // gathers the rows it touches.  (Round 1 dropped this variant after a wrong result that
+    // the rebuilt variant does not reproduce -- DESIGN.md §5 "Streaming hints".)
+#ifdef TBE_APPROX_NO_DENSE
+    constexpr bool dense = false;
+#else
     const bool dense = (e - s) >= (R >> 3);
+#endif
     if (dense) {
         for (uint32_t j = tid; j < R; j += kFoldBlock) {
             const ALocal *src = rows + (j < nrows ? j : nrows - 1);
-#ifdef TBE_APPROX_DENSE_PLAIN
-            sl[j] = *src;
-#else
             const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
             __builtin_memcpy(&sl[j], &v, sizeof v);
-#endif
         }
     }
-#else
-    constexpr bool dense = false;
-#endif
     for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
@@ -2106,13 +2104,9 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     __syncthreads();
     for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
         if (dense) {
-#if defined(TBE_APPROX_DENSE) && !defined(TBE_APPROX_DENSE_PLAIN)
             u32x4 v;
             __builtin_memcpy(&v, &sl[j], sizeof v);
             __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(rows + j));
-#else
-            rows[j] = sl[j];
-#endif
         } else if (dirty[j >> 5] & (1u << (j & 31))) {
             rows[j] = sl[j];
         }

@@ -60,6 +60,12 @@ def test_route_plan_matches_host(engine_lib, gpu, n_owners, n):
 
 def test_directory_matches_host(engine_lib, gpu):
     import torch
+    with torch.cuda.stream(torch.cuda.Stream(gpu)):   # the device path needs a real stream
+        _directory_matches_host(gpu)
+
+
+def _directory_matches_host(gpu):
+    import torch
     from distributedratelimiting.redis_amd import TbeError, cluster
     cap = 100_000                                                   # > the 90k key space: no overflow
     dd = cluster.DeviceDirectory(cap, device=0)
@@ -102,8 +108,10 @@ def test_route_batch_device_world1(engine_lib, gpu):
     s.close()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    side = torch.cuda.Stream(gpu)   # the device path orders its kernels on a real (non-NULL) stream
     try:
-        cap = 200_000
+        torch.cuda.set_stream(side)
+        cap = 400_000  # > distinct keys over the 3 batches (~330k)
         eng = TokenBucketEngine(cap, 5, 2, 10_000_000, device=0)
         dd = cluster.DeviceDirectory(cap, device=0)
         hd = cluster.HostDirectory(cap)
@@ -123,7 +131,15 @@ def test_route_batch_device_world1(engine_lib, gpu):
             t = (1_760_000_000_000_000 + b * 900_000 + np.sort(rng.integers(0, 900_000, n))).astype(np.int64)
             g, r = cluster.route_batch(decide, torch.from_numpy(k.view(np.int64)).to(gpu), torch.from_numpy(p).to(gpu),
                                        torch.from_numpy(t).to(gpu), dd)
-            g_ref, r_ref = ref.acquire_batch(hd.assign(k), p, t)
+            ids = hd.assign(k)
+            assert not hd.overflow
+            g_ref, r_ref = ref.acquire_batch(ids, p, t)
             assert np.array_equal(g.cpu().numpy(), g_ref) and np.array_equal(r.cpu().numpy(), r_ref), b
+        with pytest.raises(ValueError):                       # the NULL default stream is refused
+            torch.cuda.set_stream(torch.cuda.default_stream(gpu))
+            cluster.route_batch(decide, torch.zeros(4, dtype=torch.int64, device=gpu),
+                                torch.ones(4, dtype=torch.int32, device=gpu),
+                                torch.zeros(4, dtype=torch.int64, device=gpu), dd)
     finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(gpu))
         dist.destroy_process_group()
