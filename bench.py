@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
     ap.add_argument("--no-narrow", action="store_true",
                     help="4-byte replies even where TokenLimit <= 127 allows 1-byte ones (A/B)")
+    ap.add_argument("--no-strdir", action="store_true",
+                    help="skip the string-key directory leg (config B batches as key text)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     args = ap.parse_args()
@@ -337,6 +339,12 @@ def main():
                 a.free()
         hb.close()
 
+    # the string-key path: the same batches as key text
+    # "user-<key>" through the device string directory, after the timed region
+    strdir = None
+    if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_strdir:
+        strdir = bench_strdir(bufs[args.warmup:args.warmup + 2], keys_local, dev)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, keys_local, zkeys,
@@ -374,6 +382,7 @@ def main():
             **({"host_buffer_decisions_per_s": host_rate} if host_rate is not None else {}),
             **({"host_buffer_pinned_decisions_per_s": host_rate_pinned}
                if host_rate_pinned is not None else {}),
+            **({"string_directory": strdir} if strdir is not None else {}),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}
@@ -385,6 +394,45 @@ def main():
     eng.close()
     if dist:
         td.destroy_process_group()
+
+
+def bench_strdir(batches, n_keys: int, dev):
+    """Key text "user-<key>" of config-B batches through the device string directory
+    (tbe_sdir_*): a cold batch (every key new), a warm one (the next batch: about half its
+    keys known) and a lookup of it; HIP events on the directory's stream.  The ids must
+    equal the u64 key directory's on the same keys (both assign by first occurrence), a
+    size-independent check of the string path at full scale."""
+    import torch
+    from distributedratelimiting.redis_amd import cluster
+    from distributedratelimiting.redis_amd.strdir import StringDirectory, synthetic_key_text
+    out = {}
+    with torch.cuda.stream(torch.cuda.Stream(dev)):
+        texts = [synthetic_key_text(b[0], "user-") for b in batches]
+        sd = StringDirectory(n_keys, 16 * n_keys + (1 << 20), prefix="bench:", device=dev.index)
+        ud = cluster.DeviceDirectory(n_keys, device=dev.index)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ids = []
+        for j, (buf, offs, nb) in enumerate(texts):
+            ev[2 * j].record()
+            ids.append(sd.assign(buf, offs, nb))
+            ev[2 * j + 1].record()
+        ev[4].record()
+        look = sd.lookup(*texts[-1])
+        ev[5].record()
+        same = all(bool(torch.equal(i, ud.assign(b[0]))) for i, b in zip(ids, batches))
+        same = same and bool(torch.equal(look, ids[-1]))
+        torch.cuda.synchronize(dev)
+        n = batches[0][0].numel()
+        out = {"batch": n, "key_text_bytes": int(texts[0][2]),
+               "cold_assign_per_s": round(n / (ev[0].elapsed_time(ev[1]) / 1e3), 1),
+               "warm_assign_per_s": round(n / (ev[2].elapsed_time(ev[3]) / 1e3), 1),
+               "lookup_per_s": round(n / (ev[4].elapsed_time(ev[5]) / 1e3), 1),
+               "ids": sd.size(), "ids_equal_u64_directory": same,
+               "note": "key text 'user-<config-B key>' (prefix 'bench:'), exact byte compare; "
+                       "cold = all keys new, warm = the next batch"}
+        sd.close()
+        ud.close()
+    return out
 
 
 def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool,

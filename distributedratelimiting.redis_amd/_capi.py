@@ -172,6 +172,27 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_dir_lookup_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
     lib.tbe_dir_size.restype = c_int32
     lib.tbe_dir_size.argtypes = [c_void_p, POINTER(c_uint64)]
+    lib.tbe_key_text_lengths_device.restype = c_int32
+    lib.tbe_key_text_lengths_device.argtypes = [c_void_p, c_uint64, ctypes.c_uint32, c_void_p, c_void_p]
+    lib.tbe_key_text_device.restype = c_int32
+    lib.tbe_key_text_device.argtypes = [c_void_p, c_uint64, ctypes.c_char_p, ctypes.c_uint32, c_void_p, c_void_p,
+                                        c_void_p]
+    # string-key directory (include/tbe_strdir.h)
+    lib.tbe_sdir_create.restype = c_int32
+    lib.tbe_sdir_create.argtypes = [c_uint64, c_uint64, ctypes.c_char_p, ctypes.c_uint32, c_int32, POINTER(c_void_p)]
+    lib.tbe_sdir_destroy.restype = None
+    lib.tbe_sdir_destroy.argtypes = [c_void_p]
+    for fn in ("tbe_sdir_assign_device", "tbe_sdir_lookup_device"):
+        getattr(lib, fn).restype = c_int32
+        getattr(lib, fn).argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p]
+    lib.tbe_sdir_assign.restype = c_int32
+    lib.tbe_sdir_assign.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p]
+    lib.tbe_sdir_size.restype = c_int32
+    lib.tbe_sdir_size.argtypes = [c_void_p, POINTER(c_uint64)]
+    lib.tbe_sdir_key_of.restype = c_int32
+    lib.tbe_sdir_key_of.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]
+    lib.tbe_sdir_set_hash_bits.restype = c_int32
+    lib.tbe_sdir_set_hash_bits.argtypes = [c_void_p, ctypes.c_uint32]
     lib.tbe_numfmt_device.restype = c_int32
     lib.tbe_numfmt_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p]
     lib.tbe_layout.restype = c_int32

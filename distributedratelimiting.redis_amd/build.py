@@ -13,9 +13,9 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", n) for n in ("tbe_engine.hip", "tbe_tools.hip", "tbe_cluster.hip")]
+SOURCES = [os.path.join(HERE, "csrc", n) for n in ("tbe_engine.hip", "tbe_tools.hip", "tbe_cluster.hip", "tbe_strdir.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", n) for n in ("tbe_device.hpp", "tbe_numfmt.hpp", "tbe_hash.hpp")] + \
-    [os.path.join(ROOT, "include", n) for n in ("tbe.h", "tbe_tools.h", "tbe_cluster.h")]
+    [os.path.join(ROOT, "include", n) for n in ("tbe.h", "tbe_tools.h", "tbe_cluster.h", "tbe_strdir.h")]
 LIB = os.path.join(HERE, "libtbe.so")
 ARCH = "gfx950"
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",

@@ -112,7 +112,63 @@ __global__ void k_gen_zipf(uint64_t seed, ZipfParams Z, uint64_t g0, uint64_t n,
     }
 }
 
+struct KeyPrefix {
+    uint8_t b[32];
+    uint32_t len;
+};
+
+__device__ __forceinline__ uint32_t ndigits(uint64_t k) {
+    uint32_t d = 1;
+    while (k >= 10) {
+        k /= 10;
+        ++d;
+    }
+    return d;
+}
+
+__global__ void k_key_text_len(const uint64_t *__restrict__ keys, uint64_t n, uint32_t plen,
+                               uint64_t *__restrict__ lens) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        lens[i] = plen + ndigits(keys[i]);
+}
+
+__global__ void k_key_text(const uint64_t *__restrict__ keys, uint64_t n, KeyPrefix P,
+                           const uint64_t *__restrict__ offs, uint8_t *__restrict__ bytes) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t o = offs[i], e = offs[i + 1];
+        for (uint32_t j = 0; j < P.len && o + j < e; ++j) bytes[o + j] = P.b[j];
+        uint64_t k = keys[i];
+        for (uint64_t q = e; q > o + P.len; --q) {   // decimal digits, right-aligned
+            bytes[q - 1] = (uint8_t)('0' + k % 10);
+            k /= 10;
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int tbe_key_text_lengths_device(const uint64_t *d_keys, uint64_t n, uint32_t prefix_len,
+                                           uint64_t *d_lens, void *stream) {
+    if (n == 0) return 0;
+    if (!d_keys || !d_lens || prefix_len > 32) return 1;
+    const unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+    k_key_text_len<<<blocks, 256, 0, (hipStream_t)stream>>>(d_keys, n, prefix_len, d_lens);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+extern "C" int tbe_key_text_device(const uint64_t *d_keys, uint64_t n, const char *prefix, uint32_t prefix_len,
+                                   const uint64_t *d_offs, uint8_t *d_bytes, void *stream) {
+    if (n == 0) return 0;
+    if (!d_keys || !d_offs || !d_bytes || prefix_len > 32 || (prefix_len && !prefix)) return 1;
+    KeyPrefix P{};
+    for (uint32_t j = 0; j < prefix_len; ++j) P.b[j] = (uint8_t)prefix[j];
+    P.len = prefix_len;
+    const unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+    k_key_text<<<blocks, 256, 0, (hipStream_t)stream>>>(d_keys, n, P, d_offs, d_bytes);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 static double host_helper1(double x) {
     return std::fabs(x) > 1e-8 ? std::log1p(x) / x : 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x));

@@ -35,6 +35,16 @@ int tbe_gen_zipf_keys_device(uint64_t seed, uint64_t n_items, double s, uint64_t
  * build.  Enqueued on `stream`; returns 0 on success. */
 int tbe_numfmt_device(const double *d_in, double *d_out, uint64_t n, void *stream);
 
+/* Synthetic string keys (string-directory tests and benchmark): key text i = prefix +
+ * decimal(keys[i]).  lens[i] = prefix_len + its digit count (prefix_len <= 32); after the
+ * caller's scan into n + 1 offsets, the text of key i fills bytes[offs[i], offs[i+1])
+ * (digits right-aligned, zero-padded on the left when the span is longer).  Enqueued on
+ * `stream`; returns 0 on success. */
+int tbe_key_text_lengths_device(const uint64_t *d_keys, uint64_t n, uint32_t prefix_len, uint64_t *d_lens,
+                                void *stream);
+int tbe_key_text_device(const uint64_t *d_keys, uint64_t n, const char *prefix, uint32_t prefix_len,
+                        const uint64_t *d_offs, uint8_t *d_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,7 @@ import re
 import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("tbe.h", "tbe_tools.h", "tbe_cluster.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("tbe.h", "tbe_tools.h", "tbe_cluster.h", "tbe_strdir.h")]
 
 
 def declared_functions(headers=HEADERS):

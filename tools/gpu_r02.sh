@@ -42,14 +42,15 @@ fi
 timeout -k 10 420 python -u bench.py > "$OUT/r02_bench.log" 2>&1
 rc=$?; grep '^{' "$OUT/r02_bench.log" | cut -c1-400; fatal $rc && stop bench $rc
 [ $rc -ne 0 ] && stop bench $rc
+[ "${SKIP_PROF:-0}" = 1 ] && { echo r02-done; exit 0; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/r02_prof" -o run -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer \
+    python3 "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer --no-strdir \
     > "$OUT/r02_rocprof.log" 2>&1
 rc=$?; echo "[rocprof] rc=$rc"; [ $rc -ne 0 ] && stop rocprof $rc
 for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_uniform_$C" -o run -- \
-        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer \
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer --no-strdir \
         > "$OUT/pmc_uniform_$C.log" 2>&1
     rc=$?; echo "[pmc $C] rc=$rc"; [ $rc -ne 0 ] && stop pmc $rc
 done
