@@ -636,7 +636,6 @@ constexpr int kFoldBlock = 512;
 constexpr int kFoldPer = 4;                                 // requests per thread per chunk
 constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
 constexpr int kMaxRows = 1 << kMaxRBits;
-constexpr int kFoldTail = kFoldBlock;                       // compact pending list after round 1
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Slot slot_load_nt(const Slot *p) {
@@ -672,11 +671,45 @@ __device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
     return (dirty[j >> 5] >> (j & 31u)) & 1u;
 }
 
-// Full buckets (>= R/2 requests, uniform traffic): 512-thread workgroups with the rows'
-// field t cached in LDS (74.5 KB, two workgroups per CU), one chunk of 2048 requests.
-// k_fold below takes the other buckets.
+// Shape of k_fold_wide (profiles/r02_ablate_wide*.log): 512 threads x 2 requests per
+// chunk, the rows' field t derived per evaluation instead of cached, a 256-entry pending
+// list: 49.9 KB of LDS and 80 VGPRs, so three workgroups (24 waves) share a CU.  The
+// fold is latency-bound; against two workgroups of 4 requests per thread with a cached
+// field t (74.5 KB, 128 VGPRs) it takes 1.05 instead of 1.20 ms per config-B batch
+// (0.92 instead of 1.09 in the denial-dominated steady state).
+#ifndef TBE_WIDE_BLOCK
+#define TBE_WIDE_BLOCK 512
+#endif
+#ifndef TBE_WIDE_PER
+#define TBE_WIDE_PER 2
+#endif
+#ifndef TBE_WIDE_FT
+#define TBE_WIDE_FT 0
+#endif
+#ifndef TBE_WIDE_WAVES
+#define TBE_WIDE_WAVES 6                     // minimum waves per SIMD (register budget)
+#endif
+#ifndef TBE_WIDE_TAIL
+#define TBE_WIDE_TAIL 256
+#endif
+constexpr int kWideBlock = TBE_WIDE_BLOCK;
+constexpr int kWidePer = TBE_WIDE_PER;
+constexpr int kWideChunk = kWideBlock * kWidePer;
+constexpr int kWideTail = TBE_WIDE_TAIL;
+static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and tail list");
+// The rows' field t (TB:203 of the stored t_us): cached in LDS, or derived per evaluation
+#if TBE_WIDE_FT
+#define WIDE_FT_GET(j, srow) ft[j]
+#define WIDE_FT_SET(j, v) (ft[j] = (v))
+#else
+#define WIDE_FT_GET(j, srow) req_time_rel((srow).t_us == kAbsent ? 0 : (srow).t_us, TB, 0).new_t
+#define WIDE_FT_SET(j, v) ((void)0)
+#endif
+
+// Full buckets (>= R/2 requests, uniform traffic), shaped as above (three workgroups per
+// CU, chunks of 1024 requests).  k_fold below takes the other buckets.
 template <bool PACKED>
-__global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
+__global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
@@ -686,16 +719,18 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
-    __shared__ uint64_t aux[kFoldTail * 4];
-    __shared__ uint32_t wsum[kFoldBlock / 64];
+    __shared__ uint64_t aux[kWideTail * 4];
+    __shared__ uint32_t wsum[kWideBlock / 64];
     uint32_t *hcnt = reinterpret_cast<uint32_t *>(aux);
     uint32_t *t_kl_lid = reinterpret_cast<uint32_t *>(aux);
-    int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kFoldTail;
-    double *t_newt = reinterpret_cast<double *>(aux) + kFoldTail;
-    int64_t *t_exp = reinterpret_cast<int64_t *>(aux) + 2 * kFoldTail;
-    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + 3 * kFoldTail;
-    static_assert(kFoldTail * 4 * 8 >= kMaxRows * 4, "hcnt fits in aux");
+    int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kWideTail;
+    double *t_newt = reinterpret_cast<double *>(aux) + kWideTail;
+    int64_t *t_exp = reinterpret_cast<int64_t *>(aux) + 2 * kWideTail;
+    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + 3 * kWideTail;
+    static_assert(kWideTail * 4 * 8 >= kMaxRows * 4, "hcnt fits in aux");
+#if TBE_WIDE_FT
     __shared__ double ft[kMaxRows];
+#endif
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t loaded[kMaxRows / 32];
     __shared__ uint32_t dirty[kMaxRows / 32];
@@ -721,15 +756,15 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
 
-    uint32_t kl[kFoldPer];
-    int32_t pm[kFoldPer];
-    int64_t tsv[kFoldPer];
+    uint32_t kl[kWidePer];
+    int32_t pm[kWidePer];
+    int64_t tsv[kWidePer];
     uint32_t pend = 0;
     auto load_chunk = [&](uint32_t c) {
         pend = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
-            const uint32_t q = c + r * kFoldBlock + tid;
+        for (int r = 0; r < kWidePer; ++r) {
+            const uint32_t q = c + r * kWideBlock + tid;
             kl[r] = 0;
             pm[r] = 0;
             tsv[r] = 0;
@@ -750,20 +785,20 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
 
     load_chunk(s);   // in flight together with the dense slice
     if (dense) {
-        constexpr int kRowsPerThread = kMaxRows / kFoldBlock;
+        constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
         Slot tmp[kRowsPerThread];
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kFoldBlock;
+            const uint32_t j = tid + u * kWideBlock;
             tmp[u] = LD_S(rows + (j < nrows ? j : nrows - 1));   // unconditional: keeps tmp in VGPRs
         }
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kFoldBlock;
+            const uint32_t j = tid + u * kWideBlock;
             if (j < nrows) row[j] = tmp[u];
         }
     }
-    for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
+    for (uint32_t j = tid; j < (R + 31) / 32; j += kWideBlock) {
         loaded[j] = 0;
         dirty[j] = 0;
     }
@@ -771,25 +806,25 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
     // A/B floor (not a decision path): the fold's memory traffic without its rounds --
     // records and slice in, the whole slice and one reply per request out
     __syncthreads();
-    for (uint32_t c = s; c < e; c += kFoldChunk) {
+    for (uint32_t c = s; c < e; c += kWideChunk) {
         if (c != s) load_chunk(c);
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r)
-            if (pend & (1u << r)) put_reply(res, c + r * kFoldBlock + tid, kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
+        for (int r = 0; r < kWidePer; ++r)
+            if (pend & (1u << r)) put_reply(res, c + r * kWideBlock + tid, kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
     }
-    for (uint32_t j = tid; j < nrows; j += kFoldBlock) ST_S(rows + j, row[j]);
+    for (uint32_t j = tid; j < nrows; j += kWideBlock) ST_S(rows + j, row[j]);
     return;
 #endif
 
-    for (uint32_t c = s; c < e; c += kFoldChunk) {
+    for (uint32_t c = s; c < e; c += kWideChunk) {
         if (c != s) load_chunk(c);
-        for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
+        for (uint32_t j = tid; j < R; j += kWideBlock) own[j] = 0;
         if (count_hot && c == s)
-            for (uint32_t j = tid; j < R; j += kFoldBlock) hcnt[j] = 0;
+            for (uint32_t j = tid; j < R; j += kWideBlock) hcnt[j] = 0;
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
         if (count_hot) {
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
+            for (int r = 0; r < kWidePer; ++r)
                 if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
         }
         {
@@ -797,34 +832,34 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
             // buckets) and derive its field t.
             uint32_t mine = 0;
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 if (pend & (1u << r)) {
                     const uint32_t bit = 1u << (kl[r] & 31);
                     if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
                 }
             }
-            Slot tmp[kFoldPer];
+            Slot tmp[kWidePer];
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 tmp[r] = Slot{0.0, 0};                   // fully initialised: stays in VGPRs
                 if (mine & (1u << r)) tmp[r] = dense ? row[kl[r]] : rows[kl[r]];
             }
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 if (mine & (1u << r)) {
                     if (!dense) row[kl[r]] = tmp[r];
-                    ft[kl[r]] = new_t_of(tmp[r].t_us == kAbsent ? 0 : tmp[r].t_us);
+                    WIDE_FT_SET(kl[r], new_t_of(tmp[r].t_us == kAbsent ? 0 : tmp[r].t_us));
                 }
             }
         }
-        ReqTime rq[kFoldPer];
+        ReqTime rq[kWidePer];
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) rq[r] = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms)
+        for (int r = 0; r < kWidePer; ++r) rq[r] = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms)
                                                            : req_time(tsv[r], P.ttl_ms);
         __syncthreads();   // claimed rows and their field t visible
-        uint32_t rep[kFoldPer];
+        uint32_t rep[kWidePer];
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) rep[r] = 0;
+        for (int r = 0; r < kWidePer; ++r) rep[r] = 0;
         // Speculative rounds.  Every pending request evaluates the script
         // against its key's current row.  An evaluation that does not modify the row (a
         // deny without expiry) leaves it as it found it, so the key's pending requests up
@@ -834,36 +869,36 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
         // Election slot: (round << 12) | (4095 - local id); the max is the key's earliest
         // modifier of the newest round, so no reset between rounds.  Workgroup-uniform
         // loops: every thread runs every round and the only exits are __syncthreads_or.
-        auto eval_slots = [&](uint32_t round, Slot (&nrow)[kFoldPer]) {
+        auto eval_slots = [&](uint32_t round, Slot (&nrow)[kWidePer]) {
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 nrow[r] = Slot{0.0, 0};
                 if (pend & (1u << r)) {
                     nrow[r] = row[kl[r]];
                     bool m;
-                    rep[r] = tb_step_ft(nrow[r], ft[kl[r]], pm[r], rq[r], P, m);
-                    if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
+                    rep[r] = tb_step_ft(nrow[r], WIDE_FT_GET(kl[r], nrow[r]), pm[r], rq[r], P, m);
+                    if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kWideBlock + tid)));
                 }
             }
         };
-        auto resolve_slots = [&](uint32_t round, const Slot (&nrow)[kFoldPer]) {
+        auto resolve_slots = [&](uint32_t round, const Slot (&nrow)[kWidePer]) {
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 if (!(pend & (1u << r))) continue;
-                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid));
+                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kWideBlock + tid));
                 const uint32_t o = own[kl[r]];
                 if ((o >> 12) != round || o < tag) {
                     pend &= ~(1u << r);             // before the key's first modifier: decided
                 } else if (o == tag) {
                     row[kl[r]] = nrow[r];           // the row this round's evaluation produced
-                    ft[kl[r]] = rq[r].new_t;        // its field t (unused while absent)
+                    WIDE_FT_SET(kl[r], rq[r].new_t);        // its field t (unused while absent)
                     atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     pend &= ~(1u << r);
                 }
             }
         };
         {
-            Slot nrow[kFoldPer];
+            Slot nrow[kWidePer];
             eval_slots(1u, nrow);
             __syncthreads();
             resolve_slots(1u, nrow);
@@ -872,14 +907,14 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
         // compact list (one per thread) so later rounds evaluate one request per thread
         // instead of every slot of every lane.
         uint32_t n_tail;
-        const uint32_t tail_at = block_excl_scan<kFoldBlock>(__popc(pend), wsum, &n_tail);
+        const uint32_t tail_at = block_excl_scan<kWideBlock>(__popc(pend), wsum, &n_tail);
         uint32_t keep = ~0u;                     // slots whose reply this thread stores
-        if (n_tail != 0 && n_tail <= kFoldTail && !count_hot) {
+        if (n_tail != 0 && n_tail <= kWideTail && !count_hot) {
             uint32_t at = tail_at;
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kWidePer; ++r) {
                 if (pend & (1u << r)) {
-                    t_kl_lid[at] = kl[r] | ((uint32_t)(r * kFoldBlock + tid) << 16);
+                    t_kl_lid[at] = kl[r] | ((uint32_t)(r * kWideBlock + tid) << 16);
                     t_pm[at] = pm[r];
                     t_newt[at] = rq[r].new_t;
                     t_exp[at] = rq[r].exp_lt;
@@ -906,7 +941,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
                 if (tp) {
                     nr = row[tkl];
                     bool m;
-                    trep = tb_step_ft(nr, ft[tkl], tpm, trq, P, m);
+                    trep = tb_step_ft(nr, WIDE_FT_GET(tkl, nr), tpm, trq, P, m);
                     if (m) atomicMax(&own[tkl], tag);
                 }
                 __syncthreads();
@@ -916,7 +951,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
                         tp = false;
                     } else if (o == tag) {
                         row[tkl] = nr;
-                        ft[tkl] = trq.new_t;
+                        WIDE_FT_SET(tkl, trq.new_t);
                         atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
                         tp = false;
                     }
@@ -926,7 +961,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
             }
         } else if (n_tail != 0) {
             for (uint32_t round = 2;; ++round) {
-                Slot nrow[kFoldPer];
+                Slot nrow[kWidePer];
                 eval_slots(round, nrow);
                 __syncthreads();
                 resolve_slots(round, nrow);
@@ -934,18 +969,18 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_wide(
             }
         }
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
-            const uint32_t q = c + r * kFoldBlock + tid;
+        for (int r = 0; r < kWidePer; ++r) {
+            const uint32_t q = c + r * kWideBlock + tid;
             if (q < e && (keep & (1u << r))) put_reply(res, q, rep[r], narrow);
         }
     }
     __syncthreads();
     // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log)
-    for (uint32_t j = tid; j < nrows; j += kFoldBlock)
+    for (uint32_t j = tid; j < nrows; j += kWideBlock)
         if (row_line_dirty(dirty, j)) ST_S(rows + j, row[j]);
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
-        for (uint32_t j = tid; j < nrows; j += kFoldBlock) {
+        for (uint32_t j = tid; j < nrows; j += kWideBlock) {
             if (hcnt[j] >= kHotMin) {
                 const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
                 if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)hcnt[j] << 32) | (uint32_t)(row0 + j);
@@ -2658,14 +2693,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (e->packed) {
         // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
-        k_fold_wide<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+        k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
         k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
     } else {
-        k_fold_wide<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+        k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
             e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
         k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(

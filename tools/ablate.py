@@ -18,10 +18,14 @@ VARIANTS = {
     # name: (build defines, extra bench args); steady state: 15 warm-up batches age the
     # table into config B's denial-dominated regime before the timed ones
     "base": ([], []),
-    "base_steady": ([], ["--warmup", "15"]),
-    "narrow8": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=8", "TBE_TB_TAIL=512"], []),
-    "narrow8_steady": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=8", "TBE_TB_TAIL=512"], ["--warmup", "15"]),
-    "narrow6": (["TBE_FOLD_NARROW_ONLY", "TBE_TB_PER=6", "TBE_TB_TAIL=512"], []),
+    "wide768": (["TBE_WIDE_BLOCK=768", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0"], []),
+    "wide1024w8": (["TBE_WIDE_BLOCK=1024", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=8"], []),
+    "wide512x3": (["TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=6", "TBE_WIDE_TAIL=256"], []),
+    "wide768_steady": (["TBE_WIDE_BLOCK=768", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0"], ["--warmup", "15"]),
+    "wide1024w8_steady": (["TBE_WIDE_BLOCK=1024", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=8"],
+                          ["--warmup", "15"]),
+    "wide512x3_steady": (["TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=6", "TBE_WIDE_TAIL=256"],
+                         ["--warmup", "15"]),
 }
 
 
@@ -34,8 +38,7 @@ def build():
     os.makedirs(OUTDIR, exist_ok=True)
     for name, (defs, _) in VARIANTS.items():
         lib = os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so")
-        if not os.path.exists(lib):
-            m.build_engine(force=True, defines=defs, out=lib)
+        m.build_engine(defines=defs, out=lib)   # sha256-stamped: rebuilt when sources change
         print("built", name)
 
 
@@ -45,7 +48,7 @@ def run(rounds: int, steps: int):
         for name, (_, extra) in VARIANTS.items():
             defs = VARIANTS[name][0]
             env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so"))
-            args = ["--steps", str(steps), "--cpu-seconds", "0", "--no-host-buffer"]
+            args = ["--steps", str(steps), "--cpu-seconds", "0", "--no-host-buffer", "--no-strdir"]
             if "--warmup" not in extra:
                 args += ["--warmup", "2"]
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + extra, env=env,
