@@ -25,6 +25,7 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait):
     clients = [ApproxClient(limit, tokens, ticks, qlimit, order) for _ in range(n_clients)]
     table = ApproxGlobalTable(clients[0].decay_rate)
     counts = [torch.zeros(n_keys, dtype=torch.int32, device=gpu) for _ in range(n_clients)]
+    torch.cuda.synchronize()   # the engine's NULL-stream calls take inputs complete at the call
     rid = 0
     for epoch in range(6):
         for r in range(n_clients):
@@ -86,6 +87,7 @@ def test_golden_sync_trace_on_gpu(engine_lib, gpu, name):
     cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
     for i in range(len(g["counts"])):
         cnt.fill_(int(g["counts"][i]))
+        torch.cuda.synchronize()
         eng.sync(cnt, 1, 0, int(g["ts_us"][i]), 0)
         _, gl, est, _, _ = eng.local_state(0)
         assert gl == int(g["global_score"][i]), i
@@ -150,6 +152,7 @@ def test_zero_permit_waits_queue(engine_lib, gpu, order):
         assert eng.cancel(np.array([1], np.uint64), np.array([102], np.int64)).tolist() == [1]
         assert cli.cancel(1, 102)
     counts = torch.zeros(4, dtype=torch.int32, device=gpu)
+    torch.cuda.synchronize()
     tbl = ApproxGlobalTable(cli.decay_rate)
     ts = S_US
     for epoch in range(3):
@@ -177,6 +180,7 @@ def test_global_tier_snapshot_restore(engine_lib, gpu):
     a = mk()
     rng = np.random.default_rng(8)
     counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    torch.cuda.synchronize()
     v0, p0, t0 = a.export_global()
     assert (t0 == ABS).all() and (v0 == 0).all() and (p0 == 0).all()
     ts = S_US
@@ -216,7 +220,9 @@ def test_global_tier_snapshot_restore(engine_lib, gpu):
             assert c.local_state(key)[1:3] == d.local_state(key)[1:3]
     # past the one-day TTL every key is absent again: the next sync starts from {0, 0, now}
     day = 86_400 * 1_000_000
-    b.sync(torch.zeros(n_keys, dtype=torch.int32, device=gpu), 1, 0, ts + day + 2_000, 0)
+    zero = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    torch.cuda.synchronize()
+    b.sync(zero, 1, 0, ts + day + 2_000, 0)
     vb, pb, _ = b.export_global()
     assert (pb == 0.0).all() and (vb == 0.0).all()
     with pytest.raises(TbeError):

@@ -57,7 +57,7 @@ def test_wait_and_refresh_device(engine_lib, gpu, order, n_keys, qlimit, n, roun
             lk = torch.empty(cap, dtype=torch.int64, device=gpu)
             li = torch.empty(cap, dtype=torch.int64, device=gpu)
             lr = torch.empty(cap, dtype=torch.int32, device=gpu)
-            cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+            cnt = torch.empty(1, dtype=torch.int32, device=gpu)   # the tick zeroes it on its stream
             eng.refresh_device(t, lk, li, lr, cnt)
             eng.synchronize()
             k1, i1, r1 = _sorted_log(lk, li, lr, cnt)
@@ -81,14 +81,15 @@ def test_refresh_device_capacity_checked(engine_lib, gpu):
     keys = np.arange(n, dtype=np.int64) % 100
     d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
     d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
-    eng.wait_batch_device(_dev(keys, gpu), torch.ones(n, dtype=torch.int32, device=gpu),
-                          torch.full((n,), S_US, dtype=torch.int64, device=gpu), d_st, d_rem, 0)
+    ones, full = torch.ones(n, dtype=torch.int32, device=gpu), torch.full((n,), S_US, dtype=torch.int64, device=gpu)
+    torch.cuda.synchronize()   # NULL stream: inputs must be complete at the call (include/tbe.h)
+    eng.wait_batch_device(_dev(keys, gpu), ones, full, d_st, d_rem, 0)
     eng.synchronize()
     assert eng.refresh_bound() == 100 * 2   # n_keys * min(QueueLimit, TokenLimit)
     small = torch.empty(10, dtype=torch.int64, device=gpu)
     with pytest.raises(TbeError):
         eng.refresh_device(S_US + 1, small, small, small.view(torch.int32)[:10],
-                           torch.zeros(1, dtype=torch.int32, device=gpu))
+                           torch.empty(1, dtype=torch.int32, device=gpu))
 
 
 def test_config_d_shape_device(engine_lib, gpu):
@@ -104,7 +105,7 @@ def test_config_d_shape_device(engine_lib, gpu):
     lk = torch.empty(cap, dtype=torch.int64, device=gpu)
     li = torch.empty(cap, dtype=torch.int64, device=gpu)
     lr = torch.empty(cap, dtype=torch.int32, device=gpu)
-    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    cnt = torch.empty(1, dtype=torch.int32, device=gpu)
     d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
     d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
     for b in range(4):
@@ -132,6 +133,7 @@ def test_approx_acquire_device(engine_lib, gpu, order, qlimit, wait):
     client = ApproxClient(limit, tokens, ticks, qlimit, order)
     table = ApproxGlobalTable(client.decay_rate)
     counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    torch.cuda.synchronize()   # NULL stream: buffers complete at the call (include/tbe.h)
     d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
     d_av = torch.empty(n, dtype=torch.int32, device=gpu)
     rid = 0

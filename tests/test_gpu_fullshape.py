@@ -153,7 +153,7 @@ def test_config_d_full_shape(engine_lib, gpu):
         lk = torch.empty(cap, dtype=torch.int64, device=gpu)
         li = torch.empty(cap, dtype=torch.int64, device=gpu)
         lr = torch.empty(cap, dtype=torch.int32, device=gpu)
-        cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+        cnt = torch.empty(1, dtype=torch.int32, device=gpu)   # zeroed by the tick on its stream
         tick = T0_US + (b + 1) * interval
         eng.refresh_device(tick, lk, li, lr, cnt, stream=sh)
         stream.synchronize()

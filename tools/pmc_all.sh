@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 for W in ${WORKLOADS:-uniform zipf queue approx}; do
     for C in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$C" -o run -- \
-            python3 "$ROOT/bench.py" --workload $W --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline \
+            python3 "$ROOT/bench.py" --workload $W --steps 2 --warmup 1 --cpu-seconds 0 --no-stage-timing --no-pipeline --no-host-buffer --no-strdir \
             > "$OUT/pmc_${W}_$C.log" 2>&1
         rc=$?
         echo "[pmc $W $C] rc=$rc"

@@ -18,9 +18,18 @@ STAGE = {"k_hist": "hist", "k_colscan": "colscan", "k_scatter": "scatter", "k_sc
          "k_hot_replies": "hot", "k_hot_update": "hot"}
 
 
+def our_kernels():
+    """Kernel names defined in the engine's HIP sources (torch / rocPRIM kernels of the
+    benchmark harness are not part of a step)."""
+    names = set()
+    for f in glob.glob(os.path.join(ROOT, "distributedratelimiting.redis_amd", "csrc", "*.hip")):
+        names.update(re.findall(r"\bvoid\s+(k_\w+)\s*\(", open(f).read()))
+    return names
+
+
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
-    m = re.search(r"(k_\w+)", n)
+    m = re.search(r"\b(k_\w+)", n)
     base = m.group(1) if m else n.split("(")[0]
     t = re.search(r"k_\w+<([^>]*)>", n)
     return base + (f"<{t.group(1)}>" if t else "")
@@ -67,13 +76,14 @@ def main():
     marker = {"uniform": "k_fold_wide<true>", "zipf": "k_fold_wide<true>", "queue": "k_fold_q",
               "approx": "k_fold_a"}
     skip = ("k_gen_batch", "k_init_table", "k_init_approx", "k_count_queued", "k_gen_zipf")
+    ours = our_kernels()
     for w, kern in by_w.items():
         m = kern.get(marker.get(w, ""), {}).get("dispatches")
         if not m:
             continue
         tot = 0.0
         for k, d in kern.items():
-            if k.split("<")[0] in skip or "hbm_bytes_per_launch" not in d:
+            if k.split("<")[0] in skip or k.split("<")[0] not in ours or "hbm_bytes_per_launch" not in d:
                 continue
             tot += d["hbm_bytes_per_launch"] * d["dispatches"] / m
         step[w] = round(tot, 1)
