@@ -59,9 +59,9 @@ def _pmc_traffic(workload, kernels):
 
 
 PMC_KERNELS = {
-    ("queue", "fold"): ["k_fold_q"],
+    ("queue", "fold"): ["k_fold_q<true>"],
     ("queue", "drain"): ["k_drain"],
-    ("queue", "scatter"): ["k_scatter<unsigned long, true, true>", "k_scatter<unsigned int, true, true>"],
+    ("queue", "scatter"): ["k_scatter_rec<true, false, true>", "k_scatter_rec<false, false, true>"],
     ("approx", "fold"): ["k_fold_a"],
     ("approx", "scatter"): ["k_scatter<unsigned long, true, false>", "k_scatter<unsigned int, true, false>"],
 }
@@ -77,6 +77,23 @@ def _roofline(name, alg_bytes, ms, note, workload=None):
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4),
             "alg_bytes_note": note,
             "timing": "HIP events on the engine's launch stream over the timed region"}
+
+
+def _step_roofline(line, alg, note, workload):
+    """Whole-step figures beside the dominant kernel's: §8(d)'s algorithmic bytes over the
+    timed ms_per_step, and the PMC bytes of one step (tools/pmc_summary.py), if committed."""
+    r = line.get("roofline")
+    if r is None:
+        return
+    import json
+    achieved = alg / (line["ms_per_step"] * 1e-3) / 1e9
+    r.update({"step_alg_bytes": int(alg), "step_alg_note": note, "step_achieved": round(achieved, 1),
+              "step_frac": round(achieved / HBM_PEAK_GBS, 4)})
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")) as f:
+            r["step_traffic"] = json.load(f).get("step_hbm_bytes", {}).get(workload)
+    except (OSError, ValueError):
+        r["step_traffic"] = None
 
 
 def run(args, lib, dev, world, rank, dist):
@@ -108,7 +125,7 @@ def run_queue(args, lib, dev, world, rank, dist):
     total = warm + steps
     eng = QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, args.period_ticks,
                                     args.queue_limit, 0, device=dev.index,
-                                    stage_timing=not args.no_stage_timing, max_batch=n)
+                                    stage_timing=not args.no_stage_timing, max_batch=n, pack=not args.no_pack)
     seed = SEED_D + 7919 * rank
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -167,19 +184,25 @@ def run_queue(args, lib, dev, world, rank, dist):
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
     u = _distinct(n, kl)
+    packed = bool(eng.layout().get("packed"))
     if name == "fold":
-        # wide records (key 4, permits 4, ts 8, arrival index 4) + packed reply 4 per request;
-        # per distinct key: bucket row 16 + queue header 8, read and written; 8 per enqueue
-        alg = n * 24 + u * 48 + q_last * 8
-        note = "n*24 + distinct*48 + enqueued*8 (last batch's enqueues)"
+        # records (packed: u64 record 8 + arrival index 4; wide: key 4, permits 4, ts 8,
+        # index 4) + packed reply 4 per request; per distinct key: bucket row 16 + queue
+        # header 8, read and written; 8 per enqueue
+        rec = 12 if packed else 20
+        alg = n * (rec + 4) + u * 48 + q_last * 8
+        note = f"n*{rec + 4} + distinct*48 + enqueued*8 (last batch's enqueues)"
     elif name == "drain":
         # every key's queue header 8; per grant: ring entry 8 + log record 20 (lower bound)
         alg = kl * 8 + d_last * 28
         note = "n_keys*8 + grants*28 (lower bound: rows of keys with queues not counted)"
     elif name == "scatter":
-        # per pass: read the caller's key 8 + permits 4 + ts 8 (pass 0) or one wide record
-        # 20; write the wide record {key 4, permits 4, ts 8, index 4} and perm 4
-        alg, note = n * 44, "n*44 (wide records, per pass)"
+        # per pass: read the caller's key 8 + permits 4 + ts 8 (pass 0) or one record (packed
+        # 8 + index 4, wide 20); write the record and perm 4 (averaged over the two passes)
+        if packed:
+            alg, note = n * 32, "n*32 (packed records + index, per pass: (36 + 28) / 2)"
+        else:
+            alg, note = n * 44, "n*44 (wide records, per pass)"
     else:
         alg = n * 20
         note = "n*20"
@@ -199,6 +222,10 @@ def run_queue(args, lib, dev, world, rank, dist):
         "roofline": _roofline(name, alg, ms, note, "queue"),
         "cpu_baseline": None,
     }
+    # SURVEY.md §8(d) config D, whole step: the B formula (W ~ distinct keys x grant share)
+    # + 8 B per enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
+    _step_roofline(line, n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8,
+                   "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)", "queue")
     eng.close()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_queue(args, kl)
@@ -326,6 +353,9 @@ def run_approx(args, lib, dev, world, rank, dist):
         "roofline": _roofline(name, alg, ms, note, "approx"),
         "cpu_baseline": None,
     }
+    # SURVEY.md §8(d) config E, whole step: 8+4+1 in/out + 8 local-tier state per decision,
+    # K_shared * (4 count + 24 v,p,t) per refresh
+    _step_roofline(line, n * 21 + kshared * 28, "21*N + 28*K_shared (one refresh per batch)", "approx")
     eng.close()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_approx(args, kshared)
@@ -333,28 +363,28 @@ def run_approx(args, lib, dev, world, rank, dist):
 
 
 def cpu_approx(args, kshared):
-    """The Python restatement (oracle/semantics.py ApproxClient, one client, pure Python):
-    AcquireCore over the first 2^16 requests of each config-E batch plus a refresh of the
-    keys those requests touched, until ~min(args.cpu_seconds, 10) s."""
+    """oracle/tb_ref.c tba_* (the C restatement of A's local tier and sync, one client, one
+    thread): AcquireCore over the first 2^24 requests of each config-E batch, then that
+    batch's refresh epoch over every shared key (collect + sync script replay), until
+    ~args.cpu_seconds."""
     from oracle import cref
-    from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
 
-    c = ApproxClient(args.token_limit, args.tokens_per_period, args.period_ticks, 0, 0)
-    table = ApproxGlobalTable(c.decay_rate)
-    sample = min(args.batch, 1 << 16)
+    c = cref.CApprox(kshared, args.token_limit, args.tokens_per_period, args.period_ticks, 0, 0)
+    sample = min(args.batch, 1 << 24)
     done, spent, b = 0, 0.0, 0
-    budget = min(args.cpu_seconds, 10.0)
-    while spent < budget and b < 64:
+    while spent < args.cpu_seconds and b < 64:
         k, p, _ = cref.gen_batch(SEED_E, kshared, b, args.batch, args.interval_us)
-        k, p = k[:sample].tolist(), p[:sample].tolist()
+        k, p = k[:sample], p[:sample]
         t0 = time.perf_counter()
-        for key, pm in zip(k, p):
-            c.acquire(key, pm)
-        approx_refresh_all([c], table, T0_US + (b + 1) * args.interval_us, 0, sorted(set(k)))
+        c.acquire_batch(k, p, wait=False, id_base=b * args.batch, threads=1)
+        counts = c.collect()
+        c.sync(counts, 1, 0, T0_US + (b + 1) * args.interval_us, 0, threads=1)
         spent += time.perf_counter() - t0
         done += sample
         b += 1
+    c.close()
     return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} requests of each of {b} config-E batches + a refresh of their "
-                      f"keys ({done} decisions, {spent:.1f} s), oracle/semantics.py pure Python",
+            "sample": f"first {sample} requests of each of {b} config-E batches, each followed by a "
+                      f"refresh epoch over all {kshared} keys ({done} decisions, {spent:.1f} s), "
+                      f"oracle/tb_ref.c tba_* single thread",
             "host_cpus": os.cpu_count()}

@@ -535,14 +535,17 @@ __device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restri
 // timestamps, and pack; otherwise read the previous pass's records.
 // HOT (with FIRST): a hot key's record carries its run's partition key (hot_sortkey)
 // in the key field.
-template <bool FIRST, bool HOT = false>
+// IDX (queueing kind): each request's arrival index travels beside its record (a second,
+// 4-byte staging round); pass 0 generates it.
+template <bool FIRST, bool HOT = false, bool IDX = false>
 __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
     const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
     uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
-    uint32_t nb = 0, int r_bits = 0) {
+    uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
+    uint32_t *__restrict__ iout = nullptr) {
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
@@ -608,13 +611,36 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         }
     }
     __syncthreads();
+    uint32_t gpos[kPartItems];
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int j = it * kPartBlock + tid;
         if (j < nvalid) {
             const uint64_t s = stage[j];
             const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
-            rout[goff[d] + (uint32_t)j - L.lstart[d]] = s;   // runs merge in L2: keep cached
+            gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
+            rout[gpos[it]] = s;   // runs merge in L2: keep cached
+        }
+    }
+    if (IDX) {
+        uint32_t *stage32 = reinterpret_cast<uint32_t *>(stage);
+        uint32_t iv[kPartItems];
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            iv[it] = (e < nvalid) ? (FIRST ? (uint32_t)(base + e) : iin[base + e]) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = it * kPartBlock + tid;
+            if (e < nvalid) stage32[lpos[it]] = iv[it];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int j = it * kPartBlock + tid;
+            if (j < nvalid) iout[gpos[it]] = stage32[j];
         }
     }
     if (FIRST && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
@@ -1677,17 +1703,30 @@ __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t
     return (uint64_t)(head & 0xFFFFu) | ((uint64_t)(cnt & 0xFFFFu) << 16) | ((uint64_t)qsum << 32);
 }
 
-constexpr int kQBlock = 512;                       // k_fold_q workgroup (4 waves/SIMD at 2 per CU)
-constexpr int kQItems = 4;
+#ifndef TBE_Q_BLOCK
+#define TBE_Q_BLOCK 512
+#endif
+#ifndef TBE_Q_ITEMS
+#define TBE_Q_ITEMS 4
+#endif
+#ifndef TBE_Q_WAVES
+#define TBE_Q_WAVES 4
+#endif
+constexpr int kQBlock = TBE_Q_BLOCK;               // k_fold_q workgroup (two per CU: 56.5 KB of LDS)
+constexpr int kQItems = TBE_Q_ITEMS;
 constexpr int kQChunk = kQBlock * kQItems;         // 2048 requests per chunk
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
 // the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
 // LDS and its ring in HBM.  A ring entry written in one round and read (evicted) in a
 // later round of the same workgroup is ordered by the round's __syncthreads
 // (workgroup-scope fence; one CU, one vector L1).
-__global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
+// PACKED: requests arrive as packed records (PackFmt; permit code min(p, TokenLimit + 1),
+// which leaves REJECTED exactly where p > TokenLimit) beside their arrival indices.
+template <bool PACKED>
+__global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint32_t *__restrict__ sidx,
+    const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
     uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
@@ -1714,6 +1753,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
     // pulls its whole slice of rows and queue headers with coalesced loads and writes it
     // back whole; a sparse one gathers and writes back only the rows it touches.
     const bool dense = (e - s) >= (R >> 3);
+    const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     if (dense) {
         for (uint32_t j = tid; j < R; j += kQBlock) {
             const uint32_t jj = j < nrows ? j : nrows - 1;
@@ -1739,9 +1779,15 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(
         for (int r = 0; r < kQItems; ++r) {
             const uint32_t q = c + r * kQBlock + tid;
             if (q < e) {
-                kl[r] = skeys[q] & rmask;
-                pm[r] = sperm[q];
-                ts[r] = sts[q];
+                if (PACKED) {
+                    uint32_t k;
+                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts[r]);
+                    kl[r] = k & rmask;
+                } else {
+                    kl[r] = skeys[q] & rmask;
+                    pm[r] = sperm[q];
+                    ts[r] = sts[q];
+                }
                 ai[r] = sidx[q];
                 pend |= 1u << r;
             } else {
@@ -2335,7 +2381,7 @@ struct tbe_engine {
     int r_bits = 0;          // bucket = key >> r_bits
     uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
     int passes = 0;          // 8-bit LSD passes over the bucket id
-    bool packed = false;     // token bucket: passes move packed u64 records (PackFmt)
+    bool packed = false;     // token bucket and queueing kinds: passes move packed u64 records (PackFmt)
     bool narrow = false;     // token bucket, packed, TokenLimit <= 127: one-byte replies (put_reply)
     PackFmt pf{};
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
@@ -2566,6 +2612,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (n == 0) return TBE_OK;
     if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
                                        (unsigned long long)n);
+    if (e->packed && !ts) return fail(e, TBE_EINVAL, "null timestamps");
     const bool pipe = e->pipeline;
     Workspace &w = e->ws[pipe ? e->ws_cur : 0];
     tbe_status rc = ensure_workspace(e, w, n);
@@ -2623,7 +2670,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_colscan<<<kDigits, kBlock, 0, sp>>>(w.blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, sp);
         stage_begin(e, ST_SCATTER, sp);
-        if (e->packed && p == 0 && hot)
+        if (e->packed && wait && p == 0)
+            k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
+        else if (e->packed && wait)
+            k_scatter_rec<false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0,
+                w.pass[p - 1].idx, out.idx);
+        else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits);
@@ -2687,10 +2743,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         QParams q = e->qp;
         q.id_base = id_base;
         q.wait = e->wait_mode;
-        k_fold_q<<<e->nbuckets, kQBlock, 0, sf>>>(
-            sorted.keys, sorted.permits, sorted.ts, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
-            e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+        if (e->packed)
+            k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
+                nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
+                e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
+                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+        else
+            k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
+                sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
+                e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
+                e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (e->packed) {
         // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
@@ -2842,11 +2904,11 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
             e->pf.kmask = (kbits >= 64) ? ~0ull : ((1ull << kbits) - 1);
             e->pf.pc_max = (c.token_limit == INT32_MAX) ? INT32_MAX : c.token_limit + 1;
             e->pf.wb = 64 - kbits - pbits - 1;
-            return c.kind == TBE_KIND_TOKEN_BUCKET && e->pf.wb >= 32 && kbits <= 32 &&
-                   (c.flags & TBE_FLAG_NO_PACK) == 0;
+            return (c.kind == TBE_KIND_TOKEN_BUCKET || c.kind == TBE_KIND_QUEUEING) && e->pf.wb >= 32 &&
+                   kbits <= 32 && (c.flags & TBE_FLAG_NO_PACK) == 0;
         };
         uint32_t hot_cap = 0;
-        if ((c.flags & TBE_FLAG_NO_HOT) == 0) {
+        if ((c.flags & TBE_FLAG_NO_HOT) == 0 && c.kind == TBE_KIND_TOKEN_BUCKET) {
             const uint64_t room = (1ull << (kDigitBits * e->passes)) - e->nbuckets;
             hot_cap = (uint32_t)std::min<uint64_t>(kHotKeysMax, room);
             if (hot_cap < 16) hot_cap = 0;
@@ -2858,7 +2920,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
-        e->narrow = e->packed && c.token_limit <= 127 && (c.flags & TBE_FLAG_NO_NARROW) == 0;
+        e->narrow = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127 &&
+                    (c.flags & TBE_FLAG_NO_NARROW) == 0;
     }
 
     auto bail = [&](tbe_status st) {

@@ -15,17 +15,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
-    # name: (build defines, extra bench args); steady state: 15 warm-up batches age the
-    # table into config B's denial-dominated regime before the timed ones
-    "base": ([], []),
-    "wide768": (["TBE_WIDE_BLOCK=768", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0"], []),
-    "wide1024w8": (["TBE_WIDE_BLOCK=1024", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=8"], []),
-    "wide512x3": (["TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=6", "TBE_WIDE_TAIL=256"], []),
-    "wide768_steady": (["TBE_WIDE_BLOCK=768", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0"], ["--warmup", "15"]),
-    "wide1024w8_steady": (["TBE_WIDE_BLOCK=1024", "TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=8"],
-                          ["--warmup", "15"]),
-    "wide512x3_steady": (["TBE_WIDE_PER=2", "TBE_WIDE_FT=0", "TBE_WIDE_WAVES=6", "TBE_WIDE_TAIL=256"],
-                         ["--warmup", "15"]),
+    # name: (build defines, extra bench args)
+    "q_base": ([], ["--workload", "queue"]),
+    "q_nopack": ([], ["--workload", "queue", "--no-pack"]),
+    "q768": (["TBE_Q_BLOCK=768", "TBE_Q_ITEMS=2", "TBE_Q_WAVES=6"], ["--workload", "queue"]),
 }
 
 

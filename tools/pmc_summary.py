@@ -73,7 +73,7 @@ def main():
     # whole-step HBM bytes: every pipeline kernel's median bytes per launch times its
     # average launches per batch (dispatches / dispatches of the fold kernel)
     step = {}
-    marker = {"uniform": "k_fold_wide<true>", "zipf": "k_fold_wide<true>", "queue": "k_fold_q",
+    marker = {"uniform": "k_fold_wide<true>", "zipf": "k_fold_wide<true>", "queue": "k_fold_q<true>",
               "approx": "k_fold_a"}
     skip = ("k_gen_batch", "k_init_table", "k_init_approx", "k_count_queued", "k_gen_zipf")
     ours = our_kernels()
