@@ -1334,6 +1334,16 @@ constexpr uint32_t kRemNone = 0x3FFFFFFFu;
 __device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, uint32_t rem) {
     return (status << 30) | (evaluated ? (rem & kRemNone) : kRemNone);
 }
+// Queueing kind with TokenLimit <= 62: one byte, status in bits 6-7 and remaining in bits
+// 0-5 (63 = no script call), through the fold and the un-partition passes.
+constexpr uint32_t kRemNone8 = 63u;
+__device__ __forceinline__ void put_wait(uint32_t *res, uint32_t q, uint32_t status, bool evaluated, uint32_t rem,
+                                         uint32_t narrow) {
+    if (narrow)
+        reinterpret_cast<uint8_t *>(res)[q] = (uint8_t)((status << 6) | (evaluated ? (rem & 63u) : kRemNone8));
+    else
+        res[q] = pack_wait(status, evaluated, rem);
+}
 
 template <bool FINAL, bool WAIT, bool NARROW = false>
 __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
@@ -1365,7 +1375,11 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
         const int e = it * kUnBlock + tid;
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
-        if (FINAL && WAIT) {
+        if (FINAL && WAIT && NARROW) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 6));
+            const uint32_t rem = r[it] & 63u;
+            ST_U(remaining + i, (rem == kRemNone8) ? -1 : (int32_t)rem);
+        } else if (FINAL && WAIT) {
             ST_U(granted + i, (uint8_t)(r[it] >> 30));
             const uint32_t rem = r[it] & kRemNone;
             ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
@@ -1703,16 +1717,19 @@ __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t
     return (uint64_t)(head & 0xFFFFu) | ((uint64_t)(cnt & 0xFFFFu) << 16) | ((uint64_t)qsum << 32);
 }
 
+// k_fold_q's shape: 768 threads x 2 requests (79 VGPRs, 56.8 KB of LDS), two workgroups
+// (24 waves) per CU; against 512 x 4 (128 VGPRs, 16 waves) the config-D fold takes 1.91
+// instead of 2.04 ms (profiles/r02_ablate_q.log).
 #ifndef TBE_Q_BLOCK
-#define TBE_Q_BLOCK 512
+#define TBE_Q_BLOCK 768
 #endif
 #ifndef TBE_Q_ITEMS
-#define TBE_Q_ITEMS 4
+#define TBE_Q_ITEMS 2
 #endif
 #ifndef TBE_Q_WAVES
-#define TBE_Q_WAVES 4
+#define TBE_Q_WAVES 6
 #endif
-constexpr int kQBlock = TBE_Q_BLOCK;               // k_fold_q workgroup (two per CU: 56.5 KB of LDS)
+constexpr int kQBlock = TBE_Q_BLOCK;               // k_fold_q workgroup
 constexpr int kQItems = TBE_Q_ITEMS;
 constexpr int kQChunk = kQBlock * kQItems;         // 2048 requests per chunk
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
@@ -1730,7 +1747,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
     uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
-    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err) {
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow) {
     __shared__ Slot slot[1 << kMaxRBits];
     __shared__ uint64_t qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];
@@ -1883,7 +1900,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                         }
                     }
                 }
-                res[c + r * kQBlock + tid] = pack_wait(status, evaluated, rem);
+                put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
                 if (hmod) qh[kl[r]] = qh_pack(head, cnt, qsum);
                 if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
@@ -2382,7 +2399,8 @@ struct tbe_engine {
     uint32_t nbuckets = 0;   // ceil(n_keys / 2^r_bits)
     int passes = 0;          // 8-bit LSD passes over the bucket id
     bool packed = false;     // token bucket and queueing kinds: passes move packed u64 records (PackFmt)
-    bool narrow = false;     // token bucket, packed, TokenLimit <= 127: one-byte replies (put_reply)
+    bool narrow = false;     // one-byte replies: token bucket (packed, TokenLimit <= 127, put_reply),
+                             // queueing kind (TokenLimit <= 62, put_wait)
     PackFmt pf{};
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
@@ -2747,12 +2765,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
                 e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
-                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->narrow ? 1u : 0u);
         else
             k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
                 e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
-                e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+                e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
+                e->narrow ? 1u : 0u);
     } else if (e->packed) {
         // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
@@ -2790,7 +2809,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
-        if (e->narrow && !wait && !approx)
+        if (e->narrow && !approx)
             k_unscatter<false, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
                                                                       w.res[cur ^ 1], nullptr, nullptr);
         else
@@ -2801,6 +2820,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (e->narrow && !wait && !approx)
         k_unscatter<true, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                      nullptr, granted, remaining);
+    else if (wait && e->narrow)
+        k_unscatter<true, true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                    nullptr, granted, remaining);
     else if (wait)
         k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                               nullptr, granted, remaining);
@@ -2920,8 +2942,9 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
-        e->narrow = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127 &&
-                    (c.flags & TBE_FLAG_NO_NARROW) == 0;
+        e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
+                    ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
+                     (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
     }
 
     auto bail = [&](tbe_status st) {
