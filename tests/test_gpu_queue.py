@@ -104,3 +104,38 @@ def test_attempt_mixed_with_wait(engine_lib, gpu, order):
         log = ref.refresh(t)
         assert list(zip(keys_l.tolist(), ids_l.tolist(), rem_l.tolist())) == log
         t += 1_000
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("layout", ["wide", "packed_wide_reply", "token_limit_100", "escaped_ts"])
+def test_queue_layouts(engine_lib, gpu, order, layout):
+    """The queue path's record and reply layouts against the C restatement: wide pass
+    records (TBE_FLAG_NO_PACK), packed records with 4-byte replies (TBE_FLAG_NO_NARROW),
+    TokenLimit 100 (too large for one-byte wait replies), and packed records whose
+    timestamps leave the 32-bit window (escape records: the fold reads ts by index)."""
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    tl = 100 if layout == "token_limit_100" else 4
+    kw = {"wide": dict(pack=False, narrow=False), "packed_wide_reply": dict(narrow=False)}.get(layout, {})
+    n_keys, n = 5000, 60_000
+    eng = QueueingTokenBucketEngine(n_keys, tl, 1, 10_000_000, 16, order, device=0, **kw)
+    ref = cref.CQueueingTokenBucket(n_keys, tl, fill_rate(1, 10_000_000), 16, order)
+    lay = eng.layout()
+    assert lay["packed"] == (layout != "wide") and lay["narrow"] == (layout in ("escaped_ts",))
+    rng = np.random.default_rng(hash(layout) % 1000 + order)
+    t, rid = S_US, 0
+    for _ in range(4):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 2, 3, 5, tl + 1], n).astype(np.int32)
+        span = 3 * 3_600_000_000 if layout == "escaped_ts" else 1_000
+        ts = (t + np.sort(rng.integers(0, span, n))).astype(np.int64)
+        check_round(eng, ref, keys, permits, ts, rid)
+        rid += n
+        t = int(ts[-1]) + 1_000 + int(rng.integers(0, 3_000_000))
+        k1, i1, r1 = eng.refresh(t)
+        k2, i2, r2 = ref.refresh(t)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
