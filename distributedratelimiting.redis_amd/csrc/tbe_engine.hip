@@ -1710,7 +1710,7 @@ struct QParams {
     int32_t order;       // 0 OldestFirst, 1 NewestFirst
     uint32_t cap;        // ring entries per key (max(1, QueueLimit))
     int32_t wait;        // 1 = WaitAsyncCore (may queue), 0 = AcquireCore (lease or fail)
-    int32_t pad;
+    uint32_t ai_base;    // added to eviction causes (a chunk's offset in its host batch)
     int64_t id_base;     // request id of arrival index 0 of this batch
 };
 __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t qsum) {
@@ -1876,7 +1876,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                                     const uint64_t ent = kr[head];
                                     const uint32_t at = atomicAdd(ev_count, 1u);
                                     if (at < ev_cap) {
-                                        ev_cause[at] = ai[r];
+                                        ev_cause[at] = ai[r] + Q.ai_base;
                                         ev_id[at] = (int64_t)(ent >> 16);
                                     }
                                     qsum -= (int64_t)(ent & 0xFFFFu);
@@ -2003,6 +2003,8 @@ struct AParams {
     int64_t id_base;
     int32_t wait;           // 1: WaitAsyncCore (A:116-183), 0: AcquireCore (A:84-113)
     int32_t zero_slots;     // ring entries a key may give to zero-permit registrations
+    uint32_t ai_base;       // added to eviction causes (a chunk's offset in its host batch)
+    uint32_t pad;
     double decay_rate;      // FillRatePerSecond (A:224 decay_rate)
     double period_s;        // ReplenishmentPeriod.TotalSeconds (A:443)
 };
@@ -2159,7 +2161,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                                 const uint64_t ent = kr[head];
                                 const uint32_t at = atomicAdd(ev_count, 1u);
                                 if (at < ev_cap) {
-                                    ev_cause[at] = ai[r];
+                                    ev_cause[at] = ai[r] + A.ai_base;
                                     ev_id[at] = (int64_t)(ent >> 16);
                                 }
                                 a.qsum = (uint16_t)(a.qsum - (uint32_t)(ent & 0xFFFFu));
@@ -2624,7 +2626,7 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                      const int64_t *ts, uint64_t n, uint8_t *granted, int32_t *remaining,
                      hipStream_t caller, int64_t id_base = 0, hipEvent_t in_ready = nullptr,
-                     hipStream_t out_stream = nullptr) {
+                     hipStream_t out_stream = nullptr, uint32_t ai_base = 0) {
     const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
     const bool wait = e->cfg.kind != TBE_KIND_TOKEN_BUCKET;   // status-packed replies
     if (n == 0) return TBE_OK;
@@ -2648,6 +2650,8 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             HIP_TRY(e, hipStreamWaitEvent(sp, e->ev_in, 0));
         }
         if (w.used) HIP_TRY(e, hipStreamWaitEvent(sp, w.done, 0));
+    } else if (in_ready) {            // chunked host-buffer path (queueing / approximate)
+        HIP_TRY(e, hipStreamWaitEvent(sf, in_ready, 0));
     }
     HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
 
@@ -2753,6 +2757,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         AParams a = e->ap;
         a.id_base = id_base;
         a.wait = e->wait_mode;
+        a.ai_base = ai_base;
         k_fold_a<<<e->nbuckets, kFoldBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
             e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
@@ -2761,6 +2766,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         QParams q = e->qp;
         q.id_base = id_base;
         q.wait = e->wait_mode;
+        q.ai_base = ai_base;
         if (e->packed)
             k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
@@ -2841,6 +2847,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             HIP_TRY(e, hipStreamWaitEvent(outs, e->ev_out, 0));
         }
         e->ws_cur ^= 1;
+    } else if (out_stream && out_stream != sf) {
+        HIP_TRY(e, hipEventRecord(e->ev_out, sf));
+        HIP_TRY(e, hipStreamWaitEvent(out_stream, e->ev_out, 0));
     }
     e->last_err = w.err;
     ++e->nbatch;
@@ -3084,7 +3093,10 @@ static bool host_validate(const tbe_engine *e, const uint64_t *keys, const int32
         th.emplace_back([&, t] {
             const uint64_t a = n * t / nt, b = n * (t + 1) / nt;
             bool x = false;
-            for (uint64_t i = a; i < b; ++i) x |= (keys[i] >= nk) | (permits[i] < 0) | (ts[i] < 0);
+            if (ts)
+                for (uint64_t i = a; i < b; ++i) x |= (keys[i] >= nk) | (permits[i] < 0) | (ts[i] < 0);
+            else
+                for (uint64_t i = a; i < b; ++i) x |= (keys[i] >= nk) | (permits[i] < 0);
             bad[t] = x;
         });
     for (auto &x : th) x.join();
@@ -3378,6 +3390,51 @@ tbe_status tbe_approx_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys
     return status_batch_device(e, d_keys, d_permits, nullptr, n, id_base, d_status, d_available, stream);
 }
 
+// Host-buffer queue / approximate batch from page-locked buffers: chunks of kHostChunk
+// requests, copy-in on cin, decide on the engine stream, copy-out on cout, so copies
+// overlap the decisions (as acquire_chunked).  The batch is validated on the host before
+// anything is applied; chunk c's request ids and eviction causes are offset by c's
+// position, so the result is the unchunked call's.
+static tbe_status status_chunked(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
+                                 uint64_t n, int64_t id_base, uint8_t *status, int32_t *remaining,
+                                 uint32_t *nev) {
+    if (!e->cin) {
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
+        HIP_TRY(e, hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
+    }
+    const uint64_t nch = (n + kHostChunk - 1) / kHostChunk;
+    while (e->ev_chunk.size() < nch) {
+        hipEvent_t ev = nullptr;
+        HIP_TRY(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        e->ev_chunk.push_back(ev);
+    }
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
+        HIP_TRY(e, hipMemcpyAsync(e->d_keys + o, keys + o, m * sizeof(uint64_t), hipMemcpyHostToDevice, e->cin));
+        HIP_TRY(e, hipMemcpyAsync(e->d_permits + o, permits + o, m * sizeof(int32_t), hipMemcpyHostToDevice, e->cin));
+        if (ts) HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin));
+        HIP_TRY(e, hipEventRecord(e->ev_chunk[c], e->cin));
+    }
+    if (!host_validate(e, keys, permits, ts, n)) {
+        HIP_TRY(e, hipStreamSynchronize(e->cin));
+        return fail(e, TBE_EINVAL, "invalid request in batch (key >= n_keys, permits < 0 or ts < 0)");
+    }
+    HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), e->stream));
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
+        tbe_status rc = run_batch(e, e->d_keys + o, e->d_permits + o, ts ? e->d_ts + o : nullptr, m,
+                                  e->d_granted + o, e->d_remaining + o, nullptr, id_base + (int64_t)o,
+                                  e->ev_chunk[c], e->cout, (uint32_t)o);
+        if (rc != TBE_OK) return rc;
+        HIP_TRY(e, hipMemcpyAsync(status + o, e->d_granted + o, m, hipMemcpyDeviceToHost, e->cout));
+        HIP_TRY(e, hipMemcpyAsync(remaining + o, e->d_remaining + o, m * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  e->cout));
+    }
+    HIP_TRY(e, hipMemcpyAsync(nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost, e->cout));
+    HIP_TRY(e, hipStreamSynchronize(e->cout));
+    return TBE_OK;
+}
+
 static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits,
                                const int64_t *ts_us, uint64_t n, int64_t id_base, uint8_t *status,
                                int32_t *remaining, uint64_t *n_evicted) {
@@ -3406,20 +3463,26 @@ static tbe_status status_batch(tbe_engine *e, const uint64_t *keys, const int32_
         e->ev_cap = need_ev;
     }
     hipStream_t st = e->stream;
-    HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), st));
-    HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    if (ts_us)
-        HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    rc = run_batch(e, e->d_keys, e->d_permits, ts_us ? e->d_ts : nullptr, n, e->d_granted,
-                   e->d_remaining, st, id_base);
-    if (rc != TBE_OK) return rc;
     uint32_t flag = 0, nev = 0;
-    HIP_TRY(e, hipMemcpyAsync(&flag, e->last_err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipMemcpyAsync(&nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipMemcpyAsync(status, e->d_granted, n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipStreamSynchronize(st));
+    if (n >= 2 * kHostChunk && host_pinned(keys) && host_pinned(permits) && (!ts_us || host_pinned(ts_us)) &&
+        host_pinned(status) && host_pinned(remaining)) {
+        rc = status_chunked(e, keys, permits, ts_us, n, id_base, status, remaining, &nev);
+        if (rc != TBE_OK) return rc;
+    } else {
+        HIP_TRY(e, hipMemsetAsync(e->counters, 0, sizeof(uint32_t), st));
+        HIP_TRY(e, hipMemcpyAsync(e->d_keys, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(e, hipMemcpyAsync(e->d_permits, permits, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if (ts_us)
+            HIP_TRY(e, hipMemcpyAsync(e->d_ts, ts_us, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        rc = run_batch(e, e->d_keys, e->d_permits, ts_us ? e->d_ts : nullptr, n, e->d_granted,
+                       e->d_remaining, st, id_base);
+        if (rc != TBE_OK) return rc;
+        HIP_TRY(e, hipMemcpyAsync(&flag, e->last_err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(e, hipMemcpyAsync(&nev, e->counters, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(e, hipMemcpyAsync(status, e->d_granted, n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(e, hipMemcpyAsync(remaining, e->d_remaining, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(e, hipStreamSynchronize(st));
+    }
     if (flag) {
         HIP_TRY(e, hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), st));
         HIP_TRY(e, hipStreamSynchronize(st));

@@ -194,14 +194,16 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
                          queue_limit=queue_limit, queue_order=queue_order, **kw)
         self.queue_limit = queue_limit
 
-    def wait_batch(self, keys, permits, ts_us, id_base: int):
-        """Returns (status u8, remaining i32, evicted (cause index u64, request id i64))."""
+    def wait_batch(self, keys, permits, ts_us, id_base: int, status=None, remaining=None):
+        """Returns (status u8, remaining i32, evicted (cause index u64, request id i64)).
+        `status` / `remaining` may be caller arrays (e.g. PinnedArray: with page-locked
+        inputs too, batches of >= 2 chunks take the overlapped chunked path)."""
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         permits = np.ascontiguousarray(permits, dtype=np.int32)
         ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
         n = keys.shape[0]
-        status = np.empty(n, dtype=np.uint8)
-        remaining = np.empty(n, dtype=np.int32)
+        status = np.empty(n, dtype=np.uint8) if status is None else status
+        remaining = np.empty(n, dtype=np.int32) if remaining is None else remaining
         n_ev = ctypes.c_uint64()
         self._check(self._lib.tbe_wait_batch(self.handle, keys.ctypes.data, permits.ctypes.data,
                                              ts_us.ctypes.data, n, id_base, status.ctypes.data,
@@ -319,13 +321,13 @@ class ApproximateEngine(QueueingTokenBucketEngine):
                          queue_order, zero_wait_slots=zero_wait_slots, **kw)
         self.zero_wait_slots = zero_wait_slots
 
-    def acquire_batch(self, keys, permits, wait: bool = True, id_base: int = 0):
+    def acquire_batch(self, keys, permits, wait: bool = True, id_base: int = 0, status=None, available=None):
         """Returns (status u8, available i32, evicted (cause index, request id))."""
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         permits = np.ascontiguousarray(permits, dtype=np.int32)
         n = keys.shape[0]
-        status = np.empty(n, dtype=np.uint8)
-        avail = np.empty(n, dtype=np.int32)
+        status = np.empty(n, dtype=np.uint8) if status is None else status
+        avail = np.empty(n, dtype=np.int32) if available is None else available
         n_ev = ctypes.c_uint64()
         self._check(self._lib.tbe_approx_acquire_batch(self.handle, keys.ctypes.data, permits.ctypes.data,
                                                        n, 1 if wait else 0, id_base, status.ctypes.data,

@@ -65,3 +65,44 @@ def test_pinned_chunked_overlap(engine_lib, gpu):
     for a in bufs:
         a.free()
     ref.close()
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_pinned_chunked_queue_and_approx(engine_lib, gpu, order):
+    """Queue waits and approximate waits from page-locked buffers of >= 2 chunks take the
+    chunked path: statuses, remaining / available and the eviction list (causes are
+    offsets in the whole batch) equal the C restatement; an invalid request in the last
+    chunk rejects the whole batch with nothing applied."""
+    from distributedratelimiting.redis_amd import (ApproximateEngine, QueueingTokenBucketEngine, TbeError,
+                                                   fill_rate)
+    from distributedratelimiting.redis_amd.engine import PinnedArray
+    n_keys, n = 2_000_000, (1 << 23) + 4_321
+    bufs = [PinnedArray(n, d) for d in (np.uint64, np.int32, np.int64, np.uint8, np.int32)]
+    bk, bp, bt, bs, br = (b.array for b in bufs)
+    q = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, 4, order, device=0)
+    qref = cref.CQueueingTokenBucket(n_keys, 4, fill_rate(1, 10_000_000), 4, order)
+    a = ApproximateEngine(n_keys, 6, 1, 10_000_000, 4, order, device=0)
+    aref = cref.CApprox(n_keys, 6, 1, 10_000_000, 4, order)
+    for b in range(3):
+        k, p, t = cref.gen_batch(0x5EED000D, n_keys, b, n, 1_000, 1, 3)
+        bk[:], bp[:], bt[:] = k, p, t
+        st, rem, (cause, ids) = q.wait_batch(bk, bp, bt, b * n, bs, br)
+        st2, rem2, cause2, ids2 = qref.acquire_batch(k, p, t, b * n, threads=8)
+        assert np.array_equal(st, st2) and np.array_equal(rem, rem2), b
+        assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2), b
+        st, av, (cause, ids) = a.acquire_batch(bk, bp, wait=True, id_base=b * n, status=bs, available=br)
+        st2, av2, cause2, ids2 = aref.acquire_batch(k, p, True, b * n, threads=8)
+        assert np.array_equal(st, st2) and np.array_equal(av, av2), b
+        assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2), b
+    v, tt = q.export_state()
+    k, p, t = cref.gen_batch(0x5EED000D, n_keys, 3, n, 1_000, 1, 3)
+    bk[:], bp[:], bt[:] = k, p, t
+    bp[n - 3] = -1
+    with pytest.raises(TbeError):
+        q.wait_batch(bk, bp, bt, 3 * n, bs, br)
+    v2, t2 = q.export_state()
+    assert np.array_equal(t2, tt) and np.array_equal(v2.view(np.uint64), v.view(np.uint64))
+    for x in bufs:
+        x.free()
+    qref.close()
+    aref.close()
