@@ -272,7 +272,7 @@ def main():
     if stages and sum(stages.values()) > 0:
         passes = layout["passes"]
         launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                    "unscatter": 1 if passes == 2 else passes, "hot": 5}   # per step (k_unscatter2: both passes)
+                    "unscatter": passes, "hot": 5}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
         distinct = None
@@ -446,19 +446,15 @@ def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool
         # plus the table rows of the distinct keys in the batch (16 B read + 16 B written)
         u = distinct if distinct is not None else n_keys * (1.0 - np.exp(-n / n_keys))
         return int(n * (rec + reply) + u * 32)
-    side = packed and passes == 2          # pass 0 also writes a 2-byte bucket id per request
     if stage == "scatter":
         # pass 0 reads the caller's key 8 + permits 4 + ts 8, later passes one record;
         # every pass writes a record and its 4-byte permutation entry
-        return int(n * ((20 + (rec if packed else 16) * (passes - 1) + (2 if side else 0)) / passes + rec + 4))
+        return int(n * ((20 + (rec if packed else 16) * (passes - 1)) / passes + rec + 4))
     if stage == "hist":
-        # pass 0 reads the keys; pass 1 the 2-byte bucket ids (or the records)
-        return int(n * (8 + (2 if side else (8 if packed else 4)) * (passes - 1)) / passes)
+        return int(n * (8 + (8 if packed else 4) * (passes - 1)) / passes)
     if stage == "bounds":
         return n * (8 if packed else 4)
     if stage == "unscatter":
-        if passes == 2:   # k_unscatter2: perm0 4 + gathered perm1 4 + gathered reply + u8 + i32
-            return int(n * (13 + reply))
         # perm 4 + gathered reply + written reply (inner passes) or 5 (final: u8 + i32)
         return int(n * ((4 + 2 * reply) * (passes - 1) + 9 + reply) / passes)
     return n * 4
@@ -476,7 +472,7 @@ def pmc_traffic(stage: str, workload: str = "uniform"):
     if workload == "uniform":
         return d.get(stage, {}).get("hbm_bytes_per_launch")
     prefixes = {"fold": ("k_fold<", "k_fold_wide<"), "scatter": ("k_scatter_rec<",),
-                "hist": ("k_hist<",), "unscatter": ("k_unscatter<", "k_unscatter2<")}.get(stage, ())
+                "hist": ("k_hist<",), "unscatter": ("k_unscatter<",)}.get(stage, ())
     kern = d.get("workloads", {}).get(workload, {})
     v = [k["hbm_bytes_per_launch"] for name, k in kern.items()
          if name.startswith(prefixes) and "hbm_bytes_per_launch" in k]

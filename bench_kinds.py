@@ -180,7 +180,7 @@ def run_queue(args, lib, dev, world, rank, dist):
     passes = eng.layout()["passes"]
     stages["drain"] = drain_ms
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                "unscatter": 1 if passes == 2 else passes, "hot": 1, "drain": 1}
+                "unscatter": passes, "hot": 1, "drain": 1}
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
     u = _distinct(n, kl)
@@ -318,7 +318,7 @@ def run_approx(args, lib, dev, world, rank, dist):
     value = n * steps * world / elapsed
     passes = eng.layout()["passes"]
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                "unscatter": 1 if passes == 2 else passes, "hot": 1}
+                "unscatter": passes, "hot": 1}
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
     u = _distinct(n, kshared)

@@ -154,8 +154,6 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
 
 // ----------------------------------------------------------------------------- kernels
 // Per-tile digit histograms.  Block j walks tiles [j*tpb, (j+1)*tpb) in order and
-// (KeyT = uint16_t: the input is the previous pass's side array of bucket ids, 2 bytes
-// per request instead of an 8-byte record; then r_bits places the id in the key bits)
 // writes for each tile the exclusive running count per digit within its block
 // (tileprefix) and, at the end, the block's totals (blocksum).  Pass 0 also validates
 // keys (key < n_keys).  Digits come from the key bits under `kmask` (the low 32 bits, or
@@ -201,12 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
             hot_sortkeys<kHistItems>(kv, hs, nb, r_bits, skv);
         } else {
 #pragma unroll
-            for (int it = 0; it < kHistItems; ++it) {
-                if constexpr (sizeof(KeyT) == 2)
-                    skv[it] = (uint32_t)kv[it] << r_bits;   // a bucket id (k_scatter_rec's bucket side array)
-                else
-                    skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
-            }
+            for (int it = 0; it < kHistItems; ++it) skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
         }
 #pragma unroll
         for (int it = 0; it < kHistItems; ++it) {
@@ -552,7 +545,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
     uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
     uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
-    uint32_t *__restrict__ iout = nullptr, uint16_t *__restrict__ bout = nullptr) {
+    uint32_t *__restrict__ iout = nullptr) {
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
@@ -627,8 +620,6 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
             const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             rout[gpos[it]] = s;   // runs merge in L2: keep cached
-            // the next pass's histogram reads the bucket id (< 2^16 with two passes)
-            if (bout) bout[gpos[it]] = (uint16_t)((uint32_t)(s & F.kmask) >> r_bits);
         }
     }
     if (IDX) {
@@ -1402,59 +1393,6 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
             ST_U(reinterpret_cast<uint8_t *>(res_out) + i, (uint8_t)r[it]);
         } else {
             ST_U(res_out + i, r[it]);
-        }
-    }
-}
-
-// Both inverse passes of a two-pass partition in one launch: out[i] = res[perm1[perm0[i]]]
-// (perm0[i] is where pass 0 put request i, perm1 where pass 1 put that position), then
-// the final unpack.  Saves the intermediate reply array's write and read and a launch.
-template <bool WAIT, bool NARROW>
-__global__ __launch_bounds__(kUnBlock) void k_unscatter2(uint64_t n, const uint32_t *__restrict__ perm0,
-                                                         const uint32_t *__restrict__ perm1,
-                                                         const uint32_t *__restrict__ res_in,
-                                                         uint8_t *__restrict__ granted,
-                                                         int32_t *__restrict__ remaining) {
-    const int tid = threadIdx.x;
-    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kUnTile;
-    const int nvalid = (int)min<uint64_t>(kUnTile, n - base);
-    uint32_t pv[kUnItems], r[kUnItems];
-#pragma unroll
-    for (int it = 0; it < kUnItems; ++it) {
-        const int e = it * kUnBlock + tid;
-        pv[it] = (e < nvalid) ? LD_U(perm0 + base + e) : 0u;
-    }
-#pragma unroll
-    for (int it = 0; it < kUnItems; ++it) {
-        const int e = it * kUnBlock + tid;
-        pv[it] = (e < nvalid) ? perm1[pv[it]] : 0u;
-    }
-#pragma unroll
-    for (int it = 0; it < kUnItems; ++it) {
-        const int e = it * kUnBlock + tid;
-        r[it] = (e < nvalid) ? (NARROW ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[pv[it]] : res_in[pv[it]])
-                             : 0u;
-    }
-#pragma unroll
-    for (int it = 0; it < kUnItems; ++it) {
-        const int e = it * kUnBlock + tid;
-        if (e >= nvalid) continue;
-        const uint64_t i = base + e;
-        if (WAIT && NARROW) {
-            ST_U(granted + i, (uint8_t)(r[it] >> 6));
-            const uint32_t rem = r[it] & 63u;
-            ST_U(remaining + i, (rem == kRemNone8) ? -1 : (int32_t)rem);
-        } else if (WAIT) {
-            ST_U(granted + i, (uint8_t)(r[it] >> 30));
-            const uint32_t rem = r[it] & kRemNone;
-            ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
-        } else if (NARROW) {
-            ST_U(granted + i, (uint8_t)(r[it] >> 7));
-            ST_U(remaining + i, (int32_t)(r[it] & 0x7Fu));
-        } else {
-            ST_U(granted + i, (uint8_t)(r[it] >> 31));
-            ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
         }
     }
 }
@@ -2437,7 +2375,6 @@ struct Workspace {
     uint32_t *res[2] = {nullptr, nullptr};
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
-    uint16_t *bkt16 = nullptr;    // bucket id per request after pass 0 (two packed passes)
     uint32_t *err = nullptr;      // the batch's invalid-request flag
     uint32_t *segbase = nullptr;  // hot runs
     SegSummary *summ = nullptr;
@@ -2583,7 +2520,6 @@ void free_workspace(Workspace &w) {
     dfree(w.res[1]);
     dfree(w.bstart);
     dfree(w.bcount);
-    dfree(w.bkt16);
     dfree(w.err);
     w.cap_n = 0;
     w.used = false;
@@ -2603,16 +2539,6 @@ void tiles_for(uint64_t n, uint32_t &ntiles, uint32_t &nblk, uint32_t &tpb) {
     tpb = (ntiles + kMaxHistBlocks - 1) / kMaxHistBlocks;
     if (tpb == 0) tpb = 1;
     nblk = (ntiles + tpb - 1) / tpb;
-}
-
-// Two packed passes: pass 0 also writes each request's bucket id (u16) beside its record,
-// and pass 1's histogram reads those 2 bytes instead of the 8-byte records.
-inline bool bucket_side_array(const tbe_engine *e) {
-#ifdef TBE_NO_BKT16
-    return false;
-#else
-    return e->packed && e->passes == 2 && e->nb_total <= 65536u;
-#endif
 }
 
 tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
@@ -2647,7 +2573,6 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.res[1], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bcount, (uint64_t)e->nb_total * sizeof(uint32_t)));
-    if (bucket_side_array(e)) HIP_TRY(e, hipMalloc(&w.bkt16, cap * sizeof(uint16_t)));
     HIP_TRY(e, hipMalloc(&w.err, sizeof(uint32_t)));
     w.cap_n = cap;
     return TBE_OK;
@@ -2731,7 +2656,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
-    const bool b16 = bucket_side_array(e);
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
     HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
@@ -2753,10 +2677,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total);
-        else if (b16 && p == 1)
-            k_hist<uint16_t><<<nblk, kBlock, 0, sp>>>(w.bkt16, n, shift, tpb, ntiles, out.tileprefix,
-                                                       w.blocksum, e->cfg.n_keys, w.err, 0, kmask, nullptr,
-                                                       e->nbuckets, e->r_bits, bc, lowbits, e->nb_total);
         else if (e->packed)
             k_hist<uint64_t><<<nblk, kBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
                                                        out.tileprefix, w.blocksum, e->cfg.n_keys,
@@ -2772,12 +2692,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_colscan<<<kDigits, kBlock, 0, sp>>>(w.blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, sp);
         stage_begin(e, ST_SCATTER, sp);
-        uint16_t *bout = (b16 && p == 0) ? w.bkt16 : nullptr;
         if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, e->nbuckets, e->r_bits, nullptr, out.idx,
-                bout);
+                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
         else if (e->packed && wait)
             k_scatter_rec<false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -2786,13 +2704,11 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits, nullptr, nullptr,
-                bout);
+                out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits);
         else if (e->packed && p == 0)
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, e->nbuckets, e->r_bits, nullptr,
-                nullptr, bout);
+                out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -2897,23 +2813,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     }
     stage_begin(e, ST_UNSCATTER, sf);
     const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
-#ifndef TBE_NO_COMPOSE
-    if (e->passes == 2) {
-        if (wait && e->narrow)
-            k_unscatter2<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.pass[1].perm, w.res[0],
-                                                                   granted, remaining);
-        else if (wait)
-            k_unscatter2<true, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.pass[1].perm, w.res[0],
-                                                                    granted, remaining);
-        else if (e->narrow)
-            k_unscatter2<false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.pass[1].perm, w.res[0],
-                                                                    granted, remaining);
-        else
-            k_unscatter2<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.pass[1].perm, w.res[0],
-                                                                     granted, remaining);
-    } else
-#endif
-    {
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
         if (e->narrow && !approx)
@@ -2936,7 +2835,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     else
         k_unscatter<true, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                nullptr, granted, remaining);
-    }
     stage_end(e, ST_UNSCATTER, sf);
     k_sticky<<<1, 64, 0, sf>>>(w.err, e->sticky);
     HIP_TRY(e, hipGetLastError());

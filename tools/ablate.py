@@ -16,10 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "base": ([], []),
-    "no_bkt16": (["TBE_NO_BKT16"], []),
-    "no_compose": (["TBE_NO_COMPOSE"], []),
-    "neither": (["TBE_NO_BKT16", "TBE_NO_COMPOSE"], []),
+    "q_base": ([], ["--workload", "queue"]),
+    "q_nopack": ([], ["--workload", "queue", "--no-pack"]),
+    "q768": (["TBE_Q_BLOCK=768", "TBE_Q_ITEMS=2", "TBE_Q_WAVES=6"], ["--workload", "queue"]),
 }
 
 

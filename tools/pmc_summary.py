@@ -14,7 +14,6 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE = {"k_hist": "hist", "k_colscan": "colscan", "k_scatter": "scatter", "k_scatter_rec": "scatter",
          "k_bounds": "bounds", "k_fold": "fold", "k_fold_wide": "fold", "k_unscatter": "unscatter",
-         "k_unscatter2": "unscatter",
          "k_drain": "drain", "k_hot_plan": "hot", "k_hot_summary": "hot", "k_hot_chain": "hot",
          "k_hot_replies": "hot", "k_hot_update": "hot"}
 
