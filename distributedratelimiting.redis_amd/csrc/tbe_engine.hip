@@ -88,7 +88,11 @@ constexpr int kUnBlock = 1024;
 constexpr int kUnItems = 8;
 constexpr int kUnTile = kUnBlock * kUnItems;
 constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
-constexpr int kMaxHistBlocks = 1024;
+#ifndef TBE_HIST_BLOCKS
+#define TBE_HIST_BLOCKS 1024
+#endif
+constexpr int kMaxHistBlocks = TBE_HIST_BLOCKS;   // k_hist workgroups (each walks consecutive tiles)
+static_assert(kMaxHistBlocks % 256 == 0, "k_colscan reads kMaxHistBlocks / 256 blocks per thread");
 constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
 constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_colscan(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ digit_total) {
     __shared__ uint32_t wsum[kWaves];
     const int d = blockIdx.x, tid = threadIdx.x;
-    constexpr int PER = kMaxHistBlocks / kBlock;   // 4 blocks per thread
+    constexpr int PER = kMaxHistBlocks / kBlock;   // blocks per thread
     uint32_t c[PER], s = 0;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {

@@ -16,9 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
+    "base": ([], []),
+    "hist2048": (["TBE_HIST_BLOCKS=2048"], []),
+    "hist4096": (["TBE_HIST_BLOCKS=4096"], []),
     "q_base": ([], ["--workload", "queue"]),
-    "q_nopack": ([], ["--workload", "queue", "--no-pack"]),
-    "q768": (["TBE_Q_BLOCK=768", "TBE_Q_ITEMS=2", "TBE_Q_WAVES=6"], ["--workload", "queue"]),
+    "q_hist4096": (["TBE_HIST_BLOCKS=4096"], ["--workload", "queue"]),
 }
 
 
