@@ -423,68 +423,6 @@ __global__ __launch_bounds__(kSdBlock) void k_sd_lookup(SdBatch B, uint64_t n, S
     }
 }
 
-// Warm path: every request first looks its string up (the lookup rounds, text compared
-// with the arena).  A known string's slot is final; the others -- new strings, and those
-// whose tag leads to a slot claimed but never assigned -- are listed for the claim rounds.
-__global__ __launch_bounds__(kSdBlock) void k_sd_find(SdBatch B, uint64_t n, SdParams P,
-                                                      const uint64_t *__restrict__ stag,
-                                                      const uint32_t *__restrict__ sid,
-                                                      const uint64_t *__restrict__ sloc, uint64_t smask, SdArena A,
-                                                      uint32_t *__restrict__ slot_of, uint32_t *__restrict__ next,
-                                                      uint32_t *__restrict__ next_n,
-                                                      unsigned long long *__restrict__ err) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x; t0 < n; t0 += stride) {
-        const uint64_t i = t0 + threadIdx.x;
-        bool defer = false;
-        if (i < n) {
-            uint64_t off;
-            uint32_t len;
-            uint32_t found = kNoId;
-            if (!sd_span(B.offs, i, B.n_bytes, off, len)) {
-                atomicOr(err, kErrBatch);
-            } else {
-                bool done = false;
-                for (uint32_t round = 0; round < (uint32_t)kRounds && !done; ++round) {
-                    const uint64_t tag = sd_tag(round, sd_hash(B.bytes, B.safe, off, len, P.seed[round]), P.hmask);
-                    uint64_t h = mix64(tag) & smask;
-                    for (uint64_t probe = 0; probe <= smask; ++probe) {
-                        const uint64_t cur = stag[h];
-                        if (cur == kEmptyTag) {
-                            done = true;
-                            defer = true;
-                            break;
-                        }
-                        if (cur == tag) {
-                            const uint64_t loc = sloc[h];
-                            if (sid[h] == kNoId) {
-                                done = true;
-                                defer = true;
-                            } else if (loc_len(loc) == len &&
-                                       sd_equal(A.bytes, A.safe, loc_off(loc), B.bytes, B.safe, off, len)) {
-                                found = (uint32_t)h;
-                                done = true;
-                            }
-                            break;
-                        }
-                        h = (h + 1) & smask;
-                    }
-                }
-                if (!done) defer = true;
-            }
-            slot_of[i] = found;
-        }
-        const uint64_t m = __ballot(defer);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t base = 0;
-            if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(next_n, (uint32_t)__popcll(m));
-            base = __shfl(base, leader, 64);
-            if (defer) next[base + __popcll(m & lanemask_lt())] = (uint32_t)i;
-        }
-    }
-}
-
 __global__ void k_sd_init(uint64_t *__restrict__ stag, uint32_t *__restrict__ sid, uint32_t *__restrict__ sfirst,
                           uint64_t nslots) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -531,7 +469,7 @@ struct tbe_string_directory {
     uint64_t tmp_cap = 0;
     uint32_t *slot_of = nullptr;
     uint32_t *list[2] = {nullptr, nullptr};
-    uint32_t *list_n = nullptr;            // [kRounds + 1]
+    uint32_t *list_n = nullptr;            // [kRounds]
     uint32_t *bsum = nullptr, *bbytes = nullptr;
     uint64_t *bbase = nullptr;
     // host-buffer staging
@@ -612,7 +550,7 @@ tbe_status tbe_sdir_create(uint64_t capacity, uint64_t arena_bytes, const char *
               hipMalloc(&d->iloc, capacity * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&d->arena, d->arena_alloc) == hipSuccess &&
               hipMalloc(&d->state, 8 * sizeof(unsigned long long)) == hipSuccess &&
-              hipMalloc(&d->list_n, (kRounds + 1) * sizeof(uint32_t)) == hipSuccess;
+              hipMalloc(&d->list_n, kRounds * sizeof(uint32_t)) == hipSuccess;
     if (!ok) {
         tbe_sdir_destroy(d);
         return TBE_ENOMEM;
@@ -654,32 +592,19 @@ tbe_status tbe_sdir_assign_device(tbe_string_directory *d, const uint8_t *d_byte
     if (hipSetDevice(d->device) != hipSuccess) return TBE_EDEVICE;
     tbe_status rc = sd_scratch(d, n);
     if (rc != TBE_OK) return rc;
+    d->used = true;
     hipStream_t st = (hipStream_t)stream;
     const SdBatch B{d_bytes, d_offs, n_bytes, n_bytes & ~7ull};
     const SdArena A{d->arena, d->arena_alloc & ~7ull};
     unsigned long long *err = d->state + 1;
-    if (hipMemsetAsync(d->list_n, 0, (kRounds + 1) * sizeof(uint32_t), st) != hipSuccess) return TBE_EDEVICE;
+    if (hipMemsetAsync(d->list_n, 0, kRounds * sizeof(uint32_t), st) != hipSuccess) return TBE_EDEVICE;
     const uint64_t smask = d->nslots - 1;
-    // After the first batch, known strings are resolved by one lookup pass and only the
-    // rest enter the claim rounds (lists alternate: find -> list[0] -> list[1] -> ...).
-    const bool warm = d->used;
-    d->used = true;
-    if (warm)
-        k_sd_find<<<sd_grid(n, kSdBlock), kSdBlock, 0, st>>>(B, n, d->P, d->stag, d->sid, d->sloc, smask, A,
-                                                             d->slot_of, d->list[0], d->list_n + kRounds, err);
     for (int round = 0; round < kRounds; ++round) {
-        const uint32_t *in, *in_n;
-        if (warm) {
-            in = d->list[round & 1];
-            in_n = round ? d->list_n + (round - 1) : d->list_n + kRounds;
-        } else {
-            in = round ? d->list[(round - 1) & 1] : nullptr;
-            in_n = round ? d->list_n + (round - 1) : nullptr;
-        }
-        const int nxi = warm ? ((round + 1) & 1) : (round & 1);
-        uint32_t *nx = (round + 1 < kRounds) ? d->list[nxi] : nullptr;
+        const uint32_t *in = round ? d->list[(round - 1) & 1] : nullptr;
+        const uint32_t *in_n = round ? d->list_n + (round - 1) : nullptr;
+        uint32_t *nx = (round + 1 < kRounds) ? d->list[round & 1] : nullptr;
         uint32_t *nx_n = (round + 1 < kRounds) ? d->list_n + round : nullptr;
-        const unsigned g = (round || warm) ? kListGrid * 4 : sd_grid(n, kSdBlock);
+        const unsigned g = round ? kListGrid : sd_grid(n, kSdBlock);
         k_sd_claim<<<g, kSdBlock, 0, st>>>(B, n, in, in_n, (uint32_t)round, d->P, d->stag, d->sid, d->sfirst, smask,
                                            d->slot_of, err);
         k_sd_verify<<<g, kSdBlock, 0, st>>>(B, n, in, in_n, A, d->sid, d->sfirst, d->sloc, d->slot_of, nx, nx_n, err);
