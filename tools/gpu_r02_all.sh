@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-2 measurement of every workload: bench line (N=1), rocprofv3 kernel stats
-# (--no-pipeline, so kernel durations match the serial replay the roofline uses) and the
+# (--no-pipeline and the bench's own step counts, so kernel durations match the serial
+# replay the roofline uses) and the
 # HBM PMC passes (tools/pmc_all.sh).  Each GPU step has its own time limit; a failure
 # ends the script.
 set -u
@@ -16,7 +17,7 @@ done
 cd /tmp && export TMPDIR=/tmp
 for W in ${WORKLOADS:-uniform zipf queue approx}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/r02_prof_$W" -o run -- \
-        python3 "$ROOT/bench.py" --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-stage-timing --no-pipeline \
+        python3 "$ROOT/bench.py" --workload $W --steps 10 --warmup 3 --cpu-seconds 0 --no-stage-timing --no-pipeline \
         --no-host-buffer --no-strdir > "$OUT/r02_rocprof_$W.log" 2>&1
     rc=$?; echo "[rocprof $W] rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
