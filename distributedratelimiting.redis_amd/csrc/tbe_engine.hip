@@ -2458,6 +2458,8 @@ struct tbe_engine {
     uint32_t *last_err = nullptr;    // the error flag of the last enqueued batch
     // host-buffer path staging
     hipStream_t cin = nullptr, cout = nullptr;   // chunked pinned path: copy-in / copy-out streams
+    hipStream_t cin2 = nullptr;                  // second copy-in stream (TBE_CIN_STREAMS == 2)
+    std::vector<hipEvent_t> ev_chunk2;
     std::vector<hipEvent_t> ev_chunk;            // per-chunk copy-in done
     uint64_t stage_cap = 0;
     uint64_t *d_keys = nullptr;
@@ -3030,7 +3032,7 @@ void tbe_destroy(tbe_engine *e) {
     if (!e) return;
     if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    for (hipStream_t s2 : {e->cin, e->cout})
+    for (hipStream_t s2 : {e->cin, e->cout, e->cin2})
         if (s2) (void)hipStreamSynchronize(s2);
     free_workspace(e->ws[0]);
     free_workspace(e->ws[1]);
@@ -3060,7 +3062,9 @@ void tbe_destroy(tbe_engine *e) {
     if (e->pstream) (void)hipStreamDestroy(e->pstream);
     for (hipEvent_t ev : e->ev_chunk)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipStream_t s2 : {e->cin, e->cout})
+    for (hipEvent_t ev : e->ev_chunk2)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t s2 : {e->cin, e->cout, e->cin2})
         if (s2) (void)hipStreamDestroy(s2);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -3109,24 +3113,52 @@ static bool host_validate(const tbe_engine *e, const uint64_t *keys, const int32
     return true;
 }
 
-static tbe_status acquire_chunked(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
-                                  uint64_t n, uint8_t *granted, int32_t *remaining) {
+// Copy a page-locked batch in, chunk by chunk, in chunk order; ev_chunk[c] fires when
+// chunk c is on the device.  With TBE_CIN_STREAMS == 2 the timestamps travel on a second
+// copy stream (another DMA queue) beside the keys and permits.
+#ifndef TBE_CIN_STREAMS
+#define TBE_CIN_STREAMS 1
+#endif
+static tbe_status copy_in_chunks(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
+                                 uint64_t n, uint64_t nch) {
     if (!e->cin) {
         HIP_TRY(e, hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
         HIP_TRY(e, hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
     }
-    const uint64_t nch = (n + kHostChunk - 1) / kHostChunk;
+    const bool two = TBE_CIN_STREAMS == 2 && ts;
+    if (two && !e->cin2) HIP_TRY(e, hipStreamCreateWithFlags(&e->cin2, hipStreamNonBlocking));
     while (e->ev_chunk.size() < nch) {
         hipEvent_t ev = nullptr;
         HIP_TRY(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         e->ev_chunk.push_back(ev);
     }
-    for (uint64_t c = 0; c < nch; ++c) {   // all copies in, in chunk order
+    while (two && e->ev_chunk2.size() < nch) {
+        hipEvent_t ev = nullptr;
+        HIP_TRY(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        e->ev_chunk2.push_back(ev);
+    }
+    for (uint64_t c = 0; c < nch; ++c) {
         const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
+        if (two) {
+            HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin2));
+            HIP_TRY(e, hipEventRecord(e->ev_chunk2[c], e->cin2));
+        }
         HIP_TRY(e, hipMemcpyAsync(e->d_keys + o, keys + o, m * sizeof(uint64_t), hipMemcpyHostToDevice, e->cin));
         HIP_TRY(e, hipMemcpyAsync(e->d_permits + o, permits + o, m * sizeof(int32_t), hipMemcpyHostToDevice, e->cin));
-        HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin));
+        if (ts && !two)
+            HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin));
+        if (two) HIP_TRY(e, hipStreamWaitEvent(e->cin, e->ev_chunk2[c], 0));
         HIP_TRY(e, hipEventRecord(e->ev_chunk[c], e->cin));
+    }
+    return TBE_OK;
+}
+
+static tbe_status acquire_chunked(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
+                                  uint64_t n, uint8_t *granted, int32_t *remaining) {
+    const uint64_t nch = (n + kHostChunk - 1) / kHostChunk;
+    {
+        tbe_status rc = copy_in_chunks(e, keys, permits, ts, n, nch);
+        if (rc != TBE_OK) return rc;
     }
     if (!host_validate(e, keys, permits, ts, n)) {   // overlaps the first copies
         HIP_TRY(e, hipStreamSynchronize(e->cin));
@@ -3402,22 +3434,10 @@ tbe_status tbe_approx_acquire_batch_device(tbe_engine *e, const uint64_t *d_keys
 static tbe_status status_chunked(tbe_engine *e, const uint64_t *keys, const int32_t *permits, const int64_t *ts,
                                  uint64_t n, int64_t id_base, uint8_t *status, int32_t *remaining,
                                  uint32_t *nev) {
-    if (!e->cin) {
-        HIP_TRY(e, hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
-        HIP_TRY(e, hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
-    }
     const uint64_t nch = (n + kHostChunk - 1) / kHostChunk;
-    while (e->ev_chunk.size() < nch) {
-        hipEvent_t ev = nullptr;
-        HIP_TRY(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        e->ev_chunk.push_back(ev);
-    }
-    for (uint64_t c = 0; c < nch; ++c) {
-        const uint64_t o = c * kHostChunk, m = std::min(kHostChunk, n - o);
-        HIP_TRY(e, hipMemcpyAsync(e->d_keys + o, keys + o, m * sizeof(uint64_t), hipMemcpyHostToDevice, e->cin));
-        HIP_TRY(e, hipMemcpyAsync(e->d_permits + o, permits + o, m * sizeof(int32_t), hipMemcpyHostToDevice, e->cin));
-        if (ts) HIP_TRY(e, hipMemcpyAsync(e->d_ts + o, ts + o, m * sizeof(int64_t), hipMemcpyHostToDevice, e->cin));
-        HIP_TRY(e, hipEventRecord(e->ev_chunk[c], e->cin));
+    {
+        tbe_status rc = copy_in_chunks(e, keys, permits, ts, n, nch);
+        if (rc != TBE_OK) return rc;
     }
     if (!host_validate(e, keys, permits, ts, n)) {
         HIP_TRY(e, hipStreamSynchronize(e->cin));

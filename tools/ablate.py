@@ -15,12 +15,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
-    # name: (build defines, extra bench args)
-    "base": ([], []),
-    "hist2048": (["TBE_HIST_BLOCKS=2048"], []),
-    "hist4096": (["TBE_HIST_BLOCKS=4096"], []),
-    "q_base": ([], ["--workload", "queue"]),
-    "q_hist4096": (["TBE_HIST_BLOCKS=4096"], ["--workload", "queue"]),
+    # name: (build defines, extra bench args): host-buffer rates of config B
+    "base": ([], ["--no-strdir"]),
+    "cin2": (["TBE_CIN_STREAMS=2"], ["--no-strdir"]),
 }
 
 
@@ -43,7 +40,7 @@ def run(rounds: int, steps: int):
         for name, (_, extra) in VARIANTS.items():
             defs = VARIANTS[name][0]
             env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so"))
-            args = ["--steps", str(steps), "--cpu-seconds", "0", "--no-host-buffer", "--no-strdir"]
+            args = ["--steps", str(steps), "--cpu-seconds", "0"] + ([] if "--no-strdir" in extra else ["--no-host-buffer", "--no-strdir"])
             if "--warmup" not in extra:
                 args += ["--warmup", "2"]
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + extra, env=env,
@@ -55,7 +52,8 @@ def run(rounds: int, steps: int):
             d = json.loads(line[0])
             results.setdefault(name, []).append(d["stage_ms_per_step"])
             print(r, name, d["ms_per_step"], d["stage_ms_per_step"],
-                  (d.get("roofline") or {}).get("avg_launch_ms"), flush=True)
+                  (d.get("roofline") or {}).get("avg_launch_ms"), d.get("host_buffer_decisions_per_s"),
+                  d.get("host_buffer_pinned_decisions_per_s"), flush=True)
     print(json.dumps(results))
 
 
