@@ -1736,6 +1736,71 @@ __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t
 constexpr int kQBlock = TBE_Q_BLOCK;               // k_fold_q workgroup
 constexpr int kQItems = TBE_Q_ITEMS;
 constexpr int kQChunk = kQBlock * kQItems;         // 2048 requests per chunk
+// One request of one key (WaitAsyncCore Q:67-134 / TryLeaseUnsynchronized Q:136-165)
+// against the key's row `st` and queue header `hdr`; `kr` is the key's ring.  Sets the
+// reply fields and ORs smod / hmod when the row / header changed.
+__device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool &hmod, int32_t p, int64_t ts,
+                                       uint32_t ai, uint64_t *__restrict__ kr, const TbParams &P, const QParams &Q,
+                                       uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
+                                       uint32_t *__restrict__ ev_count, uint32_t ev_cap, uint32_t &status,
+                                       uint32_t &rem, bool &evaluated) {
+    uint32_t head = (uint32_t)(hdr & 0xFFFFu), cnt = (uint32_t)((hdr >> 16) & 0xFFFFu);
+    int64_t qsum = (int64_t)(hdr >> 32);
+    rem = 0;
+    evaluated = false;
+    if (p > Q.token_limit) {                                   // Q:70-73
+        status = TBE_WAIT_REJECTED;
+        return;
+    }
+    bool granted = false;
+    if (p == 0 || !(cnt > 0 && Q.order == 0)) {                // Q:153
+        bool m;
+        const uint32_t reply = tb_acquire(st, p, ts, P, m);
+        smod |= m;
+        evaluated = true;
+        granted = (reply >> 31) != 0;
+        rem = reply & 0x7FFFFFFFu;
+    }
+    if (granted) {
+        status = TBE_WAIT_GRANTED;
+        return;
+    }
+    if (!Q.wait) {
+        status = TBE_WAIT_FAILED;                              // TryLease only
+        return;
+    }
+    if ((int64_t)Q.queue_limit - qsum < p) {                   // Q:92
+        if (!(Q.order == 1 && p <= Q.queue_limit)) {
+            status = TBE_WAIT_FAILED;                          // Q:113
+            return;
+        }
+        while ((int64_t)Q.queue_limit - qsum < p) {            // Q:94-109
+            const uint64_t ent = kr[head];
+            const uint32_t at = atomicAdd(ev_count, 1u);
+            if (at < ev_cap) {
+                ev_cause[at] = ai + Q.ai_base;
+                ev_id[at] = (int64_t)(ent >> 16);
+            }
+            qsum -= (int64_t)(ent & 0xFFFFu);
+            head = (head + 1 == Q.cap) ? 0 : head + 1;
+            --cnt;
+        }
+    }
+    uint32_t tail = head + cnt;                                // Q:117-132
+    if (tail >= Q.cap) tail -= Q.cap;
+    kr[tail] = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
+    ++cnt;
+    qsum += p;
+    hdr = qh_pack(head, cnt, qsum);
+    hmod = true;
+    status = TBE_WAIT_QUEUED;
+}
+
+#ifndef TBE_Q_WALK
+#define TBE_Q_WALK 1
+#endif
+constexpr uint32_t kWalkMax = 32;   // longest per-key run a walking thread sorts
+
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
 // the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
 // LDS and its ring in HBM.  A ring entry written in one round and read (evicted) in a
@@ -1754,9 +1819,14 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow) {
     __shared__ Slot slot[1 << kMaxRBits];
     __shared__ uint64_t qh[1 << kMaxRBits];
-    __shared__ uint32_t own[1 << kMaxRBits];
+    __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
     __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
     __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
+#if TBE_Q_WALK
+    __shared__ uint16_t wsorted[kQChunk];         // the chunk's request indices by row
+    __shared__ uint32_t wsum_q[kQBlock / 64];
+    __shared__ uint32_t wtotal, wmax;
+#endif
 
     if (*err) return;
     const int tid = threadIdx.x;
@@ -1837,7 +1907,89 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             for (int r = 0; r < kQItems; ++r)
                 if (mine & (1u << r)) { slot[kl[r]] = tmp[r]; qh[kl[r]] = th[r]; }
         }
+        __syncthreads();   // claimed rows and headers visible
+#if TBE_Q_WALK
+        // Walk: sort the chunk's requests by row (LDS counting sort; within a row the
+        // arrival order is restored by the walking thread), then one thread per row
+        // decides its requests in arrival order -- no election rounds.  A chunk whose
+        // busiest key has more than kWalkMax requests takes the rounds below.
+        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
+        if (tid == 0) wmax = 0;
         __syncthreads();
+        uint32_t off[kQItems];
+#pragma unroll
+        for (int r = 0; r < kQItems; ++r) off[r] = (pend & (1u << r)) ? atomicAdd(&own[kl[r]], 1u) : 0u;
+        __syncthreads();
+        {
+            constexpr uint32_t RPT = (kMaxRows + kQBlock - 1) / kQBlock;
+            uint32_t cn[RPT], sum = 0, mx = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < RPT; ++u) {
+                const uint32_t j = tid * RPT + u;
+                cn[u] = j < R ? own[j] : 0u;
+                sum += cn[u];
+                mx = cn[u] > mx ? cn[u] : mx;
+            }
+            uint32_t tot;
+            uint32_t at = block_excl_scan<kQBlock>(sum, wsum_q, &tot);
+#pragma unroll
+            for (uint32_t u = 0; u < RPT; ++u) {
+                const uint32_t j = tid * RPT + u;
+                if (j < R) own[j] = at;
+                at += cn[u];
+            }
+            if (mx) atomicMax(&wmax, mx);
+            if (tid == 0) wtotal = tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kQItems; ++r)
+            if (pend & (1u << r)) wsorted[own[kl[r]] + off[r]] = (uint16_t)(r * kQBlock + tid);
+        __syncthreads();
+        if (wmax <= kWalkMax) {
+            for (uint32_t j = tid; j < R; j += kQBlock) {
+                const uint32_t a = own[j], z = (j + 1 < R) ? own[j + 1] : wtotal;
+                if (a == z) continue;
+                for (uint32_t x = a + 1; x < z; ++x) {           // arrival order (insertion sort)
+                    const uint16_t v = wsorted[x];
+                    uint32_t y = x;
+                    while (y > a && wsorted[y - 1] > v) {
+                        wsorted[y] = wsorted[y - 1];
+                        --y;
+                    }
+                    wsorted[y] = v;
+                }
+                Slot st = slot[j];
+                uint64_t h = qh[j];
+                bool smod = false, hmod = false;
+                uint64_t *__restrict__ kr = ring + (row0 + j) * (uint64_t)Q.cap;
+                for (uint32_t x = a; x < z; ++x) {
+                    const uint32_t q = c + wsorted[x];
+                    int32_t p;
+                    int64_t t;
+                    if (PACKED) {
+                        uint32_t k;
+                        unpack_rec(srec[q], ts_orig, tbase, F, k, p, t);
+                    } else {
+                        p = sperm[q];
+                        t = sts[q];
+                    }
+                    uint32_t status, rem;
+                    bool evaluated;
+                    q_step(st, h, smod, hmod, p, t, sidx[q], kr, P, Q, ev_cause, ev_id, ev_count, ev_cap, status, rem,
+                           evaluated);
+                    put_wait(res, q, status, evaluated, rem, narrow);
+                }
+                if (smod) slot[j] = st;
+                if (hmod) qh[j] = h;
+                if (smod || hmod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+            }
+            __syncthreads();   // the chunk's rows are settled before the next chunk reads them
+            continue;
+        }
+        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = kNoOwner;
+        __syncthreads();
+#endif
         for (;;) {
 #pragma unroll
             for (int r = 0; r < kQItems; ++r)
@@ -1849,64 +2001,14 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 if (!((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kQBlock + tid))) continue;
                 won |= 1u << r;
                 Slot st = slot[kl[r]];
-                const uint64_t h0 = qh[kl[r]];
-                uint32_t head = (uint32_t)(h0 & 0xFFFFu), cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
-                int64_t qsum = (int64_t)(h0 >> 32);
-                const int32_t p = pm[r];
-                uint32_t status, rem = 0;
-                bool evaluated = false, smod = false, hmod = false;
-                if (p > Q.token_limit) {                                   // Q:70-73
-                    status = TBE_WAIT_REJECTED;
-                } else {
-                    bool granted = false;
-                    if (p == 0 || !(cnt > 0 && Q.order == 0)) {            // Q:153
-                        bool m;
-                        const uint32_t reply = tb_acquire(st, p, ts[r], P, m);
-                        smod = m;
-                        evaluated = true;
-                        granted = (reply >> 31) != 0;
-                        rem = reply & 0x7FFFFFFFu;
-                    }
-                    if (granted) {
-                        status = TBE_WAIT_GRANTED;
-                    } else if (!Q.wait) {
-                        status = TBE_WAIT_FAILED;                          // TryLease only
-                    } else {
-                        uint64_t *__restrict__ kr = ring + (row0 + kl[r]) * (uint64_t)Q.cap;
-                        bool fail = false;
-                        if ((int64_t)Q.queue_limit - qsum < p) {           // Q:92
-                            if (Q.order == 1 && p <= Q.queue_limit) {      // Q:94-109
-                                while ((int64_t)Q.queue_limit - qsum < p) {
-                                    const uint64_t ent = kr[head];
-                                    const uint32_t at = atomicAdd(ev_count, 1u);
-                                    if (at < ev_cap) {
-                                        ev_cause[at] = ai[r] + Q.ai_base;
-                                        ev_id[at] = (int64_t)(ent >> 16);
-                                    }
-                                    qsum -= (int64_t)(ent & 0xFFFFu);
-                                    head = (head + 1 == Q.cap) ? 0 : head + 1;
-                                    --cnt;
-                                }
-                            } else {
-                                fail = true;                               // Q:113
-                            }
-                        }
-                        if (fail) {
-                            status = TBE_WAIT_FAILED;
-                        } else {                                           // Q:117-132
-                            uint32_t tail = head + cnt;
-                            if (tail >= Q.cap) tail -= Q.cap;
-                            kr[tail] = ((uint64_t)(Q.id_base + ai[r]) << 16) | (uint32_t)p;
-                            ++cnt;
-                            qsum += p;
-                            hmod = true;
-                            status = TBE_WAIT_QUEUED;
-                        }
-                    }
-                }
+                uint64_t h = qh[kl[r]];
+                bool smod = false, hmod = false, evaluated;
+                uint32_t status, rem;
+                q_step(st, h, smod, hmod, pm[r], ts[r], ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
+                       ev_cause, ev_id, ev_count, ev_cap, status, rem, evaluated);
                 put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
-                if (hmod) qh[kl[r]] = qh_pack(head, cnt, qsum);
+                if (hmod) qh[kl[r]] = h;
                 if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
             __syncthreads();

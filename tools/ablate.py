@@ -15,9 +15,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
-    # name: (build defines, extra bench args): host-buffer rates of config B
-    "base": ([], ["--no-strdir"]),
-    "cin2": (["TBE_CIN_STREAMS=2"], ["--no-strdir"]),
+    # name: (build defines, extra bench args)
+    "q_walk": ([], ["--workload", "queue"]),
+    "q_rounds": (["TBE_Q_WALK=0"], ["--workload", "queue"]),
 }
 
 
