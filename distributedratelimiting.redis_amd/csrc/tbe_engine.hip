@@ -1799,7 +1799,9 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
 #ifndef TBE_Q_WALK
 #define TBE_Q_WALK 1
 #endif
+#if TBE_Q_WALK
 constexpr uint32_t kWalkMax = 32;   // longest per-key run a walking thread sorts
+#endif
 
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
 // the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
