@@ -1796,8 +1796,11 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     status = TBE_WAIT_QUEUED;
 }
 
+// TBE_Q_WALK=1: decide each row's requests in one thread after an LDS counting sort
+// instead of election rounds.  Parity-equal, but the config-D fold takes 3.11 ms against
+// 2.41 for the rounds (profiles/r02_ablate_qwalk.log): off by default.
 #ifndef TBE_Q_WALK
-#define TBE_Q_WALK 1
+#define TBE_Q_WALK 0
 #endif
 #if TBE_Q_WALK
 constexpr uint32_t kWalkMax = 32;   // longest per-key run a walking thread sorts
