@@ -94,7 +94,6 @@ constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 
 constexpr int kMaxHistBlocks = TBE_HIST_BLOCKS;   // k_hist workgroups (each walks consecutive tiles)
 static_assert(kMaxHistBlocks % 256 == 0, "k_colscan reads kMaxHistBlocks / 256 blocks per thread");
 constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucket (32 KB LDS)
-constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
 // Hot keys (see the "hot keys" section below for how their runs are decided).
 constexpr uint32_t kHotKeysMax = 1024;
@@ -1859,7 +1858,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             qh[j] = h;
         }
     }
-    for (uint32_t j = tid; j < R; j += kQBlock) own[j] = kNoOwner;
     for (uint32_t j = tid; j < (R + 31) / 32; j += kQBlock) {
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
@@ -1890,6 +1888,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 kl[r] = 0; pm[r] = 0; ts[r] = 0; ai[r] = 0;
             }
         }
+#if !TBE_Q_WALK
+        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;   // election slots of this chunk
+#endif
         uint32_t mine = 0;
 #pragma unroll
         for (int r = 0; r < kQItems; ++r) {
@@ -1992,18 +1993,24 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             __syncthreads();   // the chunk's rows are settled before the next chunk reads them
             continue;
         }
-        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = kNoOwner;
+        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
         __syncthreads();
 #endif
-        for (;;) {
+        // Owner rounds: each key's earliest pending request wins an election slot tagged
+        // (round << 12) | (4095 - chunk index) by atomicMax, so a newer round's tag beats
+        // every older one and the slots need no reset between rounds (two barriers per
+        // round).  Slots are zeroed at each chunk start.
+        for (uint32_t round = 1;; ++round) {
 #pragma unroll
             for (int r = 0; r < kQItems; ++r)
-                if (pend & (1u << r)) atomicMin(&own[kl[r]], (uint32_t)(r * kQBlock + tid));
+                if (pend & (1u << r)) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kQBlock + tid)));
             __syncthreads();
             uint32_t won = 0;
 #pragma unroll
             for (int r = 0; r < kQItems; ++r) {
-                if (!((pend & (1u << r)) && own[kl[r]] == (uint32_t)(r * kQBlock + tid))) continue;
+                if (!((pend & (1u << r)) &&
+                      own[kl[r]] == ((round << 12) | (4095u - (uint32_t)(r * kQBlock + tid)))))
+                    continue;
                 won |= 1u << r;
                 Slot st = slot[kl[r]];
                 uint64_t h = qh[kl[r]];
@@ -2016,10 +2023,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 if (hmod) qh[kl[r]] = h;
                 if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < kQItems; ++r)
-                if (won & (1u << r)) own[kl[r]] = kNoOwner;
             pend &= ~won;
             if (!__syncthreads_or(pend != 0)) break;
         }

@@ -16,8 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "q_walk": ([], ["--workload", "queue"]),
-    "q_rounds": (["TBE_Q_WALK=0"], ["--workload", "queue"]),
+    "q_tagged": ([], ["--workload", "queue"]),
+    "base": ([], []),
 }
 
 
