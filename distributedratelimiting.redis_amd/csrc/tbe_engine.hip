@@ -1738,8 +1738,9 @@ constexpr int kQChunk = kQBlock * kQItems;         // 2048 requests per chunk
 // One request of one key (WaitAsyncCore Q:67-134 / TryLeaseUnsynchronized Q:136-165)
 // against the key's row `st` and queue header `hdr`; `kr` is the key's ring.  Sets the
 // reply fields and ORs smod / hmod when the row / header changed.
-__device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool &hmod, int32_t p, int64_t ts,
-                                       uint32_t ai, uint64_t *__restrict__ kr, const TbParams &P, const QParams &Q,
+__device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool &hmod, int32_t p, const ReqTime &rq,
+                                       const TimeBase &TB, uint32_t ai, uint64_t *__restrict__ kr, const TbParams &P,
+                                       const QParams &Q,
                                        uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
                                        uint32_t *__restrict__ ev_count, uint32_t ev_cap, uint32_t &status,
                                        uint32_t &rem, bool &evaluated) {
@@ -1754,7 +1755,8 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     bool granted = false;
     if (p == 0 || !(cnt > 0 && Q.order == 0)) {                // Q:153
         bool m;
-        const uint32_t reply = tb_acquire(st, p, ts, P, m);
+        const double ft = req_time_rel(st.t_us == kAbsent ? 0 : st.t_us, TB, 0).new_t;   // the row's field t
+        const uint32_t reply = tb_step_ft(st, ft, p, rq, P, m);
         smod |= m;
         evaluated = true;
         granted = (reply >> 31) != 0;
@@ -1849,6 +1851,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     // back whole; a sparse one gathers and writes back only the rows it touches.
     const bool dense = (e - s) >= (R >> 3);
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
         for (uint32_t j = tid; j < R; j += kQBlock) {
             const uint32_t jj = j < nrows ? j : nrows - 1;
@@ -1982,8 +1985,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                     }
                     uint32_t status, rem;
                     bool evaluated;
-                    q_step(st, h, smod, hmod, p, t, sidx[q], kr, P, Q, ev_cause, ev_id, ev_count, ev_cap, status, rem,
-                           evaluated);
+                    const ReqTime rq1 = req_time_rel(t, TB, P.ttl_ms);
+                    q_step(st, h, smod, hmod, p, rq1, TB, sidx[q], kr, P, Q, ev_cause, ev_id, ev_count, ev_cap, status,
+                           rem, evaluated);
                     put_wait(res, q, status, evaluated, rem, narrow);
                 }
                 if (smod) slot[j] = st;
@@ -1996,6 +2000,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
         __syncthreads();
 #endif
+        ReqTime rq[kQItems];   // state-independent request times, once per request
+#pragma unroll
+        for (int r = 0; r < kQItems; ++r) rq[r] = req_time_rel(ts[r], TB, P.ttl_ms);
         // Owner rounds: each key's earliest pending request wins an election slot tagged
         // (round << 12) | (4095 - chunk index) by atomicMax, so a newer round's tag beats
         // every older one and the slots need no reset between rounds (two barriers per
@@ -2016,7 +2023,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 uint64_t h = qh[kl[r]];
                 bool smod = false, hmod = false, evaluated;
                 uint32_t status, rem;
-                q_step(st, h, smod, hmod, pm[r], ts[r], ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
+                q_step(st, h, smod, hmod, pm[r], rq[r], TB, ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
                        ev_cause, ev_id, ev_count, ev_cap, status, rem, evaluated);
                 put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
