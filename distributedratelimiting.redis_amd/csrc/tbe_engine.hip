@@ -710,7 +710,7 @@ __device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
 #define TBE_WIDE_BLOCK 512
 #endif
 #ifndef TBE_WIDE_PER
-#define TBE_WIDE_PER 2
+#define TBE_WIDE_PER 3
 #endif
 #ifndef TBE_WIDE_FT
 #define TBE_WIDE_FT 0
@@ -719,7 +719,7 @@ __device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
 #define TBE_WIDE_WAVES 6                     // minimum waves per SIMD (register budget)
 #endif
 #ifndef TBE_WIDE_TAIL
-#define TBE_WIDE_TAIL 256
+#define TBE_WIDE_TAIL 512
 #endif
 constexpr int kWideBlock = TBE_WIDE_BLOCK;
 constexpr int kWidePer = TBE_WIDE_PER;
@@ -748,15 +748,15 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
-    __shared__ uint64_t aux[kWideTail * 4];
+    // A pending entry is 16 bytes (row | local id << 16, permits, timestamp); its request
+    // times are recomputed per round rather than stored, so 512 entries fit in 8 KB.
+    __shared__ uint64_t aux[kWideTail * 2];
     __shared__ uint32_t wsum[kWideBlock / 64];
     uint32_t *hcnt = reinterpret_cast<uint32_t *>(aux);
     uint32_t *t_kl_lid = reinterpret_cast<uint32_t *>(aux);
     int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kWideTail;
-    double *t_newt = reinterpret_cast<double *>(aux) + kWideTail;
-    int64_t *t_exp = reinterpret_cast<int64_t *>(aux) + 2 * kWideTail;
-    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + 3 * kWideTail;
-    static_assert(kWideTail * 4 * 8 >= kMaxRows * 4, "hcnt fits in aux");
+    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kWideTail;
+    static_assert(kWideTail * 2 * 8 >= kMaxRows * 4, "hcnt fits in aux");
 #if TBE_WIDE_FT
     __shared__ double ft[kMaxRows];
 #endif
@@ -856,9 +856,11 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (int r = 0; r < kWidePer; ++r)
                 if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
         }
+#if TBE_WIDE_FT
         {
-            // First touch of a row in this bucket: claim it, pull it into LDS (sparse
-            // buckets) and derive its field t.
+            // First touch of a row in this bucket: claim it and derive its field t (with
+            // the field-t cache only; without it the whole slice is already in LDS and
+            // nothing needs claiming).
             uint32_t mine = 0;
 #pragma unroll
             for (int r = 0; r < kWidePer; ++r) {
@@ -886,6 +888,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         for (int r = 0; r < kWidePer; ++r) rq[r] = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms)
                                                            : req_time(tsv[r], P.ttl_ms);
         __syncthreads();   // claimed rows and their field t visible
+#endif
         uint32_t rep[kWidePer];
 #pragma unroll
         for (int r = 0; r < kWidePer; ++r) rep[r] = 0;
@@ -905,7 +908,13 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 if (pend & (1u << r)) {
                     nrow[r] = row[kl[r]];
                     bool m;
-                    rep[r] = tb_step_ft(nrow[r], WIDE_FT_GET(kl[r], nrow[r]), pm[r], rq[r], P, m);
+#if TBE_WIDE_FT
+                    const ReqTime &rqr = rq[r];
+#else
+                    // request times recomputed per evaluation (registers: three slots)
+                    const ReqTime rqr = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
+#endif
+                    rep[r] = tb_step_ft(nrow[r], WIDE_FT_GET(kl[r], nrow[r]), pm[r], rqr, P, m);
                     if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kWideBlock + tid)));
                 }
             }
@@ -935,6 +944,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         // Round 1 settles every key's first request.  The few left pending move to a
         // compact list (one per thread) so later rounds evaluate one request per thread
         // instead of every slot of every lane.
+#ifdef TBE_FOLD_R1_ONLY
+        pend = 0;   // A/B timing only (wrong replies): the cost of the rounds after round 1
+#endif
         uint32_t n_tail;
         const uint32_t tail_at = block_excl_scan<kWideBlock>(__popc(pend), wsum, &n_tail);
         uint32_t keep = ~0u;                     // slots whose reply this thread stores
@@ -945,9 +957,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 if (pend & (1u << r)) {
                     t_kl_lid[at] = kl[r] | ((uint32_t)(r * kWideBlock + tid) << 16);
                     t_pm[at] = pm[r];
-                    t_newt[at] = rq[r].new_t;
-                    t_exp[at] = rq[r].exp_lt;
-                    t_ts[at] = rq[r].ts;
+                    t_ts[at] = tsv[r];
                     ++at;
                 }
             }
@@ -962,7 +972,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 tkl = t_kl_lid[tid] & 0xFFFFu;
                 tlid = t_kl_lid[tid] >> 16;
                 tpm = t_pm[tid];
-                trq = ReqTime{t_newt[tid], t_exp[tid], t_ts[tid]};
+                trq = PACKED ? req_time_rel(t_ts[tid], TB, P.ttl_ms) : req_time(t_ts[tid], P.ttl_ms);
             }
             for (uint32_t round = 2;; ++round) {
                 const uint32_t tag = (round << 12) | (4095u - tlid);

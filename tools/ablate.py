@@ -16,8 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "q_tagged": ([], ["--workload", "queue"]),
     "base": ([], []),
+    "per2_t256": (["TBE_WIDE_PER=2", "TBE_WIDE_TAIL=256"], []),
+    "r1": (["TBE_FOLD_R1_ONLY"], []),
 }
 
 
@@ -42,7 +43,7 @@ def run(rounds: int, steps: int):
             env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so"))
             args = ["--steps", str(steps), "--cpu-seconds", "0"] + ([] if "--no-strdir" in extra else ["--no-host-buffer", "--no-strdir"])
             if "--warmup" not in extra:
-                args += ["--warmup", "2"]
+                args += ["--warmup", "3"]
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + extra, env=env,
                                  capture_output=True, text=True, timeout=300)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")]
