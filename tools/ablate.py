@@ -17,8 +17,9 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "per2_t256": (["TBE_WIDE_PER=2", "TBE_WIDE_TAIL=256"], []),
-    "r1": (["TBE_FOLD_R1_ONLY"], []),
+    "base_q": ([], ["--workload", "queue"]),
+    "base_a": ([], ["--workload", "approx"]),
+    "base_z": ([], ["--workload", "zipf"]),
 }
 
 
