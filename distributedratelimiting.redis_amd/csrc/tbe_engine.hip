@@ -87,7 +87,6 @@ constexpr int kTile = kPartBlock * kPartItems;         // 4096 requests per part
 constexpr int kUnBlock = 1024;
 constexpr int kUnItems = 8;
 constexpr int kUnTile = kUnBlock * kUnItems;
-constexpr int kHistItems = kTile / kBlock;             // k_hist: 256 threads x 32
 #ifndef TBE_HIST_BLOCKS
 #define TBE_HIST_BLOCKS 1024
 #endif
@@ -164,49 +163,62 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
 // consistent even for an (invalid) key >= 2^32.
 // HOT (first pass of a token-bucket batch with hot runs): a hot key's digits come from
 // its run's partition key (hot_sortkey), as in k_scatter_rec<true, true>.
+//
+// 512 threads x 8 keys per tile, and the next tile's keys are loaded while this one is
+// counted (the loads, not the LDS counting, bound this kernel).
+constexpr int kHBlock = 512;
+constexpr int kHItems = kTile / kHBlock;              // 8
 template <typename KeyT, bool HOT = false>
-__global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
-                                                 int shift, uint32_t tiles_per_blk,
-                                                 uint32_t ntiles, uint32_t *__restrict__ tileprefix,
-                                                 uint32_t *__restrict__ blocksum, uint64_t n_keys,
-                                                 uint32_t *__restrict__ err, int validate,
-                                                 uint64_t kmask, const HotSet *__restrict__ hot = nullptr,
-                                                 uint32_t nb = 0, int r_bits = 0,
-                                                 uint32_t *__restrict__ bcount = nullptr,
-                                                 int lowbits = 0, uint32_t nbt = 0) {
+__global__ __launch_bounds__(kHBlock, HOT ? 6 : 8) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
+                                                  int shift, uint32_t tiles_per_blk,
+                                                  uint32_t ntiles, uint32_t *__restrict__ tileprefix,
+                                                  uint32_t *__restrict__ blocksum, uint64_t n_keys,
+                                                  uint32_t *__restrict__ err, int validate,
+                                                  uint64_t kmask, const HotSet *__restrict__ hot = nullptr,
+                                                  uint32_t nb = 0, int r_bits = 0,
+                                                  uint32_t *__restrict__ bcount = nullptr,
+                                                  int lowbits = 0, uint32_t nbt = 0) {
     __shared__ uint32_t h8[kDigits * 8];
     __shared__ uint32_t tile_lo[2];
-    static_assert(kBlock == kDigits, "one digit per thread");
+    static_assert(kHBlock == 2 * kDigits && kDigits * 8 == 4 * kHBlock, "two threads per digit; 4 counters each");
     __shared__ uint64_t hs[HOT ? kHotSlots : 1];
     const int tid = threadIdx.x;
-    const bool any_hot = HOT && hot_load<kBlock>(hot, hs);
+    const bool dig = tid < kDigits;                  // this thread owns digit `tid`'s totals
+    const bool any_hot = HOT && hot_load<kHBlock>(hot, hs);
     const uint32_t t0 = blockIdx.x * tiles_per_blk;
     const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
     uint32_t run = 0;
     uint32_t acc = 0, acc_lo = 0;   // bucket counting (last pass): this thread's digit
     bool bad = false;
-    for (uint32_t t = t0; t < t1; ++t) {
+    KeyT kn[kHItems];
+    auto load = [&](uint32_t t) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) h8[u * kBlock + tid] = 0;
+        for (int it = 0; it < kHItems; ++it) {
+            const uint64_t i = (uint64_t)t * kTile + it * kHBlock + tid;
+            kn[it] = (t < t1 && i < n) ? LD_P(keys + i) : (KeyT)0;
+        }
+    };
+    load(t0);
+    for (uint32_t t = t0; t < t1; ++t) {
+        KeyT kv[kHItems];
+#pragma unroll
+        for (int it = 0; it < kHItems; ++it) kv[it] = kn[it];
+        load(t + 1);                                 // in flight while this tile is counted
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
         __syncthreads();
         const uint64_t base = (uint64_t)t * kTile;
         const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
-        KeyT kv[kHistItems];
-#pragma unroll
-        for (int it = 0; it < kHistItems; ++it) {
-            const uint64_t i = base + it * kBlock + tid;
-            kv[it] = (i < n) ? LD_P(keys + i) : (KeyT)0;
-        }
-        uint32_t skv[kHistItems];
+        uint32_t skv[kHItems];
         if (HOT && any_hot) {
-            hot_sortkeys<kHistItems>(kv, hs, nb, r_bits, skv);
+            hot_sortkeys<kHItems>(kv, hs, nb, r_bits, skv);
         } else {
 #pragma unroll
-            for (int it = 0; it < kHistItems; ++it) skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
+            for (int it = 0; it < kHItems; ++it) skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
         }
 #pragma unroll
-        for (int it = 0; it < kHistItems; ++it) {
-            const uint64_t i = base + it * kBlock + tid;
+        for (int it = 0; it < kHItems; ++it) {
+            const uint64_t i = base + it * kHBlock + tid;
             const bool valid = i < n;
             const uint32_t sk = skv[it];
             const uint32_t d = (sk >> shift) & (kDigits - 1);
@@ -216,20 +228,9 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
                 // the whole wave on one digit (a hot run's tile): one add
                 if (vmask && (vmask & lanemask_lt()) == 0 && valid) atomicAdd(&h8[d0 * 8], (uint32_t)__popcll(vmask));
             } else {
-#ifdef TBE_HIST_MATCH
-                uint64_t peers = vmask;
-#pragma unroll
-                for (int b = 0; b < kDigitBits; ++b) {
-                    const bool bit = (d >> b) & 1u;
-                    const uint64_t m = __ballot(bit);
-                    peers &= bit ? m : ~m;
-                }
-                if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h8[d * 8 + (tid & 7)], (uint32_t)__popcll(peers));
-#else
                 // 8 copies of each counter: lanes that share a digit (skewed traffic) mostly
                 // hit different words instead of serialising on one
                 if (valid) atomicAdd(&h8[d * 8 + (tid & 7)], 1u);
-#endif
             }
             if (valid) {
                 bad |= validate && ((uint64_t)kv[it] >= n_keys);
@@ -242,10 +243,12 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
         }
         __syncthreads();
         uint32_t c = 0;
+        if (dig) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c += h8[tid * 8 + ((u + tid) & 7)];
-        tileprefix[(uint64_t)t * kDigits + tid] = run;
-        run += c;
+            for (int u = 0; u < 8; ++u) c += h8[tid * 8 + ((u + tid) & 7)];
+            tileprefix[(uint64_t)t * kDigits + tid] = run;
+            run += c;
+        }
         if (bcount) {
             // Last pass: count requests per bucket for the fold's bucket starts.  The
             // previous passes left the requests sorted by the bucket's lower bits, so a
@@ -253,36 +256,40 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
             // summed here over the block's consecutive tiles and added once per change.
             const uint32_t lo0 = tile_lo[0], lo1 = tile_lo[1];
             if (lo0 == lo1) {
-                if (lo0 != acc_lo) {
-                    const uint32_t bk = ((uint32_t)tid << lowbits) | acc_lo;
-                    if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
-                    acc = 0;
-                    acc_lo = lo0;
+                if (dig) {
+                    if (lo0 != acc_lo) {
+                        const uint32_t bk = ((uint32_t)tid << lowbits) | acc_lo;
+                        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+                        acc = 0;
+                        acc_lo = lo0;
+                    }
+                    acc += c;
                 }
-                acc += c;
             } else if (lo1 - lo0 < 8) {
                 // the lower bits change inside this tile (at most once per value): count
                 // per (lower bits, digit) in LDS, then add each nonzero count once
                 __syncthreads();                     // everyone has read its digit count
 #pragma unroll
-                for (int u = 0; u < 8; ++u) h8[u * kBlock + tid] = 0;
+                for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
                 __syncthreads();
 #pragma unroll
-                for (int it = 0; it < kHistItems; ++it) {
-                    const uint64_t i = base + it * kBlock + tid;
+                for (int it = 0; it < kHItems; ++it) {
+                    const uint64_t i = base + it * kHBlock + tid;
                     const uint32_t bk = skv[it] >> r_bits;
-                    if (i < n) atomicAdd(&h8[((bk & ((1u << lowbits) - 1u)) - lo0) * kBlock + ((bk >> lowbits) & (kDigits - 1))], 1u);
+                    if (i < n) atomicAdd(&h8[((bk & ((1u << lowbits) - 1u)) - lo0) * kDigits + ((bk >> lowbits) & (kDigits - 1))], 1u);
                 }
                 __syncthreads();
-                for (uint32_t u = 0; u <= lo1 - lo0; ++u) {
-                    const uint32_t cnt = h8[u * kBlock + tid];
-                    const uint32_t bk = ((uint32_t)tid << lowbits) | (lo0 + u);
-                    if (cnt && bk < nbt) atomicAdd(&bcount[bk], cnt);
+                if (dig) {
+                    for (uint32_t u = 0; u <= lo1 - lo0; ++u) {
+                        const uint32_t cnt = h8[u * kDigits + tid];
+                        const uint32_t bk = ((uint32_t)tid << lowbits) | (lo0 + u);
+                        if (cnt && bk < nbt) atomicAdd(&bcount[bk], cnt);
+                    }
                 }
             } else {
 #pragma unroll
-                for (int it = 0; it < kHistItems; ++it) {
-                    const uint64_t i = base + it * kBlock + tid;
+                for (int it = 0; it < kHItems; ++it) {
+                    const uint64_t i = base + it * kHBlock + tid;
                     const uint32_t bk = skv[it] >> r_bits;
                     if (i < n && bk < nbt) atomicAdd(&bcount[bk], 1u);
                 }
@@ -290,11 +297,11 @@ __global__ __launch_bounds__(kBlock) void k_hist(const KeyT *__restrict__ keys, 
         }
         __syncthreads();
     }
-    if (bcount) {
+    if (bcount && dig) {
         const uint32_t bk = ((uint32_t)tid << lowbits) | acc_lo;
         if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
     }
-    blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
+    if (dig) blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
     if (__any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
@@ -2801,22 +2808,22 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         uint32_t *bc = (p == e->passes - 1) ? w.bcount : nullptr;
         const int lowbits = kDigitBits * p;
         if (p == 0 && hot)
-            k_hist<uint64_t, true><<<nblk, kBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+            k_hist<uint64_t, true><<<nblk, kHBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                              w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                              hot, e->nbuckets, e->r_bits, bc, lowbits,
                                                              e->nb_total);
         else if (p == 0)
-            k_hist<uint64_t><<<nblk, kBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
+            k_hist<uint64_t><<<nblk, kHBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total);
         else if (e->packed)
-            k_hist<uint64_t><<<nblk, kBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
+            k_hist<uint64_t><<<nblk, kHBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
                                                        out.tileprefix, w.blocksum, e->cfg.n_keys,
                                                        w.err, 0, kmask, nullptr, e->nbuckets,
                                                        e->r_bits, bc, lowbits, e->nb_total);
         else
-            k_hist<uint32_t><<<nblk, kBlock, 0, sp>>>(w.pass[p - 1].keys, n, shift, tpb, ntiles,
+            k_hist<uint32_t><<<nblk, kHBlock, 0, sp>>>(w.pass[p - 1].keys, n, shift, tpb, ntiles,
                                                        out.tileprefix, w.blocksum, e->cfg.n_keys,
                                                        w.err, 0, kmask, nullptr, e->nbuckets,
                                                        e->r_bits, bc, lowbits, e->nb_total);

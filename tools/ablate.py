@@ -17,9 +17,9 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "no_ustream": (["TBE_NO_USTREAM"], []),
-    "no_ustream_b1024": (["TBE_NO_USTREAM", "TBE_UN_BLOCK=1024"], []),
-    "ustream_b512": (["TBE_UN_BLOCK=512"], []),
+    "base_q": ([], ["--workload", "queue"]),
+    "base_z": ([], ["--workload", "zipf"]),
+    "base_a": ([], ["--workload", "approx"]),
 }
 
 
