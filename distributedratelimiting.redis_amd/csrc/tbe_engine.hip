@@ -974,13 +974,20 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             bool tp = (uint32_t)tid < n_tail;
             uint32_t tkl = 0, tlid = 0, trep = 0;
             int32_t tpm = 0;
+            int64_t tts = 0;
             ReqTime trq{0.0, 0, 0};
-            if (tp) {
-                tkl = t_kl_lid[tid] & 0xFFFFu;
-                tlid = t_kl_lid[tid] >> 16;
-                tpm = t_pm[tid];
-                trq = PACKED ? req_time_rel(t_ts[tid], TB, P.ttl_ms) : req_time(t_ts[tid], P.ttl_ms);
-            }
+            auto take = [&](uint32_t at) {
+                tkl = t_kl_lid[at] & 0xFFFFu;
+                tlid = t_kl_lid[at] >> 16;
+                tpm = t_pm[at];
+                tts = t_ts[at];
+                trq = PACKED ? req_time_rel(tts, TB, P.ttl_ms) : req_time(tts, P.ttl_ms);
+            };
+            if (tp) take(tid);
+            // Each round settles at least the first pending request of every row; when the
+            // survivors fit in fewer waves they are packed to the front of the list, so
+            // later rounds run on fewer waves (the fold is VALU-issue bound).
+            uint32_t in_use = n_tail;
             for (uint32_t round = 2;; ++round) {
                 const uint32_t tag = (round << 12) | (4095u - tlid);
                 Slot nr = Slot{0.0, 0};
@@ -1003,7 +1010,29 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     }
                     if (!tp) put_reply(res, c + tlid, trep, narrow);
                 }
-                if (!__syncthreads_or(tp)) break;
+                const uint64_t bal = __ballot(tp);
+                if ((tid & 63) == 0) wsum[tid >> 6] = (uint32_t)__popcll(bal);
+                __syncthreads();
+                uint32_t off = 0, left = 0;
+#pragma unroll
+                for (int w = 0; w < kWideBlock / 64; ++w) {
+                    const uint32_t cw = wsum[w];
+                    off += (w < (tid >> 6)) ? cw : 0u;
+                    left += cw;
+                }
+                if (left == 0) break;
+                if ((left + 63) / 64 < (in_use + 63) / 64) {
+                    if (tp) {
+                        const uint32_t at = off + (uint32_t)__popcll(bal & lanemask_lt());
+                        t_kl_lid[at] = tkl | (tlid << 16);
+                        t_pm[at] = tpm;
+                        t_ts[at] = tts;
+                    }
+                    __syncthreads();
+                    tp = (uint32_t)tid < left;
+                    if (tp) take(tid);
+                    in_use = left;
+                }
             }
         } else if (n_tail != 0) {
             for (uint32_t round = 2;; ++round) {

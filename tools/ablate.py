@@ -17,9 +17,7 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "base_q": ([], ["--workload", "queue"]),
     "base_z": ([], ["--workload", "zipf"]),
-    "base_a": ([], ["--workload", "approx"]),
 }
 
 
