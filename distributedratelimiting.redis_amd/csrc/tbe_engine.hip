@@ -1835,7 +1835,11 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     }
     uint32_t tail = head + cnt;                                // Q:117-132
     if (tail >= Q.cap) tail -= Q.cap;
+#if !defined(TBE_Q_NO_RING_WRITE)
     kr[tail] = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
+#else
+    (void)kr;   // A/B timing only (wrong queues): the cost of the ring stores
+#endif
     ++cnt;
     qsum += p;
     hdr = qh_pack(head, cnt, qsum);
@@ -1899,12 +1903,25 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
-        for (uint32_t j = tid; j < R; j += kQBlock) {
+        // every load of the slice issued before the first LDS store (one memory latency,
+        // not one per row a thread copies)
+        constexpr int kRPT = (kMaxRows + kQBlock - 1) / kQBlock;
+        Slot tv[kRPT];
+        uint64_t th[kRPT];
+#pragma unroll
+        for (int u = 0; u < kRPT; ++u) {
+            const uint32_t j = tid + u * kQBlock;
             const uint32_t jj = j < nrows ? j : nrows - 1;
-            const Slot t = LD_S(rows + jj);
-            const uint64_t h = LD_U(hrows + jj);
-            slot[j] = t;
-            qh[j] = h;
+            tv[u] = LD_S(rows + jj);
+            th[u] = LD_U(hrows + jj);
+        }
+#pragma unroll
+        for (int u = 0; u < kRPT; ++u) {
+            const uint32_t j = tid + u * kQBlock;
+            if (j < R) {
+                slot[j] = tv[u];
+                qh[j] = th[u];
+            }
         }
     }
     for (uint32_t j = tid; j < (R + 31) / 32; j += kQBlock) {
@@ -2077,6 +2094,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
             pend &= ~won;
+#ifdef TBE_Q_R1_ONLY
+            pend = 0;   // A/B timing only (wrong replies): the cost of the rounds after round 1
+#endif
             if (!__syncthreads_or(pend != 0)) break;
         }
     }
@@ -2225,10 +2245,19 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     const bool dense = (e - s) >= (R >> 3);
 #endif
     if (dense) {
-        for (uint32_t j = tid; j < R; j += kFoldBlock) {
+        // every load of the slice issued before the first LDS store
+        constexpr int kRPT = (kMaxRows + kFoldBlock - 1) / kFoldBlock;
+        u32x4 tv[kRPT];
+#pragma unroll
+        for (int u = 0; u < kRPT; ++u) {
+            const uint32_t j = tid + u * kFoldBlock;
             const ALocal *src = rows + (j < nrows ? j : nrows - 1);
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-            __builtin_memcpy(&sl[j], &v, sizeof v);
+            tv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+        }
+#pragma unroll
+        for (int u = 0; u < kRPT; ++u) {
+            const uint32_t j = tid + u * kFoldBlock;
+            if (j < R) __builtin_memcpy(&sl[j], &tv[u], sizeof tv[u]);
         }
     }
     for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
