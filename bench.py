@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--token-limit", type=int, default=None,
                     help="TokenLimit (default 10; 4 for queue, 100 for approx)")
     ap.add_argument("--queue-limit", type=int, default=16)
+    ap.add_argument("--no-fuse-tick", action="store_true",
+                    help="config D: replenish tick as its own pass (tbe_refresh_device) instead of "
+                         "fused into the batch's fold (A/B)")
     ap.add_argument("--tokens-per-period", type=int, default=1)
     ap.add_argument("--period-ticks", type=int, default=None,
                     help="ReplenishmentPeriod in 100 ns ticks (default 1 s; approx: one batch interval)")

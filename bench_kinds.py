@@ -142,11 +142,17 @@ def run_queue(args, lib, dev, world, rank, dist):
     sh = stream.cuda_stream
     torch.cuda.synchronize()
 
+    fused = not args.no_fuse_tick
+
     def step(s, ev=None):
+        tick = T0_US + (s + 1) * args.interval_us
+        if fused:   # the tick drains inside the batch's fold (tbe_wait_batch_tick_device)
+            eng.wait_batch_tick_device(*bufs[s], st, rem, s * n, tick, lk, li, lr, cnt, stream=sh)
+            return
         eng.wait_batch_device(*bufs[s], st, rem, id_base=s * n, stream=sh)
         if ev:
             ev[0].record(stream)
-        eng.refresh_device(T0_US + (s + 1) * args.interval_us, lk, li, lr, cnt, stream=sh)
+        eng.refresh_device(tick, lk, li, lr, cnt, stream=sh)
         if ev:
             ev[1].record(stream)
 
@@ -169,7 +175,7 @@ def run_queue(args, lib, dev, world, rank, dist):
     elapsed = _barrier_time(dist, dev, t0)
     eng.synchronize()
     stages = eng.stage_times()
-    drain_ms = sum(a.elapsed_time(b) for a, b in evs)
+    drain_ms = 0.0 if fused else sum(a.elapsed_time(b) for a, b in evs)
     # outcome mix of the last batch and its tick (outside the timed region)
     queued += (st == 2).sum()
     drained += cnt.sum()
@@ -178,7 +184,8 @@ def run_queue(args, lib, dev, world, rank, dist):
 
     value = n * steps * world / elapsed
     passes = eng.layout()["passes"]
-    stages["drain"] = drain_ms
+    if not fused:
+        stages["drain"] = drain_ms
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
                 "unscatter": passes, "hot": 1, "drain": 1}
     name = max(stages, key=stages.get)
@@ -216,7 +223,9 @@ def run_queue(args, lib, dev, world, rank, dist):
                    "keys_total": keys_total, "keys_per_gpu": kl, "batch_per_gpu": n,
                    "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
                    "period_ticks": args.period_ticks, "interval_us": args.interval_us,
-                   "partitioning": f"key-hash x{world}, no data-path collective"},
+                   "partitioning": f"key-hash x{world}, no data-path collective",
+                   "tick": "fused into the batch's fold (tbe_wait_batch_tick_device)" if fused
+                   else "own pass (tbe_refresh_device)"},
         "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
         "roofline": _roofline(name, alg, ms, note, "queue"),

@@ -33,7 +33,7 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
             "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device",
             "tbe_import_state", "tbe_queue_cancel", "tbe_alloc_host", "tbe_free_host",
-            "tbe_approx_export_state", "tbe_approx_import_state")
+            "tbe_approx_export_state", "tbe_approx_import_state", "tbe_wait_batch_tick_device")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -137,6 +137,10 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_refresh_device.restype = c_int32
     lib.tbe_refresh_device.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
                                        c_void_p, c_void_p]
+    lib.tbe_wait_batch_tick_device.restype = c_int32
+    lib.tbe_wait_batch_tick_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_int64,
+                                               c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                               c_void_p, c_uint64, c_void_p, c_void_p]
     lib.tbe_approx_acquire_batch_device.restype = c_int32
     lib.tbe_approx_acquire_batch_device.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_int32,
                                                     c_int64, c_void_p, c_void_p, c_void_p]

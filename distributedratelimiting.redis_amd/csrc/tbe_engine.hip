@@ -1847,6 +1847,18 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     status = TBE_WAIT_QUEUED;
 }
 
+// A replenish tick fused into a queue batch (tbe_wait_batch_tick_device): after the
+// batch's requests, every key of the bucket is drained at `ts` exactly as k_drain does,
+// on the rows and headers already in LDS.  ts < 0: no tick.
+struct QTick {
+    int64_t ts;
+    uint64_t *keyseq;
+    int64_t *id;
+    int32_t *rem;
+    uint32_t *count;
+    uint32_t cap;
+};
+
 // TBE_Q_WALK=1: decide each row's requests in one thread after an LDS counting sort
 // instead of election rounds.  Parity-equal, but the config-D fold takes 3.11 ms against
 // 2.41 for the rounds (profiles/r02_ablate_qwalk.log): off by default.
@@ -1872,7 +1884,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
     uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
-    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow) {
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow,
+    QTick T) {
     __shared__ Slot slot[1 << kMaxRBits];
     __shared__ uint64_t qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
@@ -1888,7 +1901,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t s = bstart[b], e = bstart[b + 1];
-    if (s == e) return;
+    const bool tick = T.ts >= 0;
+    if (s == e && !tick) return;
     const uint32_t R = 1u << r_bits;
     const uint32_t rmask = R - 1;
     const uint64_t row0 = (uint64_t)b << r_bits;
@@ -1899,7 +1913,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     // A dense bucket (>= R/8 requests: nearly every 128-byte line of its slice is touched)
     // pulls its whole slice of rows and queue headers with coalesced loads and writes it
     // back whole; a sparse one gathers and writes back only the rows it touches.
-    const bool dense = (e - s) >= (R >> 3);
+    const bool dense = tick || (e - s) >= (R >> 3);   // a tick drains every row
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
@@ -2101,6 +2115,59 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         }
     }
     __syncthreads();
+    if (tick) {
+        // The fused replenish tick (Q:237-271, as k_drain): head (OldestFirst) or tail
+        // (NewestFirst) entries granted while the script grants at T.ts; a one-permit
+        // probe first, so a denied key reads no ring entry.
+        const ReqTime rqT = req_time(T.ts, P.ttl_ms);
+        for (uint32_t j = tid; j < nrows; j += kQBlock) {
+            const uint64_t h0 = qh[j];
+            uint32_t cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
+            if (cnt == 0) continue;
+            uint32_t head = (uint32_t)(h0 & 0xFFFFu);
+            int64_t qsum = (int64_t)(h0 >> 32);
+            Slot st = slot[j];
+            bool smod = false;
+            uint32_t seq = 0;
+            const uint64_t *__restrict__ kr = ring + (row0 + j) * (uint64_t)Q.cap;
+            while (cnt > 0) {
+                {
+                    Slot probe = st;
+                    bool pm;
+                    if (!(tb_step(probe, 1, rqT, P, pm) >> 31)) {
+                        st = probe;
+                        smod |= pm;
+                        break;
+                    }
+                }
+                uint32_t idx = head;
+                if (Q.order == 1) {
+                    idx = head + cnt - 1;
+                    if (idx >= Q.cap) idx -= Q.cap;
+                }
+                const uint64_t ent = kr[idx];
+                const int32_t p = (int32_t)(ent & 0xFFFFu);
+                bool m;
+                const uint32_t reply = tb_step(st, p, rqT, P, m);
+                smod |= m;
+                if (!(reply >> 31)) break;
+                const uint32_t at = atomicAdd(T.count, 1u);
+                if (at < T.cap) {
+                    T.keyseq[at] = ((row0 + j) << 16) | seq;
+                    T.id[at] = (int64_t)(ent >> 16);
+                    T.rem[at] = (int32_t)(reply & 0x7FFFFFFFu);
+                }
+                ++seq;
+                qsum -= p;
+                if (Q.order == 0) head = (head + 1 == Q.cap) ? 0 : head + 1;
+                --cnt;
+            }
+            if (smod) slot[j] = st;
+            if (seq) qh[j] = qh_pack(head, cnt, qsum);
+            if (smod || seq) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+        }
+        __syncthreads();
+    }
     // dense: whole dirty lines of rows (8 per line) and of headers (16 per line)
     for (uint32_t j = tid; j < nrows; j += kQBlock) {
         if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
@@ -2635,6 +2702,7 @@ struct tbe_engine {
     int64_t *gt = nullptr;
     int32_t *acounts = nullptr;   // tbe_approx_refresh's own count buffer (single client)
     int wait_mode = 1;
+    QTick qtick{-1, nullptr, nullptr, nullptr, nullptr, 0};   // tbe_wait_batch_tick_device
     std::vector<std::pair<uint64_t, int64_t>> evicted;              // (cause, id), sorted
     std::vector<std::tuple<uint64_t, int64_t, int32_t>> drained;     // (key, id, rem)
 
@@ -2969,13 +3037,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
                 e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
-                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->narrow ? 1u : 0u);
+                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->narrow ? 1u : 0u,
+                e->qtick);
         else
             k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
                 e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
                 e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
-                e->narrow ? 1u : 0u);
+                e->narrow ? 1u : 0u, e->qtick);
     } else if (e->packed) {
         // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
@@ -3834,6 +3903,39 @@ tbe_status tbe_refresh_device(tbe_engine *e, int64_t ts_us, uint64_t *d_keyseq, 
                                                 e->qp, ts_us, d_keyseq, d_request_id, d_remaining, d_count,
                                                 (uint32_t)std::min<uint64_t>(capacity, 0xFFFFFFFFu));
     HIP_TRY(e, hipGetLastError());
+    e->queued_exact = false;   // queued_total stays an upper bound
+    return TBE_OK;
+}
+
+tbe_status tbe_wait_batch_tick_device(tbe_engine *e, const uint64_t *d_keys, const int32_t *d_permits,
+                                      const int64_t *d_ts_us, uint64_t n, int64_t id_base, int32_t wait,
+                                      uint8_t *d_status, int32_t *d_remaining, int64_t tick_ts_us,
+                                      uint64_t *d_keyseq, int64_t *d_request_id, int32_t *d_log_remaining,
+                                      uint64_t capacity, uint32_t *d_count, void *stream) {
+    if (!e || !d_count) return TBE_EINVAL;
+    if (e->cfg.kind != TBE_KIND_QUEUEING) return fail(e, TBE_EINVAL, "not a queueing engine");
+    if (tick_ts_us < 0) return fail(e, TBE_EINVAL, "tick_ts_us < 0");
+    if (n == 0) return tbe_refresh_device(e, tick_ts_us, d_keyseq, d_request_id, d_log_remaining, capacity,
+                                          d_count, stream);
+    if (!d_ts_us) return fail(e, TBE_EINVAL, "null buffer");
+    // the drain log bound after this batch's possible enqueues (tbe_refresh_bound)
+    const uint64_t per_key = std::min<uint64_t>(e->qp.cap, (uint64_t)std::max(e->qp.token_limit, 1));
+    const uint64_t queued_after = wait ? std::min<uint64_t>(e->queued_total + n, ring_entries(e)) : e->queued_total;
+    const uint64_t bound = std::min<uint64_t>(queued_after, e->cfg.n_keys * per_key);
+    if (capacity < bound || bound > 0xFFFFFFFFull)
+        return fail(e, TBE_EINVAL, "drain log capacity %llu below the bound %llu (tbe_refresh_bound after the batch)",
+                    (unsigned long long)capacity, (unsigned long long)bound);
+    if (bound && (!d_keyseq || !d_request_id || !d_log_remaining)) return fail(e, TBE_EINVAL, "null buffer");
+    HIP_TRY(e, hipSetDevice(e->device));
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    HIP_TRY(e, hipMemsetAsync(d_count, 0, sizeof(uint32_t), st));
+    e->wait_mode = wait ? 1 : 0;
+    e->qtick = QTick{tick_ts_us, d_keyseq, d_request_id, d_log_remaining, d_count,
+                     (uint32_t)std::min<uint64_t>(capacity, 0xFFFFFFFFu)};
+    const tbe_status rc = status_batch_device(e, d_keys, d_permits, d_ts_us, n, id_base, d_status, d_remaining, stream);
+    e->qtick = QTick{-1, nullptr, nullptr, nullptr, nullptr, 0};
+    if (rc != TBE_OK) return rc;
+    e->drained.clear();
     e->queued_exact = false;   // queued_total stays an upper bound
     return TBE_OK;
 }

@@ -266,6 +266,18 @@ class QueueingTokenBucketEngine(TokenBucketEngine):
                                                  d_rem.data_ptr(), d_keyseq.numel(), d_count.data_ptr(),
                                                  stream))
 
+    def wait_batch_tick_device(self, d_keys, d_permits, d_ts, d_status, d_remaining, id_base: int,
+                               tick_ts_us: int, d_keyseq, d_ids, d_rem, d_count, wait: bool = True,
+                               stream: Optional[int] = None) -> None:
+        """``wait_batch_device`` then ``refresh_device(tick_ts_us)`` as one fused call
+        (tbe_wait_batch_tick_device); the log capacity must cover ``refresh_bound()`` after
+        the batch."""
+        n = d_keys.numel()
+        self._check(self._lib.tbe_wait_batch_tick_device(
+            self.handle, d_keys.data_ptr(), d_permits.data_ptr(), d_ts.data_ptr(), n, id_base,
+            1 if wait else 0, d_status.data_ptr(), d_remaining.data_ptr(), tick_ts_us, d_keyseq.data_ptr(),
+            d_ids.data_ptr(), d_rem.data_ptr(), d_keyseq.numel(), d_count.data_ptr(), stream))
+
     def refresh(self, ts_us: int):
         """One replenish tick; returns (keys u64, request ids i64, remaining i32) in (key, drain) order."""
         n = ctypes.c_uint64()

@@ -223,6 +223,19 @@ tbe_status tbe_refresh_device(tbe_engine *engine, int64_t ts_us, uint64_t *d_key
                               int64_t *d_request_id, int32_t *d_remaining, uint64_t capacity,
                               uint32_t *d_count, void *stream);
 
+/* tbe_wait_batch_device followed by tbe_refresh_device(tick_ts_us), fused: the batch's
+ * fold drains every key of its bucket at tick_ts_us right after the batch's requests,
+ * on the rows and queue headers it already holds in LDS, so the tick costs no separate
+ * pass over the table (Q:67-134 then Q:237-271; results, logs and engine state equal
+ * the two calls').  capacity must cover tbe_refresh_bound as it stands AFTER the batch
+ * (the batch's own enqueues count).  An invalid batch skips the tick too (the call is
+ * one unit); it surfaces at tbe_synchronize like any device batch. */
+tbe_status tbe_wait_batch_tick_device(tbe_engine *engine, const uint64_t *d_keys, const int32_t *d_permits,
+                                      const int64_t *d_ts_us, uint64_t n, int64_t id_base, int32_t wait,
+                                      uint8_t *d_status, int32_t *d_remaining, int64_t tick_ts_us,
+                                      uint64_t *d_keyseq, int64_t *d_request_id, int32_t *d_log_remaining,
+                                      uint64_t capacity, uint32_t *d_count, void *stream);
+
 /* Queue of one key, oldest first (Deque enumeration order, DQ:116-125). */
 tbe_status tbe_queue_of(tbe_engine *engine, uint64_t key, int64_t *request_id, int32_t *permits,
                         uint32_t capacity, uint32_t *count);

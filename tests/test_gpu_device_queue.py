@@ -165,3 +165,57 @@ def test_approx_acquire_device(engine_lib, gpu, order, qlimit, wait):
             lo, gl, est, av, q = eng.local_state(key)
             s = client.st(key)
             assert (lo, gl, est, av, q) == (s.local, s.global_, s.est, client.available(s), len(s.queue))
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("n_keys,qlimit,n,rounds,sparse", [
+    (5000, 16, 60000, 4, False),       # dense buckets (every row in LDS)
+    (3_000_000, 4, 20000, 4, True),    # sparse and empty buckets: the tick still drains them
+    (40, 4, 3000, 5, False),
+])
+def test_wait_batch_tick_device(engine_lib, gpu, order, n_keys, qlimit, n, rounds, sparse):
+    """tbe_wait_batch_tick_device == tbe_wait_batch_device + tbe_refresh_device: replies,
+    evictions, drain logs, queues and the bucket table, against the C restatement.  In the
+    sparse case the keys queued by earlier rounds are mostly absent from later batches, so
+    the drain runs in buckets that hold few or no requests."""
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    rng = np.random.default_rng(n_keys + 7 * qlimit + order)
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, qlimit, order, device=0)
+    ref = cref.CQueueingTokenBucket(n_keys, 4, fill_rate(1, 10_000_000), qlimit, order)
+    t, rid = S_US, 0
+    hot = rng.integers(0, n_keys, 64).astype(np.uint64)
+    for rnd in range(rounds):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        if sparse and rnd == 0:
+            keys[: n // 2] = hot[rng.integers(0, 64, n // 2)]   # queues on a few keys first
+        permits = rng.choice([0, 1, 1, 1, 2, 3], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, rid)
+        t += 1_000 + int(rng.integers(0, 3_000_000))
+        k2, i2, r2 = ref.refresh(t)
+        cap = max(n_keys * min(max(qlimit, 1), 4), 1)
+        lk = torch.empty(cap, dtype=torch.int64, device=gpu)
+        li = torch.empty(cap, dtype=torch.int64, device=gpu)
+        lr = torch.empty(cap, dtype=torch.int32, device=gpu)
+        cnt = torch.empty(1, dtype=torch.int32, device=gpu)
+        d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+        d_rem = torch.empty(n, dtype=torch.int32, device=gpu)
+        dk, dp, dt = _dev(keys.view(np.int64), gpu), _dev(permits, gpu), _dev(ts, gpu)
+        torch.cuda.synchronize()   # NULL stream: inputs complete at the call
+        eng.wait_batch_tick_device(dk, dp, dt, d_st, d_rem, rid, t, lk, li, lr, cnt)
+        eng.synchronize()
+        assert np.array_equal(d_st.cpu().numpy(), st2)
+        assert np.array_equal(d_rem.cpu().numpy(), rem2)
+        cause, ids = eng.evicted()
+        assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2)
+        k1, i1, r1 = _sorted_log(lk, li, lr, cnt)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+        rid += n
+    for k in list(range(min(n_keys, 40))) + [int(x) for x in hot[:20]]:
+        assert eng.queue_of(k) == ref.queue_of(k)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))

@@ -16,8 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "base_q": ([], ["--workload", "queue"]),
-    "ringnt_q": (["TBE_Q_RING_NT"], ["--workload", "queue"]),
+    "fused_q": ([], ["--workload", "queue"]),
+    "sep_q": ([], ["--workload", "queue", "--no-fuse-tick"]),
 }
 
 
