@@ -16,8 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "fused_q": ([], ["--workload", "queue"]),
-    "sep_q": ([], ["--workload", "queue", "--no-fuse-tick"]),
+    "base": ([], []),
+    "pad16k": (["TBE_SCATTER_PAD_LDS=16384"], []),
+    "pad32k": (["TBE_SCATTER_PAD_LDS=32768"], []),
+    "pad32k_nohot": (["TBE_SCATTER_PAD_LDS=32768"], ["--no-hot"]),
+    "pad32k_q": (["TBE_SCATTER_PAD_LDS=32768"], ["--workload", "queue"]),
 }
 
 
