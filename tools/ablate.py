@@ -17,10 +17,7 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "pad16k": (["TBE_SCATTER_PAD_LDS=16384"], []),
-    "pad32k": (["TBE_SCATTER_PAD_LDS=32768"], []),
-    "pad32k_nohot": (["TBE_SCATTER_PAD_LDS=32768"], ["--no-hot"]),
-    "pad32k_q": (["TBE_SCATTER_PAD_LDS=32768"], ["--workload", "queue"]),
+    "base_z": ([], ["--workload", "zipf"]),
 }
 
 
