@@ -686,6 +686,15 @@ __device__ __forceinline__ void slot_store_nt(Slot *p, const Slot &s) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
 }
 
+// 16 bytes per lane from global memory straight into LDS (global_load_lds_dwordx4, nt):
+// the LDS destination is the wave-uniform `lds_wave` + 16 * lane.  Visible to the
+// workgroup after the next __syncthreads() (which waits for it).
+typedef __attribute__((address_space(1))) const void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ void lds_dma16(const void *src, void *lds_wave) {
+    __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)lds_wave, 16, 0, 2);
+}
+
 // A token-bucket reply is {granted, trunc(new_v)} with 0 <= trunc(new_v) <= TokenLimit.
 // When TokenLimit <= 127 it travels as one byte (bit 7 granted, bits 0-6 remaining)
 // through the fold and the un-partition passes instead of four.
@@ -821,17 +830,14 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 
     load_chunk(s);   // in flight together with the dense slice
     if (dense) {
+        // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held
+        // for it, so none of the loop invariants spill at this peak.  Rows past nrows get
+        // a copy of the last row; no request reaches them and they are never written.
         constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
-        Slot tmp[kRowsPerThread];
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
             const uint32_t j = tid + u * kWideBlock;
-            tmp[u] = LD_S(rows + (j < nrows ? j : nrows - 1));   // unconditional: keeps tmp in VGPRs
-        }
-#pragma unroll
-        for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kWideBlock;
-            if (j < nrows) row[j] = tmp[u];
+            lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
         }
     }
     for (uint32_t j = tid; j < (R + 31) / 32; j += kWideBlock) {
@@ -2312,19 +2318,13 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     const bool dense = (e - s) >= (R >> 3);
 #endif
     if (dense) {
-        // every load of the slice issued before the first LDS store
+        // HBM -> LDS directly (LDS-DMA, streaming policy; rows past nrows get a copy of
+        // the last row, which nothing reads or writes back)
         constexpr int kRPT = (kMaxRows + kFoldBlock - 1) / kFoldBlock;
-        u32x4 tv[kRPT];
 #pragma unroll
         for (int u = 0; u < kRPT; ++u) {
             const uint32_t j = tid + u * kFoldBlock;
-            const ALocal *src = rows + (j < nrows ? j : nrows - 1);
-            tv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-        }
-#pragma unroll
-        for (int u = 0; u < kRPT; ++u) {
-            const uint32_t j = tid + u * kFoldBlock;
-            if (j < R) __builtin_memcpy(&sl[j], &tv[u], sizeof tv[u]);
+            if (u * kFoldBlock < (int)R) lds_dma16(rows + (j < nrows ? j : nrows - 1), &sl[u * kFoldBlock + (tid & ~63)]);
         }
     }
     for (uint32_t j = tid; j < (R + 31) / 32; j += kFoldBlock) {
