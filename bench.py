@@ -546,7 +546,9 @@ def cpu_baseline(args, n_keys: int, zkeys=(), seed_b: int = SEED_B):
                           "kind": "port",
                           "sample": f"first {sample} requests of each of {b_t} {what} batches "
                                     f"({done_t} decisions, {spent_t:.1f} s), oracle/tb_ref.c "
-                                    f"key-sharded (key % {CPU_THREADS}) over {CPU_THREADS} threads"}
+                                    f"key-sharded (key % {CPU_THREADS}) over {CPU_THREADS} threads",
+                          "cores_note": f"{CPU_THREADS} = the host-CPU share a one-GPU job gets on the GPU box "
+                                        f"(os.cpu_count() reports the whole machine, {os.cpu_count()})"}
     return out
 
 
