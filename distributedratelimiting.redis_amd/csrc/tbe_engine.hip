@@ -1534,11 +1534,20 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
         const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
         int64_t mx = INT64_MIN;
         int32_t mn = INT32_MAX;
-        for (uint32_t q = a + tid; q < b; q += kSegBlock) {
+        uint64_t rv[kSegItems];   // every record of the segment in flight at once
+#pragma unroll
+        for (int it = 0; it < kSegItems; ++it) {
+            const uint32_t q = a + it * kSegBlock + tid;
+            rv[it] = q < b ? srec[q] : 0ull;
+        }
+#pragma unroll
+        for (int it = 0; it < kSegItems; ++it) {
+            const uint32_t q = a + it * kSegBlock + tid;
+            if (q >= b) continue;
             uint32_t k;
             int32_t p;
             int64_t ts;
-            unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
+            unpack_rec(rv[it], ts_orig, tbase, F, k, p, ts);
             mx = max(mx, ts);
             mn = min(mn, p);
         }
@@ -1699,11 +1708,20 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
         const uint32_t h = seg_run(segbase, j);
         const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
         const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
-        for (uint32_t q = a + tid; q < b; q += kSegBlock) {
+        uint64_t rv[kSegItems];   // every record of the segment in flight at once
+#pragma unroll
+        for (int it = 0; it < kSegItems; ++it) {
+            const uint32_t q = a + it * kSegBlock + tid;
+            rv[it] = q < b ? srec[q] : 0ull;
+        }
+#pragma unroll
+        for (int it = 0; it < kSegItems; ++it) {
+            const uint32_t q = a + it * kSegBlock + tid;
+            if (q >= b) continue;
             uint32_t k;
             int32_t p;
             int64_t ts;
-            unpack_rec(srec[q], ts_orig, tbase, F, k, p, ts);
+            unpack_rec(rv[it], ts_orig, tbase, F, k, p, ts);
             Slot c = st.s;
             bool m;
             put_reply(res, q, tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m), narrow);
@@ -2639,6 +2657,8 @@ struct Workspace {
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
     uint32_t *err = nullptr;      // the batch's invalid-request flag
+    hipEvent_t hot_done = nullptr;   // pipelined: k_hot_update of the last batch on this workspace
+    bool hot_pending = false;
     uint32_t *segbase = nullptr;  // hot runs
     SegSummary *summ = nullptr;
     SegState *sst = nullptr;
@@ -2713,7 +2733,8 @@ struct tbe_engine {
     int ws_cur = 0;
     bool pipeline = false;
     hipStream_t pstream = nullptr;
-    hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_out = nullptr;
+    hipStream_t hstream = nullptr;   // pipelined with hot runs: k_hot_update
+    hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_out = nullptr, ev_hot = nullptr;
     uint32_t *sticky = nullptr;      // set by any skipped batch until tbe_synchronize reads it
     uint32_t *last_err = nullptr;    // the error flag of the last enqueued batch
     // host-buffer path staging
@@ -2766,6 +2787,8 @@ void dfree(T *&p) {
 
 void free_workspace(Workspace &w) {
     if (w.used && w.done) (void)hipEventSynchronize(w.done);   // its last batch has finished
+    if (w.hot_pending && w.hot_done) (void)hipEventSynchronize(w.hot_done);
+    w.hot_pending = false;
     for (auto &pb : w.pass) {
         dfree(pb.rec);
         dfree(pb.keys);
@@ -2916,6 +2939,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             HIP_TRY(e, hipStreamWaitEvent(sp, e->ev_in, 0));
         }
         if (w.used) HIP_TRY(e, hipStreamWaitEvent(sp, w.done, 0));
+        if (w.hot_pending) HIP_TRY(e, hipStreamWaitEvent(sp, w.hot_done, 0));   // this batch's hot set
     } else if (in_ready) {            // chunked host-buffer path (queueing / approximate)
         HIP_TRY(e, hipStreamWaitEvent(sf, in_ready, 0));
     }
@@ -3075,7 +3099,17 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                       e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                    w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
-        k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap, w.err);
+        if (pipe) {
+            // The next-but-one batch's hot set, on a stream of its own beside this batch's
+            // un-partition; batch b+2 (same workspace) waits for it before its partition.
+            HIP_TRY(e, hipEventRecord(e->ev_hot, sf));
+            HIP_TRY(e, hipStreamWaitEvent(e->hstream, e->ev_hot, 0));
+            k_hot_update<<<1, 1024, 0, e->hstream>>>(hot_next, e->hot_cap, w.err);
+            HIP_TRY(e, hipEventRecord(w.hot_done, e->hstream));
+            w.hot_pending = true;
+        } else {
+            k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap, w.err);
+        }
         stage_end(e, ST_HOT, sf);
     }
     stage_begin(e, ST_UNSCATTER, sf);
@@ -3239,7 +3273,10 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     e->own_stream = true;
     if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
-    for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ws[0].done, &e->ws[1].done})
+    if (e->pipeline && hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess)
+        return bail(TBE_EDEVICE);
+    for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ev_hot, &e->ws[0].done, &e->ws[1].done,
+                           &e->ws[0].hot_done, &e->ws[1].hot_done})
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(TBE_EDEVICE);
     if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
     if (e->hot_cap) {
@@ -3293,6 +3330,7 @@ void tbe_destroy(tbe_engine *e) {
     if (!e) return;
     if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->hstream) (void)hipStreamSynchronize(e->hstream);
     for (hipStream_t s2 : {e->cin, e->cout, e->cin2})
         if (s2) (void)hipStreamSynchronize(s2);
     free_workspace(e->ws[0]);
@@ -3318,9 +3356,11 @@ void tbe_destroy(tbe_engine *e) {
     for (auto &hs : e->hot) dfree(hs);
     for (auto &ev : e->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ws[0].done, e->ws[1].done})
+    for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ev_hot, e->ws[0].done, e->ws[1].done,
+                          e->ws[0].hot_done, e->ws[1].hot_done})
         if (ev) (void)hipEventDestroy(ev);
     if (e->pstream) (void)hipStreamDestroy(e->pstream);
+    if (e->hstream) (void)hipStreamDestroy(e->hstream);
     for (hipEvent_t ev : e->ev_chunk)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->ev_chunk2)
