@@ -2516,6 +2516,12 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
     uint32_t n_clients, uint32_t my, int64_t ts_us, int64_t stagger_us,
     uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
     uint32_t *__restrict__ log_count, uint32_t log_cap) {
+    // the sync times (TIME at A:241-242) of the first clients are the same for every key
+    constexpr uint32_t kSyncTimes = 64;
+    __shared__ ReqTime crq[kSyncTimes];
+    if (threadIdx.x < min(n_clients, kSyncTimes))
+        crq[threadIdx.x] = req_time(ts_us + (int64_t)threadIdx.x * stagger_us, kApproxTtlMs);
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride) {
         double v = gv[k], p = gp[k];
@@ -2524,7 +2530,7 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
         double my_period = 0.0;
         for (uint32_t r = 0; r < n_clients; ++r) {
             const int64_t ts = ts_us + (int64_t)r * stagger_us;
-            const ReqTime rq = req_time(ts, kApproxTtlMs);                    // A:241-242
+            const ReqTime rq = r < kSyncTimes ? crq[r] : req_time(ts, kApproxTtlMs);   // A:241-242
             const bool present = (t != kAbsent) && !(t < rq.exp_lt);          // EXPIRE 86400 (A:268)
             const double pv = present ? v : 0.0;                              // A:247-252
             const double pp = present ? p : 0.0;

@@ -57,6 +57,42 @@ TBE_HD inline void scaled_fraction(uint64_t m, int e, int s, u128 &num, u128 &de
 // Bit budget on the exact domain 1e-9 <= |x| < 1e23, a = m*2^e, s = 13 - E:
 //   E >= -9  -> s <= 22: num <= 2^53 * 10^22 < 2^127; e >= -83: den <= 2^83
 //   E <= 22  -> -s <= 9: den <= 10^9 * 2^6; e <= 24: num <= 2^77
+// Fast path for 1e-9 <= a < 1e14 (every realistic EWMA period): there s = 13 - E lies in
+// [0, 22], so 10^s is an exact double P, and y = fl(a*P) with err = fma(a, P, -y) is the
+// exact product y + err (the rounding error of a product is representable).  On
+// [1e13, 1e14] y is a multiple of its ulp (2^-9 .. 2^-6) and |err| <= ulp/2, so
+//   d = (y - floor(y)) - 0.5  (exact)  and  sign(d + err) = d != 0 ? sign(d) : sign(err)
+// decide the half-even rounding of the exact value without any 128-bit division.  Same
+// result as the exact path (tests/test_numfmt.py checks both against "%.14g" + float()).
+TBE_HD inline bool round_trip_14g_fast(double a, int be, double &out) {
+    const double kP[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    int E = (int)((double)(be - 1023) * 0.30102999566398120) - ((be - 1023) < 0 ? 1 : 0);
+    E = E < -9 ? -9 : (E > 13 ? 13 : E);
+    double y = 0.0, err = 0.0;
+    for (int it = 0; it < 4; ++it) {
+        const double P = kP[13 - E];
+        y = a * P;
+        err = __builtin_fma(a, P, -y);
+        const bool below = y < 1e13 || (y == 1e13 && err < 0);    // exact product < 10^13
+        const bool above = y > 1e14 || (y == 1e14 && err >= 0);   // exact product >= 10^14
+        if (below && E > -9) { --E; continue; }
+        if (above && E < 13) { ++E; continue; }
+        if (below || above) return false;
+        break;
+    }
+    const double fl = __builtin_floor(y);
+    const double d = (y - fl) - 0.5;
+    bool up;
+    if (d != 0.0) up = d > 0.0;
+    else if (err != 0.0) up = err > 0.0;
+    else up = __builtin_fmod(fl, 2.0) != 0.0;                     // exact tie: to even
+    const double dm = up ? fl + 1.0 : fl;                          // <= 10^14 < 2^53, exact
+    const int k = E - 13;                                          // -22 <= k <= 0
+    out = (k == 0) ? dm : dm / kP[-k];                             // one rounding
+    return true;
+}
+
 TBE_HD inline double round_trip_14g(double x) {
     if (!(x == x) || x == 0.0) return x;                     // NaN, +-0
     const bool neg = x < 0;
@@ -65,6 +101,10 @@ TBE_HD inline double round_trip_14g(double x) {
     uint64_t bits;
     memcpy(&bits, &a, sizeof bits);
     const int be = (int)((bits >> 52) & 0x7FF);
+    if (a < 1e14) {
+        double r;
+        if (round_trip_14g_fast(a, be, r)) return neg ? -r : r;
+    }
     const uint64_t m = (bits & ((1ull << 52) - 1)) | (1ull << 52);
     const int e = be - 1075;                                  // a = m * 2^e
     // E = floor(log10(a)): estimate from the binary exponent, fix with exact compares.

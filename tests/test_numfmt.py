@@ -37,6 +37,12 @@ def values():
     mant = rng.integers(10 ** 13, 10 ** 14, 100_000)
     ex = rng.integers(-22, 9, 100_000)
     v += [float(f"{m}5e{k - 1}") for m, k in zip(mant, ex) if 1e-9 <= float(f"{m}5e{k - 1}") < 1e23]
+    # one ulp either side of exact 14-digit ties (the fast path's sign-of-error decisions)
+    mant = rng.integers(10 ** 13, 10 ** 14, 60_000)
+    ex = rng.integers(-22, 1, 60_000)
+    for m, k in zip(mant, ex):
+        t = float(f"{m}5e{k - 1}")
+        v += [t, np.nextafter(t, 0.0), np.nextafter(t, np.inf)]
     # EWMA periods like the sync script produces
     p = 0.0
     for dt in rng.uniform(0, 3, 20_000):

@@ -16,8 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "base_z": ([], ["--workload", "zipf"]),
-    "base": ([], []),
+    "base_a": ([], ["--workload", "approx"]),
 }
 
 
