@@ -274,7 +274,8 @@ def run_approx(args, lib, dev, world, rank, dist):
     n, steps, warm = args.batch, args.steps, args.warmup
     total = warm + steps
     eng = ApproximateEngine(kshared, args.token_limit, args.tokens_per_period, args.period_ticks,
-                            0, 0, device=dev.index, stage_timing=not args.no_stage_timing, max_batch=n)
+                            0, 0, device=dev.index, stage_timing=not args.no_stage_timing, max_batch=n,
+                            pack=not args.no_pack)
     seed = SEED_E + 7919 * rank
     bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)

@@ -547,7 +547,9 @@ __device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restri
 // in the key field.
 // IDX (queueing kind): each request's arrival index travels beside its record (a second,
 // 4-byte staging round); pass 0 generates it.
-template <bool FIRST, bool HOT = false, bool IDX = false>
+// NOTS (approximate kind, FIRST): no timestamps -- every record takes the escape form,
+// so its payload field carries the arrival index.
+template <bool FIRST, bool HOT = false, bool IDX = false, bool NOTS = false>
 __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
@@ -581,11 +583,11 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
             const bool v = e < nvalid;
             kv[it] = v ? LD_P(kin + base + e) : 0ull;
             pv[it] = v ? LD_P(pin + base + e) : 0;
-            tv[it] = v ? LD_P(tin + base + e) : 0;
+            tv[it] = NOTS ? -1 : (v ? LD_P(tin + base + e) : 0);
         }
         // the table fill overlaps the tile loads above
         any_hot = HOT && hot_load<kPartBlock>(hot, hs);
-        const int64_t tbase = pack_base(tin, F);
+        const int64_t tbase = NOTS ? 0 : pack_base(tin, F);
         uint32_t skv[kPartItems];
         if (HOT && any_hot) {
             hot_sortkeys<kPartItems>(kv, hs, nb, r_bits, skv);
@@ -596,7 +598,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
             const int e = it * kPartBlock + tid;
-            bad |= (e < nvalid) && (pv[it] < 0 || tv[it] < 0);
+            bad |= (e < nvalid) && (pv[it] < 0 || (!NOTS && tv[it] < 0));
             rec[it] = pack_rec(skv[it], pv[it], tv[it], base + e, tbase, F);
             key[it] = skv[it];
         }
@@ -2304,9 +2306,11 @@ __device__ __forceinline__ int32_t dotnet_to_int(double x) {
 // WaitAsyncCore / AcquireCore of one client for every request of one bucket, per key in
 // arrival order (same bucket/chunk/round structure as k_fold; no timestamps: the local
 // tier never reads the clock).  Reply: pack_wait(status, true, AvailableTokens after).
+template <bool PACKED>
 __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
-    const uint32_t *__restrict__ sidx, const uint32_t *__restrict__ bstart, int r_bits,
+    const uint32_t *__restrict__ sidx, const uint64_t *__restrict__ srec, PackFmt F,
+    const uint32_t *__restrict__ bstart, int r_bits,
     uint64_t n_keys, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring, AParams A,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err) {
@@ -2359,9 +2363,16 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
             const uint32_t q = c + r * kFoldBlock + tid;
             kl[r] = 0; pm[r] = 0; ai[r] = 0;
             if (q < e) {
-                kl[r] = skeys[q] & rmask;
-                pm[r] = sperm[q];
-                ai[r] = sidx[q];
+                if (PACKED) {   // key | permit code | escape | arrival index (k_scatter_rec NOTS)
+                    const uint64_t rec = srec[q];
+                    kl[r] = (uint32_t)rec & rmask;
+                    pm[r] = (int32_t)((rec >> F.kb) & ((1ull << F.pb) - 1));
+                    ai[r] = (uint32_t)(rec >> (F.kb + F.pb + 1));
+                } else {
+                    kl[r] = skeys[q] & rmask;
+                    pm[r] = sperm[q];
+                    ai[r] = sidx[q];
+                }
                 pend |= 1u << r;
             }
         }
@@ -2927,7 +2938,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     if (n == 0) return TBE_OK;
     if (n >= (1ull << 32)) return fail(e, TBE_EINVAL, "batch of %llu requests exceeds 2^32-1",
                                        (unsigned long long)n);
-    if (e->packed && !ts) return fail(e, TBE_EINVAL, "null timestamps");
+    if (e->packed && !approx && !ts) return fail(e, TBE_EINVAL, "null timestamps");
     const bool pipe = e->pipeline;
     Workspace &w = e->ws[pipe ? e->ws_cur : 0];
     tbe_status rc = ensure_workspace(e, w, n);
@@ -2988,7 +2999,15 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_colscan<<<kDigits, kBlock, 0, sp>>>(w.blocksum, nblk, out.blockprefix, out.digit_total);
         stage_end(e, ST_COLSCAN, sp);
         stage_begin(e, ST_SCATTER, sp);
-        if (e->packed && wait && p == 0)
+        if (e->packed && approx && p == 0)
+            k_scatter_rec<true, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                keys, permits, nullptr, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                out.digit_total, tpb, out.rec, out.perm, w.err);
+        else if (e->packed && approx)
+            k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err);
+        else if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
@@ -3054,10 +3073,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         a.id_base = id_base;
         a.wait = e->wait_mode;
         a.ai_base = ai_base;
-        k_fold_a<<<e->nbuckets, kFoldBlock, 0, sf>>>(
-            sorted.keys, sorted.permits, sorted.idx, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
-            e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
-            (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+        if (e->packed)
+            k_fold_a<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+                nullptr, nullptr, nullptr, sorted.rec, e->pf, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
+                e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+        else
+            k_fold_a<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+                sorted.keys, sorted.permits, sorted.idx, nullptr, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+                e->alocal, e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
     } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
@@ -3242,8 +3267,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
             e->pf.kmask = (kbits >= 64) ? ~0ull : ((1ull << kbits) - 1);
             e->pf.pc_max = (c.token_limit == INT32_MAX) ? INT32_MAX : c.token_limit + 1;
             e->pf.wb = 64 - kbits - pbits - 1;
-            return (c.kind == TBE_KIND_TOKEN_BUCKET || c.kind == TBE_KIND_QUEUEING) && e->pf.wb >= 32 &&
-                   kbits <= 32 && (c.flags & TBE_FLAG_NO_PACK) == 0;
+            return e->pf.wb >= 32 && kbits <= 32 && (c.flags & TBE_FLAG_NO_PACK) == 0;
         };
         uint32_t hot_cap = 0;
         if ((c.flags & TBE_FLAG_NO_HOT) == 0 && c.kind == TBE_KIND_TOKEN_BUCKET) {

@@ -14,14 +14,20 @@ pytestmark = pytest.mark.gpu
 S_US = 1_760_572_800 * 1_000_000
 
 
-@pytest.mark.parametrize("n_clients,order,qlimit,wait", [(1, OLDEST_FIRST, 8, True), (3, NEWEST_FIRST, 4, True),
-                                                         (8, OLDEST_FIRST, 16, True), (2, OLDEST_FIRST, 0, False)])
-def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait):
+@pytest.mark.parametrize("n_clients,order,qlimit,wait,pack", [
+    (1, OLDEST_FIRST, 8, True, True), (3, NEWEST_FIRST, 4, True, True), (8, OLDEST_FIRST, 16, True, True),
+    (2, OLDEST_FIRST, 0, False, True),
+    # the SoA partition records (TBE_FLAG_NO_PACK; the default when key + permit code
+    # leave less than 32 bits for the arrival index)
+    (3, NEWEST_FIRST, 4, True, False), (2, OLDEST_FIRST, 0, False, False)])
+def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack):
     import torch
     from distributedratelimiting.redis_amd import ApproximateEngine
     n_keys, n, limit, tokens, ticks = 300, 4000, 20, 10, 10_000_000
     rng = np.random.default_rng(n_clients * 100 + order * 10 + qlimit)
-    engines = [ApproximateEngine(n_keys, limit, tokens, ticks, qlimit, order, device=0) for _ in range(n_clients)]
+    engines = [ApproximateEngine(n_keys, limit, tokens, ticks, qlimit, order, device=0, pack=pack)
+               for _ in range(n_clients)]
+    assert engines[0].layout()["packed"] == pack
     clients = [ApproxClient(limit, tokens, ticks, qlimit, order) for _ in range(n_clients)]
     table = ApproxGlobalTable(clients[0].decay_rate)
     counts = [torch.zeros(n_keys, dtype=torch.int32, device=gpu) for _ in range(n_clients)]

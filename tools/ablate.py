@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "base_a": ([], ["--workload", "approx"]),
+    "packed_a": ([], ["--workload", "approx"]),
+    "soa_a": ([], ["--workload", "approx", "--no-pack"]),
 }
 
 
