@@ -74,7 +74,7 @@ def main():
     # average launches per batch (dispatches / dispatches of the fold kernel)
     step = {}
     marker = {"uniform": "k_fold_wide<true>", "zipf": "k_fold_wide<true>", "queue": "k_fold_q<true>",
-              "approx": "k_fold_a"}
+              "approx": "k_fold_a<true>"}
     skip = ("k_gen_batch", "k_init_table", "k_init_approx", "k_count_queued", "k_gen_zipf")
     ours = our_kernels()
     for w, kern in by_w.items():
