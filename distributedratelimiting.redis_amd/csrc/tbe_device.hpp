@@ -328,4 +328,74 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&key)[ITEMS], int shif
 #undef TBE_DIG
 }
 
+// Stable local ranking with WAVE-BLOCKED element order: element e of the tile lives in
+// wave w = e / (64*ITEMS), item slot it = (e / 64) % ITEMS, lane e % 64, so tile order is
+// (wave, slot, lane) order and each wave can rank its own 64*ITEMS elements with a
+// running per-digit count of its own:
+//   A. per slot, ballot-match the 8 digit bits; the lowest lane of each digit group adds
+//      the group's size to its wave's counter (LDS atomic returning the old value), and
+//      every lane's rank is that old value (read from the leader) plus its rank among its
+//      peers -- no per-slot count matrix and no column scan over slots;
+//   B. one thread per digit scans the W wave counts into per-wave offsets, and a block
+//      scan of the digit totals gives lstart[digit];
+//   C. lpos = lstart[d] + wave offset + in-wave rank.
+// LDS: W*256 words (callers alias it with their staging buffer) plus RankLds.  Three
+// barriers plus the block scan's two.
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ int wb_elem(int it) {
+    return (int)((threadIdx.x >> 6) * (64 * ITEMS) + it * 64 + (threadIdx.x & 63));
+}
+
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ void rank_tile_wb(const uint32_t (&key)[ITEMS], int shift, int nvalid,
+                                             RankLds<BLOCK> &L, uint32_t *wcnt, uint32_t (&lpos)[ITEMS]) {
+    constexpr int W = BLOCK / 64;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint32_t *mine = wcnt + w * kDigits;
+#pragma unroll
+    for (int i = lane; i < kDigits; i += 64) mine[i] = 0;   // this wave's row only
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const int e = wb_elem<BLOCK, ITEMS>(it);
+        const bool valid = e < nvalid;
+        const uint32_t dg = (key[it] >> shift) & (kDigits - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kDigitBits; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const int leader = peers ? __ffsll((long long)peers) - 1 : lane;
+        uint32_t old = 0;
+        if (valid && leader == lane) old = atomicAdd(&mine[dg], (uint32_t)__popcll(peers));
+        old = __shfl(old, leader, 64);
+        lpos[it] = old + (uint32_t)__popcll(peers & lt);
+    }
+    __syncthreads();
+    // B: per digit, the waves' counts -> exclusive per-wave offsets; block scan of totals
+    uint32_t tot = 0;
+    if (tid < kDigits) {
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+            const uint32_t c = wcnt[v * kDigits + tid];
+            wcnt[v * kDigits + tid] = tot;
+            tot += c;
+        }
+    }
+    {
+        uint32_t all;
+        const uint32_t ex = block_excl_scan<BLOCK>(tid < kDigits ? tot : 0u, L.wsum, &all);
+        if (tid < kDigits) L.lstart[tid] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t dg = (key[it] >> shift) & (kDigits - 1);
+        lpos[it] += L.lstart[dg] + mine[dg];
+    }
+}
+
 }  // namespace tbe

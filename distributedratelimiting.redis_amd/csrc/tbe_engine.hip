@@ -579,7 +579,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         int64_t tv[kPartItems];
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
-            const int e = it * kPartBlock + tid;
+            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             const bool v = e < nvalid;
             kv[it] = v ? LD_P(kin + base + e) : 0ull;
             pv[it] = v ? LD_P(pin + base + e) : 0;
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         }
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
-            const int e = it * kPartBlock + tid;
+            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             bad |= (e < nvalid) && (pv[it] < 0 || (!NOTS && tv[it] < 0));
             rec[it] = pack_rec(skv[it], pv[it], tv[it], base + e, tbase, F);
             key[it] = skv[it];
@@ -605,17 +605,17 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     } else {
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
-            const int e = it * kPartBlock + tid;
+            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             rec[it] = (e < nvalid) ? LD_P(rin + base + e) : 0ull;
             key[it] = (uint32_t)(rec[it] & F.kmask);
         }
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
-    rank_tile<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint16_t *>(stage), lpos);
+    rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
     __syncthreads();   // the counts in `stage` are dead from here on
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
+        const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
         if (e < nvalid) {
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             stage[lpos[it]] = rec[it];
@@ -639,13 +639,13 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         uint32_t iv[kPartItems];
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
-            const int e = it * kPartBlock + tid;
+            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             iv[it] = (e < nvalid) ? (FIRST ? (uint32_t)(base + e) : iin[base + e]) : 0u;
         }
         __syncthreads();
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
-            const int e = it * kPartBlock + tid;
+            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             if (e < nvalid) stage32[lpos[it]] = iv[it];
         }
         __syncthreads();

@@ -16,8 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "packed_a": ([], ["--workload", "approx"]),
-    "soa_a": ([], ["--workload", "approx", "--no-pack"]),
+    "base": ([], []),
+    "base_z": ([], ["--workload", "zipf"]),
+    "base_q": ([], ["--workload", "queue"]),
+    "base_a": ([], ["--workload", "approx"]),
 }
 
 
