@@ -168,8 +168,14 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
 // counted (the loads, not the LDS counting, bound this kernel).
 constexpr int kHBlock = 512;
 constexpr int kHItems = kTile / kHBlock;              // 8
+#ifndef TBE_HIST_WAVES
+#define TBE_HIST_WAVES 8                     // minimum waves per SIMD (register budget)
+#endif
+#ifndef TBE_HIST_HOT_WAVES
+#define TBE_HIST_HOT_WAVES 6
+#endif
 template <typename KeyT, bool HOT = false>
-__global__ __launch_bounds__(kHBlock, HOT ? 6 : 8) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
+__global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES) void k_hist(const KeyT *__restrict__ keys, uint64_t n,
                                                   int shift, uint32_t tiles_per_blk,
                                                   uint32_t ntiles, uint32_t *__restrict__ tileprefix,
                                                   uint32_t *__restrict__ blocksum, uint64_t n_keys,
@@ -1043,12 +1049,45 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 }
             }
         } else if (n_tail != 0) {
-            for (uint32_t round = 2;; ++round) {
-                Slot nrow[kWidePer];
-                eval_slots(round, nrow);
-                __syncthreads();
-                resolve_slots(round, nrow);
-                if (!__syncthreads_or(pend != 0)) break;
+            // More pending requests than the list holds, or its space holds hcnt: the slots
+            // settle one window of local ids at a time (slot r = ids [r*B, r*B+B)).  A key's
+            // pending requests in slot r follow all of its requests in earlier slots, which
+            // have settled, so each window is a valid order on its own; a round holds one
+            // evaluated row per thread instead of kWidePer (no spilled registers).  The round
+            // number keeps growing across windows, so own[] needs no reset.
+            uint32_t round = 2;
+#pragma unroll
+            for (int r = 0; r < kWidePer; ++r) {
+                const uint32_t bit = 1u << r;
+                const uint32_t tag_lo = 4095u - (uint32_t)(r * kWideBlock + tid);
+                if (!__syncthreads_or(pend & bit)) continue;
+                for (;; ++round) {
+                    const uint32_t tag = (round << 12) | tag_lo;
+                    Slot nr = Slot{0.0, 0};
+                    if (pend & bit) {
+                        nr = row[kl[r]];
+                        bool m;
+                        const ReqTime rqr = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
+                        rep[r] = tb_step_ft(nr, WIDE_FT_GET(kl[r], nr), pm[r], rqr, P, m);
+                        if (m) atomicMax(&own[kl[r]], tag);
+                    }
+                    __syncthreads();
+                    if (pend & bit) {
+                        const uint32_t o = own[kl[r]];
+                        if ((o >> 12) != round || o < tag) {
+                            pend &= ~bit;
+                        } else if (o == tag) {
+                            row[kl[r]] = nr;
+                            WIDE_FT_SET(kl[r], rq[r].new_t);
+                            atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                            pend &= ~bit;
+                        }
+                    }
+                    if (!__syncthreads_or(pend & bit)) {
+                        ++round;
+                        break;
+                    }
+                }
             }
         }
 #pragma unroll
