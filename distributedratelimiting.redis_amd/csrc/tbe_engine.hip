@@ -1951,8 +1951,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow,
     QTick T) {
-    __shared__ Slot slot[1 << kMaxRBits];
-    __shared__ uint64_t qh[1 << kMaxRBits];
+    __shared__ __attribute__((aligned(16))) Slot slot[1 << kMaxRBits];   // LDS-DMA destinations
+    __shared__ __attribute__((aligned(16))) uint64_t qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
     __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
     __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
@@ -1982,24 +1982,27 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
-        // every load of the slice issued before the first LDS store (one memory latency,
-        // not one per row a thread copies)
+        // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held for
+        // it.  Rows one per lane; headers two per lane (16 B), the header array being padded
+        // to an even row count.  Rows past nrows get copies of the last ones; no request
+        // reaches them and they are never written back.
         constexpr int kRPT = (kMaxRows + kQBlock - 1) / kQBlock;
-        Slot tv[kRPT];
-        uint64_t th[kRPT];
 #pragma unroll
         for (int u = 0; u < kRPT; ++u) {
-            const uint32_t j = tid + u * kQBlock;
-            const uint32_t jj = j < nrows ? j : nrows - 1;
-            tv[u] = LD_S(rows + jj);
-            th[u] = LD_U(hrows + jj);
+            const uint32_t wbase = u * kQBlock + (tid & ~63);   // wave-uniform
+            if (wbase < R) {
+                const uint32_t j = tid + u * kQBlock;
+                lds_dma16(rows + (j < nrows ? j : nrows - 1), &slot[wbase]);
+            }
         }
+        constexpr int kHPT = (kMaxRows / 2 + kQBlock - 1) / kQBlock;
+        const uint32_t npair = (nrows + 1) >> 1;
 #pragma unroll
-        for (int u = 0; u < kRPT; ++u) {
-            const uint32_t j = tid + u * kQBlock;
-            if (j < R) {
-                slot[j] = tv[u];
-                qh[j] = th[u];
+        for (int u = 0; u < kHPT; ++u) {
+            const uint32_t wbase = u * kQBlock + (tid & ~63);   // pair index of lane 0
+            if (2 * wbase < R) {
+                const uint32_t pj = tid + u * kQBlock;
+                lds_dma16(hrows + 2 * (pj < npair ? pj : npair - 1), &qh[2 * wbase]);
             }
         }
     }
@@ -2142,9 +2145,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
         __syncthreads();
 #endif
-        ReqTime rq[kQItems];   // state-independent request times, once per request
-#pragma unroll
-        for (int r = 0; r < kQItems; ++r) rq[r] = req_time_rel(ts[r], TB, P.ttl_ms);
         // Owner rounds: each key's earliest pending request wins an election slot tagged
         // (round << 12) | (4095 - chunk index) by atomicMax, so a newer round's tag beats
         // every older one and the slots need no reset between rounds (two barriers per
@@ -2165,7 +2165,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 uint64_t h = qh[kl[r]];
                 bool smod = false, hmod = false, evaluated;
                 uint32_t status, rem;
-                q_step(st, h, smod, hmod, pm[r], rq[r], TB, ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
+                // request times derived by the winner (not held across rounds: registers)
+                const ReqTime rqr = req_time_rel(ts[r], TB, P.ttl_ms);
+                q_step(st, h, smod, hmod, pm[r], rqr, TB, ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
                        ev_cause, ev_id, ev_count, ev_cap, status, rem, evaluated);
                 put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
@@ -2345,8 +2347,12 @@ __device__ __forceinline__ int32_t dotnet_to_int(double x) {
 // WaitAsyncCore / AcquireCore of one client for every request of one bucket, per key in
 // arrival order (same bucket/chunk/round structure as k_fold; no timestamps: the local
 // tier never reads the clock).  Reply: pack_wait(status, true, AvailableTokens after).
+#ifndef TBE_A_WAVES
+#define TBE_A_WAVES 6                        // minimum waves per SIMD: 80 VGPRs, 3 workgroups per CU
+                                             // (0.867 -> 0.688 ms, profiles/r02_ablate_queue_dma_approx_waves.log)
+#endif
 template <bool PACKED>
-__global__ __launch_bounds__(kFoldBlock) void k_fold_a(
+__global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const uint32_t *__restrict__ sidx, const uint64_t *__restrict__ srec, PackFmt F,
     const uint32_t *__restrict__ bstart, int r_bits,
@@ -2394,27 +2400,31 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
     }
     for (uint32_t c = s; c < e; c += kFoldChunk) {
         for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
-        uint32_t kl[kFoldPer], ai[kFoldPer];
+        uint32_t kl[kFoldPer];
         int32_t pm[kFoldPer];
         uint32_t pend = 0;
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            kl[r] = 0; pm[r] = 0; ai[r] = 0;
+            kl[r] = 0; pm[r] = 0;
             if (q < e) {
                 if (PACKED) {   // key | permit code | escape | arrival index (k_scatter_rec NOTS)
                     const uint64_t rec = srec[q];
                     kl[r] = (uint32_t)rec & rmask;
                     pm[r] = (int32_t)((rec >> F.kb) & ((1ull << F.pb) - 1));
-                    ai[r] = (uint32_t)(rec >> (F.kb + F.pb + 1));
                 } else {
                     kl[r] = skeys[q] & rmask;
                     pm[r] = sperm[q];
-                    ai[r] = sidx[q];
                 }
                 pend |= 1u << r;
             }
         }
+        // a request's arrival index is read again where it queues or evicts (rare): not
+        // held across the rounds (registers)
+        auto arrival = [&](int r) -> uint32_t {
+            const uint32_t q = c + r * kFoldBlock + tid;
+            return PACKED ? (uint32_t)(srec[q] >> (F.kb + F.pb + 1)) : sidx[q];
+        };
         __syncthreads();
         uint32_t mine = 0;
 #pragma unroll
@@ -2424,7 +2434,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                 if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
             }
         }
-        {
+        if (mine) {   // sparse buckets only (a dense slice is all loaded)
             ALocal tmp[kFoldPer];
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
@@ -2468,7 +2478,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                         uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
                         uint32_t tail = head + cnt;
                         if (tail >= A.cap) tail -= A.cap;
-                        ring[(row0 + kl[r]) * (uint64_t)A.cap + tail] = (uint64_t)(A.id_base + ai[r]) << 16;
+                        ring[(row0 + kl[r]) * (uint64_t)A.cap + tail] = (uint64_t)(A.id_base + arrival(r)) << 16;
                         a.hc = (head & 0xFFFFu) | ((cnt + 1) << 16);
                         a.zc = (uint16_t)(a.zc + 1);
                         modified = true;
@@ -2492,7 +2502,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                                 const uint64_t ent = kr[head];
                                 const uint32_t at = atomicAdd(ev_count, 1u);
                                 if (at < ev_cap) {
-                                    ev_cause[at] = ai[r] + A.ai_base;
+                                    ev_cause[at] = arrival(r) + A.ai_base;
                                     ev_id[at] = (int64_t)(ent >> 16);
                                 }
                                 a.qsum = (uint16_t)(a.qsum - (uint32_t)(ent & 0xFFFFu));
@@ -2509,7 +2519,7 @@ __global__ __launch_bounds__(kFoldBlock) void k_fold_a(
                     } else {                                               // A:166-181
                         uint32_t tail = head + cnt;
                         if (tail >= A.cap) tail -= A.cap;
-                        kr[tail] = ((uint64_t)(A.id_base + ai[r]) << 16) | (uint32_t)p;
+                        kr[tail] = ((uint64_t)(A.id_base + arrival(r)) << 16) | (uint32_t)p;
                         ++cnt;
                         a.qsum = (uint16_t)(a.qsum + (uint32_t)p);
                         status = TBE_WAIT_QUEUED;
@@ -3363,7 +3373,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->qp.queue_limit = c.queue_limit;
         e->qp.order = c.queue_order;
         e->qp.cap = (uint32_t)std::max(1, c.queue_limit);
-        if (hipMalloc(&e->qhdr, c.n_keys * sizeof(uint64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (hipMalloc(&e->qhdr, ((c.n_keys + 1) & ~1ull) * sizeof(uint64_t)) != hipSuccess)   // even: k_fold_q loads header pairs
+            return bail(TBE_ENOMEM);
         if (hipMalloc(&e->ring, c.n_keys * (uint64_t)e->qp.cap * sizeof(uint64_t)) != hipSuccess)
             return bail(TBE_ENOMEM);
         if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);

@@ -17,11 +17,9 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
-    "slotrounds": (["TBE_WIDE_SLOT_ROUNDS"], []),
-    "hist6": (["TBE_HIST_WAVES=6"], []),
     "base_z": ([], ["--workload", "zipf"]),
-    "slotrounds_z": (["TBE_WIDE_SLOT_ROUNDS"], ["--workload", "zipf"]),
-    "hist5_z": (["TBE_HIST_HOT_WAVES=5"], ["--workload", "zipf"]),
+    "base_q": ([], ["--workload", "queue"]),
+    "base_a": ([], ["--workload", "approx"]),
 }
 
 
