@@ -17,9 +17,9 @@ OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
     "base": ([], []),
+    "per4": (["TBE_WIDE_PER=4"], []),
     "base_z": ([], ["--workload", "zipf"]),
-    "base_q": ([], ["--workload", "queue"]),
-    "base_a": ([], ["--workload", "approx"]),
+    "per4_z": (["TBE_WIDE_PER=4"], ["--workload", "zipf"]),
 }
 
 
