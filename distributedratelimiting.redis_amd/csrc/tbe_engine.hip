@@ -749,6 +749,14 @@ constexpr int kWideBlock = TBE_WIDE_BLOCK;
 constexpr int kWidePer = TBE_WIDE_PER;
 constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
+#ifndef TBE_WIDE_MIN_SHIFT
+#define TBE_WIDE_MIN_SHIFT 5
+#endif
+// k_fold_wide takes buckets of >= R >> kWideMinShift requests (64 of 2048 rows): on a Zipf
+// slice, whose buckets hold fewer requests once the hot keys run apart, its 24 waves per CU
+// fold them faster than k_fold's 12 (config C fold 0.89 -> 0.69 ms; R/2 .. R/2048 measured,
+// profiles/r02_ablate_wide_threshold*.log)
+constexpr int kWideMinShift = TBE_WIDE_MIN_SHIFT;
 static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and tail list");
 // The rows' field t (TB:203 of the stored t_us): cached in LDS, or derived per evaluation
 #if TBE_WIDE_FT
@@ -759,7 +767,7 @@ static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and 
 #define WIDE_FT_SET(j, v) ((void)0)
 #endif
 
-// Full buckets (>= R/2 requests, uniform traffic), shaped as above (three workgroups per
+// Buckets of >= R/32 requests (every bucket of uniform traffic), shaped as above (three workgroups per
 // CU, chunks of 1024 requests).  k_fold below takes the other buckets.
 template <bool PACKED>
 __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
@@ -798,12 +806,12 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-    // Buckets with >= R/2 requests only (k_fold takes the others): nearly every line of
-    // the slice is touched, so the whole slice is pulled in and written back.
+    // Buckets with >= R/32 requests only (k_fold takes the others): the whole slice is
+    // pulled in (LDS-DMA) and only its dirty lines are written back.
 #ifdef TBE_FOLD_NARROW_ONLY
     return;   // A/B: k_fold takes every bucket
 #endif
-    if (e - s < (R >> 1)) return;
+    if (e - s < (R >> kWideMinShift)) return;
     const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
@@ -1167,7 +1175,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
 #ifndef TBE_FOLD_NARROW_ONLY
-    if (e - s >= (R >> 1)) return;   // k_fold_wide's
+    if (e - s >= (R >> kWideMinShift)) return;   // k_fold_wide's
 #endif
     // Whole slice (dense) or touched rows only (sparse), decided below.
     bool dense = false;

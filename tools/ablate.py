@@ -16,10 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
 VARIANTS = {
     # name: (build defines, extra bench args)
-    "base": ([], []),
-    "per4": (["TBE_WIDE_PER=4"], []),
     "base_z": ([], ["--workload", "zipf"]),
-    "per4_z": (["TBE_WIDE_PER=4"], ["--workload", "zipf"]),
+    "ws7_z": (["TBE_WIDE_MIN_SHIFT=7"], ["--workload", "zipf"]),
+    "ws11_z": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "zipf"]),
+    "base_t": ([], ["--workload", "testapp"]),
+    "ws11_t": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "testapp"]),
+    "ws1_t": (["TBE_WIDE_MIN_SHIFT=1"], ["--workload", "testapp"]),
 }
 
 
