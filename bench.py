@@ -6,9 +6,13 @@ uniform keys, batches of 2^26 requests, permits = 1, TokenLimit 10, 1 token / 1 
 batch b spans 10 ms of injected time.  A "step" is one batch: the full decision
 pipeline (partition, fold, un-partition) over 2^26 requests already resident in HBM.
 
-Multi-GPU (torchrun, one rank per GPU): keys are hash-partitioned, each rank owns
-100M / N keys in its own HBM and decides its own 2^26-request batches (no data-path
-collective: weak scaling).  value = all ranks' decisions / max-over-ranks time.
+Multi-GPU (one rank per GPU): keys are hash-partitioned, each rank owns 100M / N keys
+in its own HBM and decides its own 2^26-request batches (no data-path collective: weak
+scaling).  value = all ranks' decisions / max-over-ranks time.  Under torchrun the ranks
+come from the environment; `bench.py --gpus N` without one starts the N ranks itself
+(torch.distributed.run as a child process, from a parent that never touches the GPU)
+and exits with its status.  A run whose world size is not N exits non-zero instead of
+printing a line.
 
 Also reported: per-stage device time, the roofline of the dominant kernel (HIP events
 on the engine stream; for the pipelined engine, over a serial replay of the same timed
@@ -22,6 +26,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +36,8 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+
+from bench_kinds import gather_floats, mark, reduce_max  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED_B = 0x5EED000B
@@ -54,9 +62,14 @@ def parse():
     ap.add_argument("--route", choices=("pre", "timed"), default="pre",
                     help="N > 1: route each step's global requests to their owners before the timed "
                          "region (ingest partitioned) or inside every timed step")
-    ap.add_argument("--approx-mode", choices=("clients", "node"), default="clients",
-                    help="config E with N > 1: every rank a client (all-gather) or the node as one "
-                         "client (all-reduce of the counts)")
+    ap.add_argument("--approx-mode", choices=("node", "clients"), default="node",
+                    help="config E with N > 1: the node as one client (RCCL all-reduce of the counts, "
+                         "the north star's global tier; default) or every rank a client (all-gather); "
+                         "the other mode's refresh epoch is timed after the timed region too")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0 with the gloo backend (the "
+                         "device path's collectives stage through host memory); the line is marked "
+                         "'rehearsal' and its times are not a scaling measurement")
     ap.add_argument("--batch", type=int, default=None, help="requests per batch (default 2^26; testapp 1M)")
     ap.add_argument("--interval-us", type=int, default=None,
                     help="injected time per batch (default 10 ms; 1 ms for queue)")
@@ -66,6 +79,8 @@ def parse():
     ap.add_argument("--no-fuse-tick", action="store_true",
                     help="config D: replenish tick as its own pass (tbe_refresh_device) instead of "
                          "fused into the batch's fold (A/B)")
+    ap.add_argument("--no-drain-variant", action="store_true",
+                    help="config D: skip the second schedule whose ticks grant (draining block)")
     ap.add_argument("--tokens-per-period", type=int, default=1)
     ap.add_argument("--period-ticks", type=int, default=None,
                     help="ReplenishmentPeriod in 100 ns ticks (default 1 s; approx: one batch interval)")
@@ -101,19 +116,63 @@ def parse():
     return args
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) outside torchrun: run this script as N ranks under
+    torch.distributed.run, one per GPU, and return its exit status.  This process makes
+    no GPU call (torch.cuda.device_count() does not initialise the runtime on this image)
+    and starts the ranks as a child process, never by exec."""
+    if not args.share_device:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def dist_setup(args):
+    """(world, rank, local_rank, dist, device) of this rank; exits non-zero when the
+    world size is not --gpus."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: world size {world} != --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     dist = world > 1
     if dist:
+        print(f"bench.py: rank {rank} of {world}", file=sys.stderr, flush=True)
+    gpu = 0 if args.share_device else local_rank
+    torch.cuda.set_device(gpu)
+    if dist:
         import torch.distributed as td
-        torch.cuda.set_device(local_rank)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local_rank if dist else 0)
+        if args.share_device:
+            td.init_process_group("gloo")
+        else:
+            td.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        if td.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {td.get_world_size()} ranks, --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
+    return world, rank, local_rank, dist, torch.device("cuda", gpu)
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, local_rank, dist, dev = dist_setup(args)
+    if dist:
+        import torch.distributed as td
 
     from distributedratelimiting.redis_amd import TokenBucketEngine, _capi
 
@@ -207,6 +266,7 @@ def main():
     torch.cuda.synchronize()
     eng.stage_times()  # discard warm-up stage times
 
+    mark(lib, 1, dev)     # profiling marker: the timed batches follow (outside the timing)
     if dist:
         td.barrier()
     torch.cuda.synchronize()
@@ -218,17 +278,13 @@ def main():
     if dist:
         td.barrier()
     elapsed = time.perf_counter() - t0
+    mark(lib, 2, dev)
     load = None
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        td.all_reduce(tt, op=td.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = reduce_max(elapsed, dev)
         # requests each owner decided in the timed steps: max / mean = the hash partition's
         # imbalance (Zipf: the hot keys' owners)
-        mine = torch.tensor([float(sum(sizes[args.warmup:]))], dtype=torch.float64, device=dev)
-        every = torch.empty(world, dtype=torch.float64, device=dev)
-        td.all_gather_into_tensor(every, mine)
-        ev = every.cpu().numpy()
+        ev = gather_floats(float(sum(sizes[args.warmup:])), world, dev)
         load = {"per_rank_requests": ev.tolist(), "max_over_mean": round(float(ev.max() / ev.mean()), 4)}
     stages_overlapped = eng.stage_times()
     m_last = (raw[-1][0] if raw else bufs[total_steps - 1][0]).numel()
@@ -380,6 +436,7 @@ def main():
                                            "data-path collective timed)" if args.route == "pre" else
                                            "inside every timed step (RCCL all-to-all both ways)")),
                        "layout": layout},
+            **({"rehearsal": REHEARSAL_NOTE} if args.share_device else {}),
             "grant_rate_last_batch": round(grant_rate, 4),
             **({"owner_load": load} if load is not None else {}),
             **({"host_buffer_decisions_per_s": host_rate} if host_rate is not None else {}),
@@ -553,6 +610,8 @@ def cpu_baseline(args, n_keys: int, zkeys=(), seed_b: int = SEED_B):
 
 
 CPU_THREADS = 16
+REHEARSAL_NOTE = ("--share-device: every rank on cuda:0 over gloo (collectives staged through host "
+                  "memory); exercises the multi-rank path, times are not a scaling measurement")
 
 
 if __name__ == "__main__":

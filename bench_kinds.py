@@ -102,6 +102,40 @@ def run(args, lib, dev, world, rank, dist):
     return run_approx(args, lib, dev, world, rank, dist)
 
 
+def reduce_max(x: float, dev) -> float:
+    """Max over ranks of a host scalar (RCCL on the device; gloo on the host)."""
+    import torch.distributed as td
+    t = torch.tensor([x], dtype=torch.float64, device=dev if td.get_backend() != "gloo" else "cpu")
+    td.all_reduce(t, op=td.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_floats(x: float, world: int, dev):
+    """Every rank's host scalar, in rank order."""
+    import torch.distributed as td
+    d = dev if td.get_backend() != "gloo" else "cpu"
+    mine = torch.tensor([x], dtype=torch.float64, device=d)
+    every = torch.empty(world, dtype=torch.float64, device=d)
+    td.all_gather_into_tensor(every, mine)
+    return every.cpu().numpy()
+
+
+
+_MARK_STREAM = {}
+
+
+def mark(lib, tag: int, dev) -> None:
+    """k_mark<tag> dispatch (include/tbe_tools.h): tools/pmc_summary.py keeps the
+    dispatches enqueued between marker 1 and marker 2, i.e. exactly the timed batches.
+    On a stream of its own, outside the timed region."""
+    import ctypes
+    if dev not in _MARK_STREAM:
+        lib.tbe_mark_device.restype = ctypes.c_int
+        lib.tbe_mark_device.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
+        _MARK_STREAM[dev] = torch.cuda.Stream(dev)
+    assert lib.tbe_mark_device(tag, _MARK_STREAM[dev].cuda_stream) == 0
+
+
 def _barrier_time(dist, dev, t0):
     torch.cuda.synchronize()
     if dist:
@@ -109,24 +143,20 @@ def _barrier_time(dist, dev, t0):
         td.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        import torch.distributed as td
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        td.all_reduce(tt, op=td.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = reduce_max(elapsed, dev)
     return elapsed
 
 
-def run_queue(args, lib, dev, world, rank, dist):
+def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=False):
+    """One config-D schedule (warm-up + timed batches, each with its tick) on a fresh
+    engine; returns the timing, stage times and outcome counts."""
     from distributedratelimiting.redis_amd import QueueingTokenBucketEngine
 
-    keys_total = args.keys or 100_000_000
-    kl = (keys_total + world - 1) // world
     n, steps, warm = args.batch, args.steps, args.warmup
     total = warm + steps
-    eng = QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, args.period_ticks,
+    eng = QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, period_ticks,
                                     args.queue_limit, 0, device=dev.index,
                                     stage_timing=not args.no_stage_timing, max_batch=n, pack=not args.no_pack)
-    seed = SEED_D + 7919 * rank
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int32, device=dev)
@@ -135,36 +165,42 @@ def run_queue(args, lib, dev, world, rank, dist):
     lk = torch.empty(cap, dtype=torch.int64, device=dev)
     li = torch.empty(cap, dtype=torch.int64, device=dev)
     lr = torch.empty(cap, dtype=torch.int32, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(total, dtype=torch.int32, device=dev)   # one drain count per tick
+    queued = torch.zeros(total, dtype=torch.int64, device=dev)
     # a stream of our own (the default stream's handle is NULL, which the engine reads as
     # "its own stream"), so the drain's HIP events sit on the stream the kernels run on
     stream = torch.cuda.Stream(dev)
     sh = stream.cuda_stream
     torch.cuda.synchronize()
-
     fused = not args.no_fuse_tick
 
     def step(s, ev=None):
         tick = T0_US + (s + 1) * args.interval_us
+        c = cnt[s:s + 1]
         if fused:   # the tick drains inside the batch's fold (tbe_wait_batch_tick_device)
-            eng.wait_batch_tick_device(*bufs[s], st, rem, s * n, tick, lk, li, lr, cnt, stream=sh)
+            eng.wait_batch_tick_device(*bufs[s], st, rem, s * n, tick, lk, li, lr, c, stream=sh)
             return
         eng.wait_batch_device(*bufs[s], st, rem, id_base=s * n, stream=sh)
         if ev:
             ev[0].record(stream)
-        eng.refresh_device(tick, lk, li, lr, cnt, stream=sh)
+        eng.refresh_device(tick, lk, li, lr, c, stream=sh)
         if ev:
             ev[1].record(stream)
 
+    def outcome(s):   # enqueues of batch s (outside the timed region: warm-up only)
+        with torch.cuda.stream(stream):
+            queued[s] = (st == 2).sum()
+
     for s in range(warm):
         step(s)
+        outcome(s)
     torch.cuda.synchronize()
     eng.synchronize()
     eng.stage_times()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
-    queued = torch.zeros((), dtype=torch.int64, device=dev)
-    drained = torch.zeros((), dtype=torch.int64, device=dev)
+    if marked:
+        mark(lib, 1, dev)
     if dist:
         import torch.distributed as td
         td.barrier()
@@ -173,25 +209,42 @@ def run_queue(args, lib, dev, world, rank, dist):
     for i, s in enumerate(range(warm, total)):
         step(s, evs[i])
     elapsed = _barrier_time(dist, dev, t0)
+    if marked:
+        mark(lib, 2, dev)
     eng.synchronize()
     stages = eng.stage_times()
     drain_ms = 0.0 if fused else sum(a.elapsed_time(b) for a, b in evs)
-    # outcome mix of the last batch and its tick (outside the timed region)
-    queued += (st == 2).sum()
-    drained += cnt.sum()
-    q_last, d_last = int(queued.item()), int(drained.item())
+    outcome(total - 1)
+    torch.cuda.synchronize()
+    grants = cnt.cpu().numpy().astype(np.int64)
+    q = queued.cpu().numpy()
     granted = float((st == 1).float().mean().item())
-
-    value = n * steps * world / elapsed
-    passes = eng.layout()["passes"]
     if not fused:
         stages["drain"] = drain_ms
+    out = {"elapsed": elapsed, "stages": stages, "granted": granted, "q_last": int(q[-1]),
+           "tick_grants_per_step": grants[warm:].tolist(), "d_last": int(grants[-1]),
+           "queued_warmup": q[:warm].tolist(), "layout": eng.layout()}
+    eng.close()
+    return out
+
+
+def run_queue(args, lib, dev, world, rank, dist):
+    keys_total = args.keys or 100_000_000
+    kl = (keys_total + world - 1) // world
+    n, steps = args.batch, args.steps
+    seed = SEED_D + 7919 * rank
+    fused = not args.no_fuse_tick
+    r = _queue_pass(args, lib, dev, world, dist, kl, args.period_ticks, seed, marked=True)
+    elapsed, stages, granted, q_last, d_last = r["elapsed"], r["stages"], r["granted"], r["q_last"], r["d_last"]
+
+    value = n * steps * world / elapsed
+    passes = r["layout"]["passes"]
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
                 "unscatter": passes, "hot": 1, "drain": 1}
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
     u = _distinct(n, kl)
-    packed = bool(eng.layout().get("packed"))
+    packed = bool(r["layout"].get("packed"))
     if name == "fold":
         # records (packed: u64 record 8 + arrival index 4; wide: key 4, permits 4, ts 8,
         # index 4) + packed reply 4 per request; per distinct key: bucket row 16 + queue
@@ -215,7 +268,7 @@ def run_queue(args, lib, dev, world, rank, dist):
         note = "n*20"
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
-        "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (splitmix64 seeded trace generated in HBM)",
         "config": {"workload": f"TokenBucketWithQueue OldestFirst, QueueLimit {args.queue_limit}, "
@@ -227,6 +280,7 @@ def run_queue(args, lib, dev, world, rank, dist):
                    "tick": "fused into the batch's fold (tbe_wait_batch_tick_device)" if fused
                    else "own pass (tbe_refresh_device)"},
         "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
+        "tick_grants_per_step": r["tick_grants_per_step"],
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
         "roofline": _roofline(name, alg, ms, note, "queue"),
         "cpu_baseline": None,
@@ -235,7 +289,24 @@ def run_queue(args, lib, dev, world, rank, dist):
     # + 8 B per enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
     _step_roofline(line, n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8,
                    "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)", "queue")
-    eng.close()
+    if not args.no_drain_variant:
+        # The same schedule with ticks that grant: at 1 token/s a saturated key frees one
+        # queue entry per ~1000 ticks, so config D's ticks drain nothing within a run.  With
+        # ReplenishmentPeriod = 2 batch intervals every queued key gains half a token per
+        # tick, and the FIFO drain (Q:237-271) completes millions of entries per tick.
+        pt = 2 * args.interval_us * 10
+        d = _queue_pass(args, lib, dev, world, dist, kl, pt, seed)
+        g = np.array(d["tick_grants_per_step"], dtype=np.float64)
+        line["draining"] = {
+            "period_ticks": pt, "tokens_per_period": args.tokens_per_period,
+            "value": round(n * steps * world / d["elapsed"], 1),
+            "ms_per_step": round(d["elapsed"] / steps * 1e3, 4),
+            "tick_grants_per_step": d["tick_grants_per_step"],
+            "tick_grants_mean": round(float(g.mean()), 1) if g.size else 0.0,
+            "granted_frac_last_batch": round(d["granted"], 4), "queued_last_batch": d["q_last"],
+            "stage_ms_per_step": {k: round(v / steps, 4) for k, v in d["stages"].items()},
+            "note": "config D's schedule with ReplenishmentPeriod = 2 batch intervals: the fused ticks "
+                    "drain queued entries every step (tick_grants = entries completed by each timed tick)"}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_queue(args, kl)
     return line
@@ -285,34 +356,40 @@ def run_approx(args, lib, dev, world, rank, dist):
     period_us = args.period_ticks // 10
     stagger = period_us // world
     torch.cuda.synchronize()
-    refresh_s = [0.0]
+    refresh_s = {"node": [0.0, 0], "clients": [0.0, 0]}
+    from distributedratelimiting.redis_amd import cluster
+
+    def refresh(s, mode, timed):
+        t1 = time.perf_counter()
+        eng.collect(counts)             # A:430-435
+        ts = T0_US + (s + 1) * args.interval_us
+        if mode == "node":
+            if dist:                    # RCCL all-reduce over xGMI: the node is ONE client
+                cluster._all_reduce_sum(counts)
+                torch.cuda.current_stream(dev).synchronize()
+            eng.sync(counts, 1, 0, ts, 0)
+        else:
+            if dist:                    # RCCL all-gather: every rank a client
+                cluster._all_gather(allc, counts)
+                torch.cuda.current_stream(dev).synchronize()   # the sync replay reads allc
+            eng.sync(allc, world, rank, ts, stagger)
+        if timed:
+            refresh_s[mode][0] += time.perf_counter() - t1
+            refresh_s[mode][1] += 1
 
     def step(s, timed=False):
         # everything on the engine's stream; collect synchronises it
         eng.acquire_batch_device(*bufs[s], st, av, wait=False, id_base=s * n)
         if timed:   # collect would wait for the batch anyway; this keeps it out of refresh time
             torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        eng.collect(counts)             # A:430-435
-        if dist and args.approx_mode == "node":
-            import torch.distributed as td
-            td.all_reduce(counts)                     # RCCL over xGMI: the node is ONE client
-            torch.cuda.current_stream(dev).synchronize()
-            eng.sync(counts, 1, 0, T0_US + (s + 1) * args.interval_us, 0)
-        else:
-            if dist:
-                import torch.distributed as td
-                td.all_gather_into_tensor(allc, counts)   # RCCL over xGMI
-                torch.cuda.current_stream(dev).synchronize()   # the sync replay reads allc
-            eng.sync(allc, world, rank, T0_US + (s + 1) * args.interval_us, stagger)
-        if timed:
-            refresh_s[0] += time.perf_counter() - t1
+        refresh(s, args.approx_mode, timed)
 
     for s in range(warm):
         step(s)
     torch.cuda.synchronize()
     eng.synchronize()
     eng.stage_times()
+    mark(lib, 1, dev)
     if dist:
         import torch.distributed as td
         td.barrier()
@@ -321,9 +398,22 @@ def run_approx(args, lib, dev, world, rank, dist):
     for s in range(warm, total):
         step(s, timed=True)
     elapsed = _barrier_time(dist, dev, t0)
+    mark(lib, 2, dev)
     eng.synchronize()
     stages = eng.stage_times()
     granted = float((st == 1).float().mean().item())
+    # the other exchange mode's refresh epoch, timed after the timed region on the same
+    # engine (its counts are the last batch's local scores, then zeros)
+    alt = "clients" if args.approx_mode == "node" else "node"
+    if dist:
+        td.barrier()
+    for j in range(min(steps, 5)):
+        refresh(total + j, alt, True)
+    refresh_ms = {m: round(v[0] / v[1] * 1e3, 4) if v[1] else None for m, v in refresh_s.items()}
+    if dist:
+        refresh_ms = {m: round(reduce_max(v, dev), 4) if v is not None else None for m, v in refresh_ms.items()}
+    # bytes each GPU receives per refresh: ring all-reduce 2 (N-1)/N * 4K, all-gather (N-1) * 4K
+    xbytes = {"node": int(2 * (world - 1) * kshared * 4 // world), "clients": int((world - 1) * kshared * 4)}
 
     value = n * steps * world / elapsed
     passes = eng.layout()["passes"]
@@ -353,13 +443,18 @@ def run_approx(args, lib, dev, world, rank, dist):
                    "keys_shared": kshared, "batch_per_gpu": n, "token_limit": args.token_limit,
                    "tokens_per_period": args.tokens_per_period, "period_ticks": args.period_ticks,
                    "interval_us": args.interval_us, "clients": world,
+                   "approx_mode": args.approx_mode,
                    "exchange": ("none (one client)" if not dist else
                                 "RCCL all-reduce of int32 counts (the node is one client, SURVEY.md §8e option 1)"
                                 if args.approx_mode == "node" else
                                 "RCCL all-gather of int32 counts (every rank a client, §8e option 2)")},
         "granted_frac_last_batch": round(granted, 4),
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
-        "refresh_ms_per_step_wall": round(refresh_s[0] / steps * 1e3, 4),
+        "refresh_ms_per_step_wall": refresh_ms[args.approx_mode],
+        "refresh_modes": {m: {"ms_per_epoch_wall": refresh_ms[m], "exchange_bytes_per_gpu": xbytes[m],
+                              "timed": "in the timed steps" if m == args.approx_mode else
+                                       f"{min(steps, 5)} epochs after the timed region"}
+                          for m in ("node", "clients")},
         "roofline": _roofline(name, alg, ms, note, "approx"),
         "cpu_baseline": None,
     }

@@ -27,7 +27,15 @@ Exchanges:
   same sync calls on its replica of the global tier.
 
 Inputs as CUDA tensors take the device path (backend "nccl" = RCCL over xGMI); numpy
-arrays take a host path with identical semantics (backend "gloo", the CPU tests).
+arrays take a host path with identical semantics (backend "gloo", the CPU tests).  The
+device path also runs over a "gloo" group (its collectives then stage through host
+memory): that is how two ranks sharing one GPU exercise the whole device path in the
+tests (RCCL refuses two ranks on one device).
+
+Directories never free ids (a key keeps its bucket for the directory's lifetime, like a
+Redis key that has not expired); a batch that brings more new keys than ids remain
+raises ``TbeError(TBE_ERANGE)`` before any decision is made, and the directory must be
+recreated.
 """
 from __future__ import annotations
 
@@ -97,6 +105,12 @@ class HostDirectory:
         self.ids = {}
         self.overflow = False
 
+    def check(self) -> None:
+        """Raise TbeError(TBE_ERANGE) once a batch has brought more new keys than ids remained."""
+        if self.overflow:
+            from . import _capi
+            raise _capi.TbeError(_capi.TBE_ERANGE, f"key directory over capacity ({self.capacity} ids)")
+
     def assign(self, keys) -> np.ndarray:
         keys = np.asarray(keys, dtype=np.uint64)
         if keys.size == 0:
@@ -135,11 +149,21 @@ class DeviceDirectory:
             raise _capi.TbeError(st, f"tbe_dir_create({capacity}) failed")
         self._h = h
         self.capacity = int(capacity)
+        # upper bound of the ids assigned so far (each key of an assign batch adds at most
+        # one): while it stays below capacity no batch can have overflowed, so the exact
+        # count (a device synchronisation) is fetched only once the bound reaches it
+        self._bound = 0
 
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.tbe_dir_destroy(self._h)
             self._h = None
+
+    def check(self) -> None:
+        """Raise TbeError(TBE_ERANGE) if an assign batch overflowed the directory; free
+        (no device synchronisation) while the assigned-id bound stays below capacity."""
+        if self._bound >= self.capacity:
+            self._bound = self.size()      # raises TBE_ERANGE on overflow
 
     def __del__(self):
         try:
@@ -150,6 +174,8 @@ class DeviceDirectory:
     def _run(self, fn, d_keys):
         import torch
         from . import _capi
+        if not _is_cuda(d_keys) or d_keys.dtype not in (torch.int64, torch.uint64):
+            raise TypeError("DeviceDirectory takes an int64 (or uint64) CUDA tensor of keys")
         d_keys = d_keys.contiguous()
         ids = torch.empty(d_keys.numel(), dtype=torch.int64, device=d_keys.device)
         st = fn(self._h, d_keys.data_ptr(), d_keys.numel(), ids.data_ptr(), device_stream(d_keys.device))
@@ -158,8 +184,12 @@ class DeviceDirectory:
         return ids
 
     def assign(self, d_keys):
-        """int64 device tensor of keys -> int64 device tensor of ids (assigning new ones)."""
-        return self._run(self._lib.tbe_dir_assign_device, d_keys)
+        """int64 device tensor of keys -> int64 device tensor of ids (assigning new ones).
+        Raises TbeError(TBE_ERANGE) if the batch overflowed the directory."""
+        ids = self._run(self._lib.tbe_dir_assign_device, d_keys)
+        self._bound += d_keys.numel()
+        self.check()
+        return ids
 
     def lookup(self, d_keys):
         """ids of known keys, -1 (UINT64_MAX) for others; assigns nothing."""
@@ -180,6 +210,44 @@ def keys_per_rank(n_keys: int, world: int, slack: float = 0.01) -> int:
     a margin far above the binomial spread of the owner counts."""
     share = -(-n_keys // world)
     return n_keys if world == 1 else min(n_keys, int(share * (1.0 + slack)) + 1024)
+
+
+# ------------------------------------------------------------------ collectives
+def _stages_through_host(t, group) -> bool:
+    """A CUDA tensor on a gloo group: gloo's all-to-all / all-gather take host tensors."""
+    import torch.distributed as dist
+    return _is_cuda(t) and dist.get_backend(group) == "gloo"
+
+
+def _all_to_all(out, inp, out_splits=None, in_splits=None, group=None) -> None:
+    import torch.distributed as dist
+    if _stages_through_host(inp, group):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        out.copy_(o)
+        return
+    dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+
+
+def _all_gather(out, inp, group=None) -> None:
+    import torch.distributed as dist
+    if _stages_through_host(inp, group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+        return
+    dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def _all_reduce_sum(t, group=None) -> None:
+    import torch.distributed as dist
+    if _stages_through_host(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+        return
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
 # ------------------------------------------------------------------ all-to-all routing
@@ -204,27 +272,11 @@ def route_requests(keys, permits, ts_us, directory, group=None):
 
     world = dist.get_world_size(group)
     if _is_cuda(keys):
-        from . import _capi
-        lib = _capi.load()
         dev = keys.device
-        stream = device_stream(dev)
-        keys = keys.contiguous()
-        n = keys.numel()
-        pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        counts = torch.zeros(world, dtype=torch.int64, device=dev)
-        work = torch.empty(max(1, lib.tbe_route_workspace_bytes(n, world)), dtype=torch.uint8, device=dev)
-        _check(lib.tbe_route_plan_device(keys.data_ptr(), n, world, work.data_ptr(), pos.data_ptr(),
-                                         counts.data_ptr(), stream))
-        send = torch.empty((n, 3), dtype=torch.int64, device=dev)
-        _check(lib.tbe_route_pack_device(pos.data_ptr(), n, keys.data_ptr(), permits.contiguous().data_ptr(),
-                                         ts_us.contiguous().data_ptr(), send.data_ptr(), stream))
-        rc = torch.empty_like(counts)
-        dist.all_to_all_single(rc, counts, group=group)
-        sc_l, rc_l = counts.tolist(), rc.tolist()
-        recv = torch.empty((sum(rc_l), 3), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(recv, send, output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
+        keys, permits, ts_us = _device_columns(keys, (permits, torch.int32), (ts_us, torch.int64))
+        pos, sc_l, rc_l, recv = _route_device(keys, permits, ts_us, world, group)
         local = directory.assign(recv[:, 0])
-        return (local, recv[:, 2].to(torch.int32), recv[:, 1].contiguous()), RoutePlan(pos, sc_l, rc_l, n)
+        return (local, recv[:, 2].to(torch.int32), recv[:, 1].contiguous()), RoutePlan(pos, sc_l, rc_l, keys.numel())
     keys = np.asarray(keys, dtype=np.uint64)
     n = keys.shape[0]
     owner = key_owner(keys, world)
@@ -242,8 +294,53 @@ def route_requests(keys, permits, ts_us, directory, group=None):
                            group=group)
     r = recv.numpy()
     local = directory.assign(r[:, 0].view(np.uint64))
+    directory.check()
     return (local, r[:, 2].astype(np.int32), r[:, 1].copy()), RoutePlan(order, send_counts.tolist(),
                                                                         recv_counts.tolist(), n)
+
+
+def _device_columns(keys, *cols):
+    """The device path's input contract: keys int64 (uint64 is reinterpreted), the other
+    columns converted to the dtype the route kernels read, all on the keys' device."""
+    import torch
+    if keys.dtype == torch.uint64:
+        keys = keys.view(torch.int64)
+    if keys.dtype != torch.int64:
+        raise TypeError(f"keys must be an int64 or uint64 tensor, not {keys.dtype}")
+    out = [keys.contiguous()]
+    for c, dt in cols:
+        if not _is_cuda(c) or c.device != keys.device:
+            raise ValueError("every column of a device-path batch must be on the keys' device")
+        if c.numel() != keys.numel():
+            raise ValueError("columns differ in length")
+        out.append(c.to(dt).contiguous())
+    return tuple(out)
+
+
+def _route_device(keys, permits, payload, world, group):
+    """Owner-grouped exchange of {key, payload i64, permits i32} records on the device:
+    tbe_route_plan_device + tbe_route_pack_device, the split sizes by all-to-all, the
+    records by all-to-all.  Returns (pos, send counts, recv counts, recv [m, 3] int64)."""
+    import torch
+    from . import _capi
+    lib = _capi.load()
+    dev = keys.device
+    stream = device_stream(dev)
+    n = keys.numel()
+    pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.zeros(world, dtype=torch.int64, device=dev)
+    work = torch.empty(max(1, lib.tbe_route_workspace_bytes(n, world)), dtype=torch.uint8, device=dev)
+    _check(lib.tbe_route_plan_device(keys.data_ptr(), n, world, work.data_ptr(), pos.data_ptr(),
+                                     counts.data_ptr(), stream))
+    send = torch.empty((n, 3), dtype=torch.int64, device=dev)
+    _check(lib.tbe_route_pack_device(pos.data_ptr(), n, keys.data_ptr(), permits.data_ptr(),
+                                     payload.data_ptr(), send.data_ptr(), stream))
+    rc = torch.empty_like(counts)
+    _all_to_all(rc, counts, group=group)
+    sc_l, rc_l = counts.tolist(), rc.tolist()
+    recv = torch.empty((sum(rc_l), 3), dtype=torch.int64, device=dev)
+    _all_to_all(recv, send, rc_l, sc_l, group=group)
+    return pos, sc_l, rc_l, recv
 
 
 def route_replies(plan: RoutePlan, cols, group=None):
@@ -259,8 +356,7 @@ def route_replies(plan: RoutePlan, cols, group=None):
         reply = torch.stack([c.to(torch.int64) for c in cols], dim=1).contiguous()
         k = reply.shape[1]
         back = torch.empty((plan.n, k), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(back, reply, output_split_sizes=plan.send_counts,
-                               input_split_sizes=plan.recv_counts, group=group)
+        _all_to_all(back, reply, plan.send_counts, plan.recv_counts, group=group)
         out = torch.empty_like(back)
         _check(lib.tbe_route_gather_device(plan.order.data_ptr(), plan.n, back.data_ptr(), k, out.data_ptr(),
                                            device_stream(dev)))
@@ -306,6 +402,10 @@ def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    if _is_cuda(keys):
+        return _route_cancel_device(cancel, keys, request_ids, directory, world, group)
+    if isinstance(directory, DeviceDirectory):
+        raise TypeError("route_cancel with a DeviceDirectory takes CUDA tensors of keys and request ids")
     keys = np.asarray(keys, dtype=np.uint64)
     n = keys.shape[0]
     owner = key_owner(keys, world)
@@ -333,6 +433,36 @@ def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
     out = np.empty(n, dtype=np.uint8)
     out[order] = back.numpy()
     return out
+
+
+def _route_cancel_device(cancel, keys, request_ids, directory, world, group):
+    """route_cancel's device path: (key, request id) pairs go to the owners through the
+    route kernels (the id rides in the record's i64 payload), the owner's DeviceDirectory
+    looks the keys up (a key it never assigned has nothing queued), ``cancel(local ids,
+    request ids)`` gets the known pairs as int64 device tensors, and the hits come back
+    through the reverse all-to-all.  Returns u8 hits (device tensor) in this rank's order."""
+    import torch
+    from . import _capi
+    if not isinstance(directory, DeviceDirectory):
+        raise TypeError("route_cancel with CUDA tensors needs a DeviceDirectory")
+    keys, request_ids = _device_columns(keys, (request_ids, torch.int64))
+    dev = keys.device
+    zero = torch.zeros(keys.numel(), dtype=torch.int32, device=dev)
+    pos, sc_l, rc_l, recv = _route_device(keys, zero, request_ids, world, group)
+    hit = torch.zeros(recv.shape[0], dtype=torch.int64, device=dev)
+    if recv.shape[0]:
+        local = directory.lookup(recv[:, 0])
+        known = torch.nonzero(local != -1).flatten()
+        if known.numel():
+            h = cancel(local[known], recv[known, 1].contiguous())
+            hit[known] = torch.as_tensor(np.asarray(h) if not _is_cuda(h) else h, device=dev).to(torch.int64)
+    back = torch.empty((keys.numel(), 1), dtype=torch.int64, device=dev)
+    _all_to_all(back, hit.view(-1, 1), sc_l, rc_l, group=group)
+    out = torch.empty_like(back)
+    lib = _capi.load()
+    _check(lib.tbe_route_gather_device(pos.data_ptr(), keys.numel(), back.data_ptr(), 1, out.data_ptr(),
+                                       device_stream(dev)))
+    return out[:, 0].to(torch.uint8)
 
 
 def device_stream(dev) -> int:
@@ -373,9 +503,19 @@ def approx_epoch(engine, counts, ts_us: int, stagger_us: int, mode: str = "clien
         return engine.sync(counts, 1, 0, ts_us, stagger_us)
     if mode == "clients":       # every rank is a client: exact prefix semantics
         allc = torch.empty(world * counts.numel(), dtype=counts.dtype, device=counts.device)
-        dist.all_gather_into_tensor(allc, counts, group=group)
+        _all_gather(allc, counts, group=group)
+        _wait_collective(counts)
         return engine.sync(allc, world, rank, ts_us, stagger_us)
     if mode == "node":          # the node is one client: sum of the ranks' counts
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        _all_reduce_sum(counts, group=group)
+        _wait_collective(counts)
         return engine.sync(counts, 1, 0, ts_us, stagger_us)
     raise ValueError(f"unknown mode {mode!r}")
+
+
+def _wait_collective(t) -> None:
+    """The engine's sync replay reads the exchanged counts on its own stream: wait for the
+    collective on the current stream first."""
+    if _is_cuda(t):
+        import torch
+        torch.cuda.current_stream(t.device).synchronize()

@@ -702,6 +702,12 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 __device__ __forceinline__ void lds_dma16(const void *src, void *lds_wave) {
     __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)lds_wave, 16, 0, 2);
 }
+// LDS-DMA loads count against vmcnt, not lgkmcnt: a workgroup barrier's release fence
+// alone need not wait for them, so every barrier that publishes a DMA'd slice is
+// preceded by this explicit wait for this wave's outstanding vector-memory loads.
+__device__ __forceinline__ void lds_dma_wait() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // A token-bucket reply is {granted, trunc(new_v)} with 0 <= trunc(new_v) <= TokenLimit.
 // When TokenLimit <= 127 it travels as one byte (bit 7 granted, bits 0-6 remaining)
@@ -879,6 +885,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         for (uint32_t j = tid; j < R; j += kWideBlock) own[j] = 0;
         if (count_hot && c == s)
             for (uint32_t j = tid; j < R; j += kWideBlock) hcnt[j] = 0;
+        lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
         if (count_hot) {
 #pragma unroll
@@ -1257,6 +1264,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
         for (uint32_t j = tid; j < R; j += kTbBlock) own[j] = 0;
         if (count_hot && c == s)
             for (uint32_t j = tid; j < R; j += kTbBlock) hcnt[j] = 0;
+        lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
         if (count_hot) {
 #pragma unroll
@@ -2018,6 +2026,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
+    lds_dma_wait();    // this wave's slice and header DMA landed
     __syncthreads();
 
     for (uint32_t c = s; c < e; c += kQChunk) {
@@ -2433,6 +2442,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
             const uint32_t q = c + r * kFoldBlock + tid;
             return PACKED ? (uint32_t)(srec[q] >> (F.kb + F.pb + 1)) : sidx[q];
         };
+        lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();
         uint32_t mine = 0;
 #pragma unroll
@@ -3265,9 +3275,15 @@ static tbe_status create_fail(tbe_status st, const char *msg) {
 tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     if (!out_engine) return create_fail(TBE_EINVAL, "out_engine is NULL");
     *out_engine = nullptr;
-    if (!config || config->struct_size < sizeof(tbe_config))
+    // struct_size versions the config: a caller built against the round-1 header (which
+    // ended at max_batch) passes the shorter size, and the fields it lacks read as 0.
+    constexpr size_t kConfigV1 = offsetof(tbe_config, zero_wait_slots);
+    if (!config || config->struct_size < kConfigV1)
         return create_fail(TBE_EINVAL, "config is NULL or struct_size too small");
-    const tbe_config &c = *config;
+    tbe_config c_in;
+    std::memset(&c_in, 0, sizeof c_in);
+    std::memcpy(&c_in, config, std::min<size_t>(config->struct_size, sizeof c_in));
+    const tbe_config &c = c_in;
     if (c.kind != TBE_KIND_TOKEN_BUCKET && c.kind != TBE_KIND_QUEUEING &&
         c.kind != TBE_KIND_APPROXIMATE)
         return create_fail(TBE_EINVAL, "unknown kind");

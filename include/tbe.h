@@ -53,7 +53,10 @@ typedef enum tbe_kind {
  * (Configuration, ConfigurationOptions, ConnectionMultiplexerFactory, TBO:48-60) and
  * the ProfilingSession (TBO:70) have no counterpart: the "connection" is the device. */
 typedef struct tbe_config {
-    uint32_t struct_size;                 /* sizeof(tbe_config) */
+    uint32_t struct_size;                 /* sizeof(tbe_config); sizes down to
+                                             offsetof(tbe_config, zero_wait_slots) (the first
+                                             published layout) are accepted, and the fields
+                                             past struct_size read as 0 */
     int32_t kind;                         /* tbe_kind */
     uint64_t n_keys;                      /* table capacity, 1 <= n_keys <= 2^32 */
     int32_t token_limit;                  /* TokenLimit (TBO:43), > 0 */

@@ -45,6 +45,19 @@ int tbe_key_text_lengths_device(const uint64_t *d_keys, uint64_t n, uint32_t pre
 int tbe_key_text_device(const uint64_t *d_keys, uint64_t n, const char *prefix, uint32_t prefix_len,
                         const uint64_t *d_offs, uint8_t *d_bytes, void *stream);
 
+/* Profiling marker: enqueues one empty dispatch named k_mark<tag> (tag 1 or 2), so that a
+ * rocprofv3 trace can keep exactly the dispatches enqueued between two markers (the
+ * benchmark's timed batches).  Returns 0 on success. */
+int tbe_mark_device(uint32_t tag, void *stream);
+
+/* HBM-counter calibration (k_calib<mode>): reads or writes a known byte count with one
+ * access shape -- 0/1/2 streaming reads of 16/8/4 B per lane, 3/4/5 gathers of 16/8/4 B
+ * per lane at hashed 128-byte lines, 6/7 streaming writes of 16/4 B per lane, 8/9
+ * scatters of 16/1 B per lane -- over n elements of the `bytes`-byte buffer d_buf
+ * (bytes a multiple of 128; streams need n * width <= bytes).  d_sink: one u64 of device
+ * memory.  Returns 0 on success. */
+int tbe_calib_device(uint32_t mode, uint8_t *d_buf, uint64_t bytes, uint64_t n, uint64_t *d_sink, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -194,3 +194,161 @@ def q_route_worker(rank: int, world: int, port: int, out_dir: str):
     np.savez(os.path.join(out_dir, f"q_{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ HIP engines (GPU tests)
+# The same three protocols with this rank's decisions made by the HIP engine (libtbe.so)
+# on cuda:0: the GPU test starts two such ranks on the one GPU of its box, over gloo (RCCL
+# refuses two ranks on one device).  path "host": numpy batches, HostDirectory, the
+# engine's host-buffer calls; path "device": CUDA tensors end to end -- route kernels,
+# DeviceDirectory, device-buffer engine calls -- with gloo's collectives staged through
+# host memory by cluster.py.
+def _hip_setup():
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)     # the device path refuses the NULL stream
+    torch.cuda.set_stream(stream)
+    return torch, dev, stream
+
+
+def _owned_keys(batch_fn, steps: int, rank: int, world: int) -> np.ndarray:
+    """Every key this rank owns among all ranks' batches (each rank can compute them)."""
+    from distributedratelimiting.redis_amd import cluster
+    keys = np.unique(np.concatenate([batch_fn(r, s)[0] for r in range(world) for s in range(steps)]))
+    return keys[cluster.key_owner(keys, world) == rank].astype(np.uint64)
+
+
+def _dir_ids(directory, keys: np.ndarray, torch, dev) -> np.ndarray:
+    from distributedratelimiting.redis_amd import cluster
+    if isinstance(directory, cluster.DeviceDirectory):
+        return directory.lookup(torch.from_numpy(keys.view(np.int64)).to(dev)).cpu().numpy().view(np.uint64)
+    return directory.lookup(keys)
+
+
+def tb_route_worker_hip(rank: int, world: int, port: int, out_dir: str, path: str):
+    dist = _init(rank, world, port)
+    torch, dev, stream = _hip_setup()
+    from distributedratelimiting.redis_amd import TokenBucketEngine, cluster
+
+    cap = cluster.keys_per_rank(TB["n_keys"], world)
+    eng = TokenBucketEngine(cap, TB["token_limit"], TB["tokens_per_period"], TB["period_ticks"], device=0)
+    out = {}
+    if path == "device":
+        directory = cluster.DeviceDirectory(cap, device=0)
+
+        def decide(lk, lp, lt):
+            g = torch.empty(lk.numel(), dtype=torch.uint8, device=dev)
+            r = torch.empty(lk.numel(), dtype=torch.int32, device=dev)
+            eng.acquire_batch_device(lk, lp, lt, g, r, stream=stream.cuda_stream)
+            return g, r
+        for s in range(TB_STEPS):
+            k, p, t = (torch.from_numpy(np.asarray(x).view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+                       for x in tb_batch(rank, s))
+            g, r = cluster.route_batch(decide, k, p, t, directory)
+            out[f"g{s}"], out[f"r{s}"] = g.cpu().numpy(), r.cpu().numpy()
+    else:
+        directory = cluster.HostDirectory(cap)
+        for s in range(TB_STEPS):
+            k, p, t = tb_batch(rank, s)
+            g, r = cluster.route_batch(lambda lk, lp, lt: eng.acquire_batch(lk, lp, lt), k, p, t, directory)
+            out[f"g{s}"], out[f"r{s}"] = g, r
+    eng.synchronize()
+    v, tt = eng.export_state()
+    out["v"], out["t"] = v, tt
+    owned = _owned_keys(tb_batch, TB_STEPS, rank, world)
+    out["dir_keys"], out["dir_ids"] = owned, _dir_ids(directory, owned, torch, dev)
+    np.savez(os.path.join(out_dir, f"tb_{rank}.npz"), **out)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def q_route_worker_hip(rank: int, world: int, port: int, out_dir: str, path: str):
+    dist = _init(rank, world, port)
+    torch, dev, stream = _hip_setup()
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, cluster
+
+    eng = QueueingTokenBucketEngine(Q["n_keys"], Q["token_limit"], Q["tokens_per_period"], Q["period_ticks"],
+                                    Q["queue_limit"], Q["order"], device=0)
+    next_id = [0]
+    device = path == "device"
+
+    def wait(lk, lp, lt):   # the owner's engine: WaitAsync, ids assigned in arrival order
+        m = lk.shape[0]
+        base = next_id[0]
+        next_id[0] += m
+        if device:
+            st = torch.empty(m, dtype=torch.uint8, device=dev)
+            rem = torch.empty(m, dtype=torch.int32, device=dev)
+            if m:
+                eng.wait_batch_device(lk, lp, lt, st, rem, base, wait=True, stream=stream.cuda_stream)
+            return st, rem, base + torch.arange(m, dtype=torch.int64, device=dev)
+        st, rem, _ = eng.wait_batch(lk, lp, lt, base)
+        return st, rem, base + np.arange(m, dtype=np.int64)
+
+    def cancel(lk, ids):    # host-buffer cancel (tbe_queue_cancel); device inputs staged
+        if device:
+            eng.synchronize()
+            return eng.cancel(lk.cpu().numpy().view(np.uint64), ids.cpu().numpy())
+        return eng.cancel(lk, ids)
+
+    directory = cluster.DeviceDirectory(Q["n_keys"], device=0) if device else cluster.HostDirectory(Q["n_keys"])
+    out = {}
+    for s in range(Q_STEPS):
+        k, p, t = q_batch(rank, s)
+        if device:
+            kd, pd, td = (torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev) for x in (k, p, t))
+            st, rem, ids = (x.cpu().numpy() for x in cluster.route_batch(wait, kd, pd, td, directory))
+        else:
+            st, rem, ids = cluster.route_batch(wait, k, p, t, directory)
+        pick = q_cancel_pick(st)
+        if device:
+            hit = cluster.route_cancel(cancel, torch.from_numpy(k[pick].view(np.int64)).to(dev),
+                                       torch.from_numpy(ids[pick].astype(np.int64)).to(dev), directory).cpu().numpy()
+        else:
+            hit = cluster.route_cancel(cancel, k[pick], ids[pick], directory)
+        lk, li, lr = eng.refresh(q_refresh_ts(s))
+        out[f"st{s}"], out[f"rem{s}"], out[f"ids{s}"], out[f"hit{s}"] = st, rem, ids, hit
+        out[f"log{s}"] = np.stack([lk.astype(np.int64), li, lr.astype(np.int64)], axis=1).reshape(-1, 3)
+    owned = _owned_keys(q_batch, Q_STEPS, rank, world)
+    out["dir_keys"], out["dir_ids"] = owned, _dir_ids(directory, owned, torch, dev)
+    np.savez(os.path.join(out_dir, f"q_{rank}.npz"), **out)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def ap_epoch_worker_hip(rank: int, world: int, port: int, out_dir: str, mode: str):
+    dist = _init(rank, world, port)
+    torch, dev, stream = _hip_setup()
+    from distributedratelimiting.redis_amd import ApproximateEngine, cluster
+
+    eng = ApproximateEngine(AP["n_keys"], AP["token_limit"], AP["tokens_per_period"], AP["period_ticks"],
+                            AP["queue_limit"], AP["order"], device=0)
+    statuses, logs = [], []
+    rid = 0
+    for e in range(AP_EPOCHS):
+        keys, permits = ap_batch(rank, e)
+        st, _, _ = eng.acquire_batch(keys, permits, wait=True, id_base=rid)
+        statuses.extend(st.tolist())
+        rid += keys.shape[0]
+        counts = torch.zeros(AP["n_keys"], dtype=torch.int32, device=dev)
+        lk, li, _ = cluster.approx_epoch(eng, counts, ap_epoch_ts(e), AP_STAGGER, mode=mode)
+        logs.append(list(zip(lk.tolist(), li.tolist())))
+    # [local, global, est, queued permits (_queueCount)] per key, as the oracle client's
+    state = np.array([[lo, gl, est, sum(p for _, p in eng.queue_of(k))] for k, (lo, gl, est, _, _) in
+                      enumerate(eng.local_state(k) for k in range(AP["n_keys"]))], dtype=np.float64)
+    np.savez(os.path.join(out_dir, f"ap_{mode}_{rank}.npz"), status=np.array(statuses),
+             log=np.array([(e, k, r) for e, lg in enumerate(logs) for k, r in lg],
+                          dtype=np.int64).reshape(-1, 3),
+             state=state)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    # python tests/_dist_workers.py <worker> <rank> <world> <port> <out_dir> [arg]
+    fn = globals()[sys.argv[1]]
+    fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), *sys.argv[5:])

@@ -48,3 +48,40 @@ def test_algorithmic_bytes_model():
     assert abs(fold1 - (n * 9 + u * 32)) < n            # records 8 + reply 1, rows 32 per key
     # the decision's own minimum is <= 48.3 B per request at config B
     assert (n * 25 + u * 32) / n < 48.4
+
+
+def _bench(argv, env_extra=None, timeout=240):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_n_refuses_without_n_devices():
+    """--gpus 2 outside torchrun launches 2 ranks only if 2 GPUs are visible; here (no
+    GPU) it must exit non-zero instead of printing a one-rank line."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("GPUs visible")
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert p.returncode != 0 and not p.stdout.strip()
+    assert "--gpus 2 but only" in p.stderr
+
+
+def test_world_size_mismatch_refuses():
+    p = _bench(["--gpus", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and not p.stdout.strip()
+    assert "world size 2 != --gpus 1" in p.stderr
+
+
+def test_gpus_n_spawns_n_ranks():
+    """--share-device skips the device count, so the launcher starts torch.distributed.run
+    with 2 ranks: both report in (then fail without a GPU, and the launcher's exit status
+    is non-zero, with no line printed)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible: the spawned ranks would run the benchmark")
+    p = _bench(["--gpus", "2", "--share-device", "--steps", "1", "--warmup", "0"])
+    assert p.returncode != 0 and not p.stdout.strip()
+    assert "bench.py: rank 0 of 2" in p.stderr and "bench.py: rank 1 of 2" in p.stderr

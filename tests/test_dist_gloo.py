@@ -58,11 +58,14 @@ def test_key_owner_and_directory():
 
 
 def test_route_batch_matches_serial_reference(oracle_lib, tmp_path):
+    _spawn(W.tb_route_worker, str(tmp_path))
+    check_tb_route([np.load(tmp_path / f"tb_{r}.npz") for r in range(WORLD)])
+
+
+def check_tb_route(res):
+    """Expected: one serial table; per step rank 0's batch, then rank 1's."""
     from oracle import cref
     from oracle.semantics import fill_rate_per_second
-    _spawn(W.tb_route_worker, str(tmp_path))
-    res = [np.load(tmp_path / f"tb_{r}.npz") for r in range(WORLD)]
-
     rate = fill_rate_per_second(W.TB["tokens_per_period"], W.TB["period_ticks"])
     ref = cref.CTokenBucket(W.TB["n_keys"], W.TB["token_limit"], rate)
     for s in range(W.TB_STEPS):
@@ -90,10 +93,15 @@ def test_route_batch_matches_serial_reference(oracle_lib, tmp_path):
 
 
 def test_approx_epoch_clients_matches_multi_client_reference(tmp_path):
-    from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
     _spawn(W.ap_epoch_worker, str(tmp_path), "clients")
-    res = [np.load(tmp_path / f"ap_clients_{r}.npz") for r in range(WORLD)]
+    check_approx([np.load(tmp_path / f"ap_clients_{r}.npz") for r in range(WORLD)], "clients")
 
+
+def check_approx(res, mode):
+    """Expected: the single-process multi-client reference.  clients: client r syncs at
+    T + r*stagger and sees clients < r (approx_refresh_all); node: the ranks' counts
+    summed into ONE sync call per key, whose reply every rank applies."""
+    from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
     A = W.AP
     clients = [ApproxClient(A["token_limit"], A["tokens_per_period"], A["period_ticks"],
                             A["queue_limit"], A["order"]) for _ in range(WORLD)]
@@ -110,7 +118,15 @@ def test_approx_epoch_clients_matches_multi_client_reference(tmp_path):
             for k, p in zip(keys.tolist(), permits.tolist()):
                 statuses[r].append(clients[r].wait(k, p, rids[r])[0])
                 rids[r] += 1
-        lg = approx_refresh_all(clients, table, W.ap_epoch_ts(e), W.AP_STAGGER, range(A["n_keys"]))
+        if mode == "clients":
+            lg = approx_refresh_all(clients, table, W.ap_epoch_ts(e), W.AP_STAGGER, range(A["n_keys"]))
+        else:
+            counts = [c.collect() for c in clients]
+            for k in range(A["n_keys"]):
+                g, period, _ = table.sync(f"approx:{k}", sum(c.get(k, 0) for c in counts), W.ap_epoch_ts(e))
+                for c in clients:
+                    c.apply_sync(k, g, period)
+            lg = [c.drain() for c in clients]
         for r in range(WORLD):
             logs[r].extend((e, k, i) for k, i in lg[r])
     for r in range(WORLD):
@@ -130,17 +146,20 @@ def test_approx_epoch_node_mode_sums_counts(tmp_path):
     res = [np.load(tmp_path / f"ap_node_{r}.npz") for r in range(WORLD)]
     # both ranks replay identical sync calls -> identical global scores and estimates
     assert np.array_equal(res[0]["state"][:, 1:3], res[1]["state"][:, 1:3])
-    assert res[0]["state"][:, 1].max() > 0
+    check_approx(res, "node")
 
 
 def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
     """Queued waits routed to their owners, then cancels of some of them routed the same
     way (cluster.route_cancel), then a replenish tick on every rank.  Expected = one
     serial queueing table: per step rank 0's batch, rank 1's, the cancels, the tick."""
+    _spawn(W.q_route_worker, str(tmp_path))
+    check_q_route([np.load(tmp_path / f"q_{r}.npz") for r in range(WORLD)])
+
+
+def check_q_route(res):
     from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
     from distributedratelimiting.redis_amd import cluster
-    _spawn(W.q_route_worker, str(tmp_path))
-    res = [np.load(tmp_path / f"q_{r}.npz") for r in range(WORLD)]
     Q = W.Q
     ref = QueueingTokenBucketTable(TokenBucketConfig.from_options(
         Q["token_limit"], Q["tokens_per_period"], Q["period_ticks"]), Q["queue_limit"], Q["order"])

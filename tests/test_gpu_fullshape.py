@@ -128,8 +128,27 @@ def test_config_c_slice_full_shape(engine_lib, gpu):
     log("config C slice: 1.25e8-row table identical")
 
 
+def check_drain_log(b, m, lk, li, lr, ref_log):
+    """A device drain log (key << 16 | drain position, request id, remaining; grouped
+    arbitrarily across keys) against the C restatement's (key, drain) order."""
+    ks = lk[:m].cpu().numpy().view(np.uint64)
+    o = np.argsort(ks, kind="stable")
+    lk_ref, li_ref, lr_ref = ref_log
+    assert m == lk_ref.size, (b, m, lk_ref.size)
+    assert np.array_equal(ks[o] >> np.uint64(16), lk_ref)
+    assert np.array_equal(li[:m].cpu().numpy()[o], li_ref)
+    assert np.array_equal(lr[:m].cpu().numpy()[o], lr_ref)
+
+
 @pytest.mark.timeout(900)
 def test_config_d_full_shape(engine_lib, gpu):
+    """Config D as bench.py runs it: five 1 ms batches, each with its replenish tick
+    fused into the fold (tbe_wait_batch_tick_device) -- at 1 token/s those ticks find no
+    token for a saturated key -- then ticks that grant: standalone ticks
+    (tbe_refresh_device) one second apart, each of which completes the head entry of
+    every queue (Q:237-271), and a sixth batch whose fused tick also drains.  Statuses,
+    remaining, every drain-log entry, the table and sampled queues against the C
+    restatement (wait + refresh, tbrq_*)."""
     import torch
     from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, _capi, fill_rate
     lib = _capi.load()
@@ -143,42 +162,52 @@ def test_config_d_full_shape(engine_lib, gpu):
     rem = torch.empty(n, dtype=torch.int32, device=gpu)
     stream = torch.cuda.Stream(gpu)
     sh = stream.cuda_stream
+    cap = n_keys * min(ql, tl)            # tbe_refresh_bound's ceiling: every key, min(QL, TL) grants
+    lk = torch.empty(cap, dtype=torch.int64, device=gpu)
+    li = torch.empty(cap, dtype=torch.int64, device=gpu)
+    lr = torch.empty(cap, dtype=torch.int32, device=gpu)
+    cnt = torch.empty(1, dtype=torch.int32, device=gpu)   # zeroed by the tick on its stream
     total_queued = 0
-    for b in range(batches):
-        assert lib.tbe_gen_batch_device(0x5EED000D, n_keys, b * n, n, 1, 1, T0_US + b * interval, interval,
+    drained = []
+
+    def batch(b, ts0, tick):
+        assert lib.tbe_gen_batch_device(0x5EED000D, n_keys, b * n, n, 1, 1, ts0, interval,
                                         k.data_ptr(), p.data_ptr(), t.data_ptr(), None) == 0
         torch.cuda.synchronize()
-        eng.wait_batch_device(k, p, t, st, rem, id_base=b * n, stream=sh)
-        cap = max(1, eng.refresh_bound())
-        lk = torch.empty(cap, dtype=torch.int64, device=gpu)
-        li = torch.empty(cap, dtype=torch.int64, device=gpu)
-        lr = torch.empty(cap, dtype=torch.int32, device=gpu)
-        cnt = torch.empty(1, dtype=torch.int32, device=gpu)   # zeroed by the tick on its stream
-        tick = T0_US + (b + 1) * interval
-        eng.refresh_device(tick, lk, li, lr, cnt, stream=sh)
+        eng.wait_batch_tick_device(k, p, t, st, rem, b * n, tick, lk, li, lr, cnt, stream=sh)
         stream.synchronize()
         hk, hp, ht = cref.gen_batch(0x5EED000D, n_keys, b, n, interval)
+        ht = ht - (T0_US + b * interval) + ts0
         s_ref, r_ref, ev_c, _ = ref.acquire_batch(hk, hp, ht, b * n, threads=THREADS)
         assert ev_c.size == 0                                    # OldestFirst never evicts
         assert_replies(b, st.cpu().numpy(), rem.cpu().numpy(), s_ref, r_ref)
         m = int(cnt.item())
-        ks = lk[:m].cpu().numpy().view(np.uint64)
-        o = np.argsort(ks, kind="stable")
-        lk_ref, li_ref, lr_ref = ref.refresh(tick, threads=THREADS)
-        assert m == lk_ref.size, (m, lk_ref.size)
-        assert np.array_equal(ks[o] >> np.uint64(16), lk_ref)
-        assert np.array_equal(li[:m].cpu().numpy()[o], li_ref)
-        assert np.array_equal(lr[:m].cpu().numpy()[o], lr_ref)
-        total_queued += int((s_ref == 2).sum())
+        check_drain_log(b, m, lk, li, lr, ref.refresh(tick, threads=THREADS))
+        drained.append(m)
         log(f"config D batch {b}: {n} statuses identical ({int((s_ref == 1).sum())} granted, "
-            f"{int((s_ref == 2).sum())} queued, {int((s_ref == 0).sum())} failed); tick drained {m}")
+            f"{int((s_ref == 2).sum())} queued, {int((s_ref == 0).sum())} failed); fused tick drained {m}")
+        return int((s_ref == 2).sum())
+
+    for b in range(batches):
+        total_queued += batch(b, T0_US + b * interval, T0_US + (b + 1) * interval)
     assert total_queued > 0
+    # ticks that grant: a saturated key gains one token per second at 1 token/s
+    for j in range(1, 4):
+        tick = T0_US + j * 1_000_000
+        eng.refresh_device(tick, lk, li, lr, cnt, stream=sh)
+        stream.synchronize()
+        m = int(cnt.item())
+        check_drain_log(f"tick {j}", m, lk, li, lr, ref.refresh(tick, threads=THREADS))
+        drained.append(m)
+        log(f"config D standalone tick at T+{j} s: {m} queued entries completed, log identical")
+    total_queued += batch(batches, T0_US + 4_000_000, T0_US + 5_000_000)
+    assert min(drained[batches:]) > 1_000_000, drained          # the granting ticks drain millions
     v, t_us = eng.export_state()
     assert_same_table(v, t_us, *ref.bucket_state())
     rng = np.random.default_rng(4)
     for key in rng.integers(0, n_keys, 3000).tolist():
         assert eng.queue_of(key) == ref.queue_of(key)
-    log("config D: bucket table identical, 3000 sampled queues identical")
+    log(f"config D: {sum(drained)} drained entries, bucket table and 3000 sampled queues identical")
 
 
 @pytest.mark.timeout(900)
@@ -196,6 +225,31 @@ def test_config_e_full_shape_two_clients(engine_lib, gpu):
     ticks = interval * 10
     engs = [ApproximateEngine(kshared, tl, tpp, ticks, 0, 0, device=0, max_batch=n) for _ in range(clients)]
     refs = [cref.CApprox(kshared, tl, tpp, ticks, 0, 0, 4) for _ in range(clients)]
+    run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait=False)
+
+
+@pytest.mark.timeout(900)
+def test_config_e_full_shape_queued_waits(engine_lib, gpu):
+    """Config E's shape with QueueLimit 16 and WaitAsync (wait = 1): requests the local
+    tier cannot lease queue (A:116-183), and every refresh epoch drains the queues in
+    order while AvailableTokens covers the head (A:467-501) -- statuses, the drain logs,
+    the global-tier replica and sampled local tiers against the C restatement."""
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    kshared, n, tl, tpp, interval, clients, epochs, ql = 10_000_000, 1 << 26, 100, 10, 10_000, 2, 3, 16
+    ticks = interval * 10
+    engs = [ApproximateEngine(kshared, tl, tpp, ticks, ql, 0, device=0, max_batch=n) for _ in range(clients)]
+    refs = [cref.CApprox(kshared, tl, tpp, ticks, ql, 0, 4) for _ in range(clients)]
+    drained, queued = run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait=True)
+    assert queued > 1_000_000 and drained > 1_000_000, (queued, drained)
+
+
+def run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait):
+    """Epochs of 2^26 requests per client, then collect -> the all-gather's layout ->
+    client-ordered sync replay with staggered timestamps; returns (drained, queued)."""
+    import torch
+    from distributedratelimiting.redis_amd import _capi
+    lib = _capi.load()
+    clients = len(engs)
     k = torch.empty(n, dtype=torch.int64, device=gpu)
     p = torch.empty(n, dtype=torch.int32, device=gpu)
     t = torch.empty(n, dtype=torch.int64, device=gpu)
@@ -203,19 +257,22 @@ def test_config_e_full_shape_two_clients(engine_lib, gpu):
     av = torch.empty(n, dtype=torch.int32, device=gpu)
     counts = [torch.empty(kshared, dtype=torch.int32, device=gpu) for _ in range(clients)]
     stagger = (ticks // 10) // clients
+    drained = queued = 0
     for e in range(epochs):
         for r in range(clients):
             seed = 0x5EED000E + 7919 * r
             assert lib.tbe_gen_batch_device(seed, kshared, e * n, n, 1, 1, T0_US + e * interval, interval,
                                             k.data_ptr(), p.data_ptr(), t.data_ptr(), None) == 0
             torch.cuda.synchronize()
-            engs[r].acquire_batch_device(k, p, st, av, wait=False, id_base=e * n)
+            engs[r].acquire_batch_device(k, p, st, av, wait=wait, id_base=e * n)
             engs[r].synchronize()
             hk = k.cpu().numpy().view(np.uint64)
-            s_ref, a_ref, _, _ = refs[r].acquire_batch(hk, np.ones(n, np.int32), wait=False, id_base=e * n,
+            s_ref, a_ref, _, _ = refs[r].acquire_batch(hk, np.ones(n, np.int32), wait=wait, id_base=e * n,
                                                        threads=THREADS)
             assert_replies(e * clients + r, st.cpu().numpy(), av.cpu().numpy(), s_ref, a_ref)
-            log(f"config E epoch {e} client {r}: {n} statuses identical (granted {s_ref.mean():.4f})")
+            queued += int((s_ref == 2).sum())
+            log(f"config E epoch {e} client {r}: {n} statuses identical (granted {(s_ref == 1).mean():.4f}, "
+                f"queued {int((s_ref == 2).sum())})")
         for r in range(clients):
             engs[r].collect(counts[r])
         allc = torch.cat(counts)
@@ -223,9 +280,13 @@ def test_config_e_full_shape_two_clients(engine_lib, gpu):
         assert np.array_equal(allc.cpu().numpy(), allc_h)
         ts = T0_US + (e + 1) * interval
         for r in range(clients):
-            dk, _, _ = engs[r].sync(allc, clients, r, ts, stagger)
-            rk, _, _ = refs[r].sync(allc_h, clients, r, ts, stagger, threads=THREADS)
-            assert dk.size == rk.size == 0                  # QueueLimit 0: nothing queued
+            got = engs[r].sync(allc, clients, r, ts, stagger)
+            exp = refs[r].sync(allc_h, clients, r, ts, stagger, threads=THREADS)
+            for a, b in zip(got, exp):                       # (key, request id, available) in key order
+                assert np.array_equal(a, b)
+            drained += got[0].size
+            if not wait:
+                assert got[0].size == 0                      # QueueLimit 0: nothing queued
         x = refs[0].export()
         v, pp, tt = engs[0].export_global()
         for a, b in ((v, x["v"]), (pp, x["p"]), (tt, x["t_us"])):
@@ -236,4 +297,8 @@ def test_config_e_full_shape_two_clients(engine_lib, gpu):
                 lo, gl, est, a, q = engs[r].local_state(key)
                 assert (lo, gl, est, a, q) == (x["local"][key], x["global"][key], x["est"][key],
                                                x["available"][key], x["queued"][key])
-        log(f"config E epoch {e}: global tier replica (1e7 keys) and sampled local tiers identical")
+                if wait and key % 10 == 0:
+                    assert engs[r].queue_of(key) == refs[r].queue_of(key)
+        log(f"config E epoch {e}: global tier replica (1e7 keys) and sampled local tiers identical "
+            f"({drained} queued requests drained so far)")
+    return drained, queued
