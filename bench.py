@@ -213,16 +213,19 @@ def main():
     seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B)
     directory = cluster.DeviceDirectory(keys_local, device=dev.index) if routed else None
     bufs, raw = [], []
+    # generate on the current stream: the routing kernels run on it too (a torch stream does
+    # not wait for the legacy NULL stream)
+    gen_stream = torch.cuda.current_stream(dev).cuda_stream or None
     for s in range(total_steps):
         g0 = (s * world + rank) * n          # this rank's share of the global stream
         k = torch.empty(n, dtype=torch.int64, device=dev)
         p = torch.empty(n, dtype=torch.int32, device=dev)
         t = torch.empty(n, dtype=torch.int64, device=dev)
         rc = lib.tbe_gen_batch_device(seed, keys_total, g0, n, 1, 1, T0_US + s * args.interval_us,
-                                      args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), None)
+                                      args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), gen_stream)
         assert rc == 0
         if args.workload == "zipf":
-            assert lib.tbe_gen_zipf_keys_device(seed, keys_total, args.zipf_s, g0, n, k.data_ptr(), None) == 0
+            assert lib.tbe_gen_zipf_keys_device(seed, keys_total, args.zipf_s, g0, n, k.data_ptr(), gen_stream) == 0
         if routed and args.route == "pre":
             (lk, lp, lt), _ = cluster.route_requests(k, p, t, directory)
             bufs.append((lk, lp, lt))

@@ -184,11 +184,10 @@ class DeviceDirectory:
         return ids
 
     def assign(self, d_keys):
-        """int64 device tensor of keys -> int64 device tensor of ids (assigning new ones).
-        Raises TbeError(TBE_ERANGE) if the batch overflowed the directory."""
+        """int64 device tensor of keys -> int64 device tensor of ids (assigning new ones;
+        keys beyond capacity get -1, and check() raises from then on)."""
         ids = self._run(self._lib.tbe_dir_assign_device, d_keys)
         self._bound += d_keys.numel()
-        self.check()
         return ids
 
     def lookup(self, d_keys):
@@ -276,6 +275,7 @@ def route_requests(keys, permits, ts_us, directory, group=None):
         keys, permits, ts_us = _device_columns(keys, (permits, torch.int32), (ts_us, torch.int64))
         pos, sc_l, rc_l, recv = _route_device(keys, permits, ts_us, world, group)
         local = directory.assign(recv[:, 0])
+        directory.check()        # an over-capacity batch raises before anything is decided
         return (local, recv[:, 2].to(torch.int32), recv[:, 1].contiguous()), RoutePlan(pos, sc_l, rc_l, keys.numel())
     keys = np.asarray(keys, dtype=np.uint64)
     n = keys.shape[0]

@@ -67,3 +67,12 @@ def test_fill_rate_matches_oracle(engine_lib):
 def test_gpu_code_object_targets_gfx950(engine_lib):
     blob = open(engine_lib, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_integration_binds_every_engine_entry_point():
+    """INTEGRATION.md's C# binding (the reference-side P/Invoke a maintainer adds) has a
+    LibraryImport for every function include/tbe.h declares."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    bound = set(re.findall(r'EntryPoint = "(tbe_\w+)"', doc))
+    missing = [n for n in declared_functions(HEADERS[:1]) if n not in bound]
+    assert not missing, missing

@@ -96,6 +96,80 @@ def _directory_matches_host(gpu):
         small.size()
 
 
+def cluster_error():
+    from distributedratelimiting.redis_amd import TbeError
+    return TbeError
+
+
+def test_route_cancel_device_world1(engine_lib, gpu):
+    """Queued waits routed through the device path and canceled through route_cancel with
+    a DeviceDirectory (RCCL, world size 1) against the Python restatement."""
+    import torch
+    import torch.distributed as dist
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, cluster
+    from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    side = torch.cuda.Stream(gpu)
+    try:
+        torch.cuda.set_stream(side)
+        n_keys, tl, ql = 64, 3, 5
+        eng = QueueingTokenBucketEngine(n_keys, tl, 1, 10_000_000, ql, 0, device=0)
+        dd = cluster.DeviceDirectory(n_keys, device=0)
+        hd = cluster.HostDirectory(n_keys)
+        ref = QueueingTokenBucketTable(TokenBucketConfig.from_options(tl, 1, 10_000_000), ql, 0)
+        rng = np.random.default_rng(5)
+        next_id = [0]
+
+        def wait(lk, lp, lt):
+            m = lk.numel()
+            st = torch.empty(m, dtype=torch.uint8, device=gpu)
+            rem = torch.empty(m, dtype=torch.int32, device=gpu)
+            eng.wait_batch_device(lk, lp, lt, st, rem, next_id[0], stream=side.cuda_stream)
+            ids = next_id[0] + torch.arange(m, dtype=torch.int64, device=gpu)
+            next_id[0] += m
+            return st, rem, ids
+
+        def cancel(lk, ids):
+            assert lk.is_cuda and ids.is_cuda
+            eng.synchronize()
+            return eng.cancel(lk.cpu().numpy().view(np.uint64), ids.cpu().numpy())
+
+        hits = 0
+        for b in range(3):
+            n = 400
+            k = (rng.integers(0, 40, n) * 7919 + 11).astype(np.uint64)
+            p = rng.choice([1, 1, 2, 3], n).astype(np.int32)
+            t = (1_760_000_000_000_000 + b * 600_000 + np.sort(rng.integers(0, 1000, n))).astype(np.int64)
+            st, rem, ids = cluster.route_batch(wait, torch.from_numpy(k.view(np.int64)).to(gpu),
+                                               torch.from_numpy(p).to(gpu), torch.from_numpy(t).to(gpu), dd)
+            hk = hd.assign(k)
+            base = b * n
+            exp = [ref.acquire(int(hk[i]), int(p[i]), int(t[i]), base + i) for i in range(n)]
+            assert st.cpu().numpy().tolist() == [e[0] for e in exp], b
+            assert rem.cpu().numpy().tolist() == [e[1] for e in exp], b
+            assert ids.cpu().numpy().tolist() == list(range(base, base + n))
+            pick = np.array([i for i in range(n) if i % 3 == 0 or i % 41 == 7])
+            hit = cluster.route_cancel(cancel, torch.from_numpy(k[pick].view(np.int64)).to(gpu),
+                                       ids[torch.from_numpy(pick).to(gpu)], dd)
+            want = [int(ref.cancel(int(hk[i]), base + int(i))) for i in pick]
+            assert hit.cpu().numpy().tolist() == want, b
+            hits += sum(want)
+            lk, li, lr = eng.refresh(1_760_000_000_000_000 + b * 600_000 + 500_000)
+            exp_log = ref.refresh(1_760_000_000_000_000 + b * 600_000 + 500_000)
+            assert list(zip(lk.tolist(), li.tolist(), lr.tolist())) == [tuple(e) for e in exp_log], b
+        assert hits > 0
+        with pytest.raises(TypeError):    # a DeviceDirectory takes device tensors only
+            cluster.route_cancel(cancel, np.zeros(2, np.uint64), np.zeros(2, np.int64), dd)
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(gpu))
+        dist.destroy_process_group()
+
+
 def test_route_batch_device_world1(engine_lib, gpu):
     """route_batch's device path (route kernels + RCCL all-to-all + directory + the HIP
     engine) at world size 1, against the C restatement on the directory's dense ids."""
@@ -135,6 +209,23 @@ def test_route_batch_device_world1(engine_lib, gpu):
             assert not hd.overflow
             g_ref, r_ref = ref.acquire_batch(ids, p, t)
             assert np.array_equal(g.cpu().numpy(), g_ref) and np.array_equal(r.cpu().numpy(), r_ref), b
+        # int64 permits (the host API's natural type) are converted, not misread
+        k = (_keys(5000, 77, hot=0.2) % np.uint64(1 << 20)).astype(np.uint64)
+        p = rng.integers(0, 4, 5000)
+        t = (1_760_000_000_000_000 + 3 * 900_000 + np.sort(rng.integers(0, 900_000, 5000))).astype(np.int64)
+        g, r = cluster.route_batch(decide, torch.from_numpy(k.view(np.int64)).to(gpu), torch.from_numpy(p).to(gpu),
+                                   torch.from_numpy(t).to(gpu), dd)
+        g_ref, r_ref = ref.acquire_batch(hd.assign(k), p.astype(np.int32), t)
+        assert np.array_equal(g.cpu().numpy(), g_ref) and np.array_equal(r.cpu().numpy(), r_ref)
+        # a batch bringing more new keys than ids remain raises before any decision
+        small = cluster.DeviceDirectory(1000, device=0)
+        calls = []
+        with pytest.raises(cluster_error()):
+            cluster.route_batch(lambda *a: calls.append(1) or decide(*a),
+                                torch.arange(1500, dtype=torch.int64, device=gpu),
+                                torch.ones(1500, dtype=torch.int32, device=gpu),
+                                torch.full((1500,), 1_760_000_000_000_000, dtype=torch.int64, device=gpu), small)
+        assert not calls
         with pytest.raises(ValueError):                       # the NULL default stream is refused
             torch.cuda.set_stream(torch.cuda.default_stream(gpu))
             cluster.route_batch(decide, torch.zeros(4, dtype=torch.int64, device=gpu),

@@ -388,3 +388,29 @@ def test_hot_key_cools_down(engine_lib, gpu):
         t = trace.batch_timestamps(b, n, 10_000)
         run_and_compare(eng, ref, k, p, t)
         assert_same_state(eng, ref)
+
+
+def test_config_struct_size_versions(engine_lib, gpu):
+    """tbe_create accepts the first published tbe_config layout (struct_size 56, without
+    zero_wait_slots/reserved) and reads the missing fields as 0; smaller sizes are EINVAL."""
+    import ctypes
+    from distributedratelimiting.redis_amd import _capi
+    lib = _capi.load()
+    cfg = _capi.make_config(1000, 5, 1, 10_000_000, device=0)
+    for size, ok in ((ctypes.sizeof(_capi.TbeConfig), True), (56, True), (55, False), (0, False)):
+        cfg.struct_size = size
+        h = ctypes.c_void_p()
+        st = lib.tbe_create(ctypes.byref(cfg), ctypes.byref(h))
+        assert (st == _capi.TBE_OK) == ok, (size, st)
+        if ok:
+            k = np.arange(10, dtype=np.uint64)
+            g = np.empty(10, np.uint8)
+            r = np.empty(10, np.int32)
+            t = np.full(10, 1_760_000_000_000_000, np.int64)
+            p = np.ones(10, np.int32)
+            assert lib.tbe_acquire_batch(h, k.ctypes.data, p.ctypes.data, t.ctypes.data, 10, g.ctypes.data,
+                                         r.ctypes.data) == _capi.TBE_OK
+            assert g.all() and (r == 4).all()
+            lib.tbe_destroy(h)
+        else:
+            assert st == _capi.TBE_EINVAL

@@ -17,7 +17,7 @@ step() {   # step <name> <seconds> <cmd...>
     return 0
 }
 [ "${SKIP_TESTS:-0}" = 1 ] || {
-step pytest_dist 400 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread
+[ "${DIST:-0}" = 1 ] && step pytest_dist 400 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 }
