@@ -298,6 +298,7 @@ def main():
     u_meas = int(torch.unique(last_keys).numel())
     w_meas = int(torch.unique(last_keys[granted[:m_last].bool()]).numel())
     step_alg = int(m_last * 25 + u_meas * 16 + w_meas * 16)
+    uw_note = "U and W measured on the last timed batch"
 
     decisions = n * args.steps * world
     value = decisions / elapsed
@@ -321,12 +322,27 @@ def main():
             ser.acquire_batch_device(*bufs[s], g2[:sizes[s]], r2[:sizes[s]])
         ser.synchronize()
         ser.stage_times()
-        for s in range(args.warmup, total_steps):
-            ser.acquire_batch_device(*bufs[s], g2[:sizes[s]], r2[:sizes[s]])
+        g_all = [torch.empty(sizes[s], dtype=torch.uint8, device=dev) for s in range(args.warmup, total_steps)]
+        for i, s in enumerate(range(args.warmup, total_steps)):
+            ser.acquire_batch_device(*bufs[s], g_all[i], r2[:sizes[s]])
         ser.synchronize()
         stages = ser.stage_times()
-        replay_check = bool(torch.equal(g2[:m_last], granted[:m_last]) and
+        replay_check = bool(torch.equal(g_all[-1][:m_last], granted[:m_last]) and
                             torch.equal(r2[:m_last], remaining[:m_last]))
+        # U and W of every timed batch (the replay's grants equal the timed run's): the
+        # step's B_alg is their mean, not just the last batch's (the table ages from
+        # grant- to denial-dominated across the timed batches)
+        uw = []
+        for i, s in enumerate(range(args.warmup, total_steps)):
+            k = bufs[s][0]
+            uw.append((int(torch.unique(k).numel()), int(torch.unique(k[g_all[i].bool()]).numel())))
+        del g_all
+        u_mean = float(np.mean([u for u, _ in uw]))
+        w_mean = float(np.mean([w for _, w in uw]))
+        step_alg = int(n * 25 + u_mean * 16 + w_mean * 16)
+        uw_note = (f"mean over the {len(uw)} timed batches: U {u_mean:.4g}, W {w_mean:.4g} "
+                   f"(first {uw[0][1]}, last {uw[-1][1]} written keys)")
+        u_meas, w_meas = int(round(u_mean)), int(round(w_mean))
         eng = ser
 
     # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
@@ -337,28 +353,28 @@ def main():
                     "unscatter": passes, "hot": 5}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
-        distinct = None
-        if zkeys:   # distinct keys per batch, measured (the uniform estimate does not apply)
-            distinct = float(np.mean([np.unique(zk).size for zk in zkeys]))
-        own_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], distinct,
-                                      1 if layout.get("narrow") else 4)
-        # achieved: §8(d)'s B_alg of one step (one batch = one launch of the dominant
-        # kernel's stage) over that kernel's launch time; step_frac: over the whole step
-        alg_bytes = step_alg if launches[name] == 1 else step_alg // launches[name]
-        achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+        # the dominant kernel's own algorithmic bytes per launch: the fold
+        # reads its sorted records and the rows of the batch's U distinct keys, writes a
+        # reply per request and the rows of the W keys it modified (U, W measured on the
+        # last timed batch)
+        own_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], u_meas,
+                                      1 if layout.get("narrow") else 4, w_meas)
+        achieved = own_bytes / (per_launch_ms * 1e-3) / 1e9
         step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
+        pmc = pmc_stage(args.workload, name)
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(name, args.workload), "alg_bytes_per_launch": alg_bytes,
-                    "alg_bytes_note": "SURVEY.md §8(d): 25 B per request + 16 B per distinct key read "
-                                      "+ 16 B per distinct key written, U and W measured on the last "
-                                      "timed batch",
+                    "traffic": (round(pmc / launches[name], 1) if pmc is not None else None),
+                    "alg_bytes_per_launch": own_bytes,
+                    "alg_bytes_note": algorithmic_note(name, layout, u_meas, w_meas),
                     "distinct_keys_U": u_meas, "written_keys_W": w_meas,
-                    "step_alg_bytes": step_alg, "step_achieved": round(step_achieved, 1),
+                    "step_alg_bytes": step_alg,
+                    "step_alg_note": "SURVEY.md §8(d) B_alg: 25 B per request + 16 B per distinct key read "
+                                     "+ 16 B per distinct key written; " + uw_note,
+                    "step_achieved": round(step_achieved, 1),
                     "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
                     "step_traffic": pmc_step_traffic(args.workload),
-                    "kernel_own_bytes_per_launch": own_bytes,
-                    "kernel_own_frac": round(own_bytes / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_source": PMC_SOURCE,
                     "avg_launch_ms": round(per_launch_ms, 4),
                     "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
                                "engine stream" if replay_check is not None else
@@ -499,61 +515,68 @@ def bench_strdir(batches, n_keys: int, dev):
 
 
 def algorithmic_bytes(stage: str, n: int, n_keys: int, passes: int, packed: bool,
-                      distinct: float = None, reply: int = 4) -> int:
+                      distinct: float = None, reply: int = 4, written: float = None) -> int:
     """Bytes one launch of `stage` must move at minimum for its function,
     averaged over the passes where a stage runs once per pass.  Packed: the passes and
-    the fold move one 8-byte record per request; wide: {key u32, permits i32, ts i64}."""
+    the fold move one 8-byte record per request; wide: {key u32, permits i32, ts i64}.
+    A pass writes each input element's one-byte digit, its inverse reads it (k_unrank)."""
     rec = 8 if packed else 16
+    u = distinct if distinct is not None else n_keys * (1.0 - np.exp(-n / n_keys))
     if stage == "fold":
-        # sorted records + packed reply (4 bytes, or 1 when TokenLimit <= 127) per request,
-        # plus the table rows of the distinct keys in the batch (16 B read + 16 B written)
-        u = distinct if distinct is not None else n_keys * (1.0 - np.exp(-n / n_keys))
-        return int(n * (rec + reply) + u * 32)
+        # sorted records + reply (4 bytes, or 1 when TokenLimit <= 127) per request; the rows
+        # of the distinct keys read (16 B) and of the keys modified written (16 B)
+        w = written if written is not None else u
+        return int(n * (rec + reply) + u * 16 + w * 16)
     if stage == "scatter":
         # pass 0 reads the caller's key 8 + permits 4 + ts 8, later passes one record;
-        # every pass writes a record and its 4-byte permutation entry
-        return int(n * ((20 + (rec if packed else 16) * (passes - 1)) / passes + rec + 4))
+        # every pass writes a record and its input's one-byte digit
+        return int(n * ((20 + rec * (passes - 1)) / passes + rec + 1))
     if stage == "hist":
         return int(n * (8 + (8 if packed else 4) * (passes - 1)) / passes)
     if stage == "bounds":
         return n * (8 if packed else 4)
     if stage == "unscatter":
-        # perm 4 + gathered reply + written reply (inner passes) or 5 (final: u8 + i32)
-        return int(n * ((4 + 2 * reply) * (passes - 1) + 9 + reply) / passes)
+        # digit 1 + gathered reply + written reply (inner passes) or 5 (final: u8 + i32)
+        return int(n * ((1 + 2 * reply) * (passes - 1) + 1 + reply + 5) / passes)
     return n * 4
 
 
-def pmc_traffic(stage: str, workload: str = "uniform"):
-    """HBM bytes per launch of `stage` in `workload`'s runs, from the committed rocprofv3
-    PMC summary (tools/pmc_all.sh + tools/pmc_summary.py --write), if present."""
+def algorithmic_note(stage: str, layout: dict, u: int, w: int) -> str:
+    r = 1 if layout.get("narrow") else 4
+    rec = 8 if layout.get("packed") else 16
+    if stage == "fold":
+        return (f"fold: n*({rec} record + {r} reply) + 16*U rows read + 16*W rows written "
+                f"(U={u}, W={w}: per-batch mean over the timed batches when the replay ran)")
+    return f"{stage}: DESIGN.md §5 per-launch minimum (bench.algorithmic_bytes)"
+
+
+PMC_SOURCE = ("profiles/pmc_summary.json: rocprofv3 --pmc passes of tools/pmc_passes.sh over bench.py "
+              "--steps 20 --warmup 5, dispatches between the timed-region markers only, bytes by the "
+              "calibrated read/write models")
+
+
+def _pmc_workload(workload: str):
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
+            return json.load(f).get("workloads", {}).get(workload)
     except (OSError, ValueError):
         return None
-    if workload == "uniform":
-        return d.get(stage, {}).get("hbm_bytes_per_launch")
-    prefixes = {"fold": ("k_fold<", "k_fold_wide<"), "scatter": ("k_scatter_rec<",),
-                "hist": ("k_hist<",), "unscatter": ("k_unscatter<",)}.get(stage, ())
-    kern = d.get("workloads", {}).get(workload, {})
-    v = [k["hbm_bytes_per_launch"] for name, k in kern.items()
-         if name.startswith(prefixes) and "hbm_bytes_per_launch" in k]
-    if not v:
-        return None
-    # the fold stage is two launches (summed); other stages one per pass (averaged)
-    return round(sum(v) if stage == "fold" else sum(v) / len(v), 1)
+
+
+def pmc_stage(workload: str, stage: str):
+    """HBM bytes per step of one bench stage (all its kernels' timed launches), from the
+    committed PMC summary, if present."""
+    w = _pmc_workload(workload)
+    st = (w or {}).get("stages", {}).get(stage)
+    return st.get("hbm_bytes_per_step") if st else None
 
 
 def pmc_step_traffic(workload: str = "uniform"):
-    """HBM bytes of one whole step (every kernel of one batch), from the committed PMC
-    summary's per-step total for `workload` (tools/pmc_summary.py --write), if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get("step_hbm_bytes", {}).get(workload)
-    except (OSError, ValueError):
-        return None
+    """HBM bytes of one whole step (every kernel of one timed batch), from the committed
+    PMC summary, if present."""
+    w = _pmc_workload(workload)
+    return round(w["step_hbm_bytes"], 1) if w and "step_hbm_bytes" in w else None
 
 
 def workload_name(args, n: int) -> str:

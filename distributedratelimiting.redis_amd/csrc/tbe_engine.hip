@@ -18,8 +18,8 @@
 //      whose keys differ decide concurrently while requests for the same key go in
 //      rounds, earliest first (LDS atomicMin "owner" election), so per-key order is the
 //      reference's serial order.  Dirty rows are written back once.
-//   4. k_unrank: the P partitions run backwards (each pass's local ranks recomputed from
-//      the one-byte digits it wrote) to return {granted, remaining} in arrival order.
+//   4. k_unscatter: the P partitions run backwards (same local ranks recomputed from the
+//      keys) to return {granted, remaining} in arrival order with coalesced runs.
 //
 // Memory-bound integer/byte work plus a little FP64; no MFMA.
 #include <hip/hip_runtime.h>
@@ -54,6 +54,7 @@ namespace {
 // -DTBE_SLICE_LOAD_CACHED keeps only the slice loads cached (fold 1.17 -> 1.31 ms).
 #ifndef TBE_NO_NT
 #define LD_P(p) ld_nt(p)
+#define ST_PERM(p, v) st_nt((p), (v))
 #define LD_U(p) ld_nt(p)
 #define ST_U(p, v) st_nt((p), (v))
 #ifdef TBE_SLICE_LOAD_CACHED
@@ -64,6 +65,7 @@ namespace {
 #define ST_S(p, v) slot_store_nt((p), (v))
 #else
 #define LD_P(p) (*(p))
+#define ST_PERM(p, v) (*(p) = (v))
 #define LD_U(p) (*(p))
 #define ST_U(p, v) (*(p) = (v))
 #define LD_S(p) (*(p))
@@ -80,6 +82,11 @@ namespace {
 constexpr int kPartBlock = TBE_PART_BLOCK;             // partition workgroup
 constexpr int kPartItems = TBE_PART_ITEMS;             // elements per thread per tile
 constexpr int kTile = kPartBlock * kPartItems;         // 4096 requests per partition tile
+// k_unscatter's own tiles (any size is correct; 8192 keeps each workgroup's gathers in
+// the digit runs of two partition tiles)
+constexpr int kUnBlock = 1024;
+constexpr int kUnItems = 8;
+constexpr int kUnTile = kUnBlock * kUnItems;
 #ifndef TBE_HIST_BLOCKS
 #define TBE_HIST_BLOCKS 1024
 #endif
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
     const uint32_t *__restrict__ iin, uint64_t n, int shift, const uint32_t *__restrict__ tileprefix,
     const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
     uint32_t tiles_per_blk, uint32_t *__restrict__ kout, int32_t *__restrict__ pout,
-    int64_t *__restrict__ tout, uint32_t *__restrict__ iout, uint8_t *__restrict__ dig,
+    int64_t *__restrict__ tout, uint32_t *__restrict__ iout, uint32_t *__restrict__ perm,
     uint32_t *__restrict__ err, int validate) {
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
@@ -397,9 +404,8 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             bad |= validate && (pm[it] < 0 || tv[it] < 0);
             stage[lpos[it]] = ((uint64_t)key[it] << 32) | (uint32_t)pm[it];
-            // input element e's digit: the inverse pass (k_unrank) re-ranks the tile from
-            // these bytes to find where e went
-            dig[base + e] = (uint8_t)d;
+            // where input element e goes: the inverse pass is a plain gather through it
+            perm[base + e] = goff[d] + lpos[it] - L.lstart[d];
         }
     }
     __syncthreads();
@@ -555,7 +561,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
     const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
-    uint8_t *__restrict__ dig, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
+    uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
     uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
     uint32_t *__restrict__ iout = nullptr) {
     __shared__ RankLds<kPartBlock> L;
@@ -617,8 +623,9 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     for (int it = 0; it < kPartItems; ++it) {
         const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
         if (e < nvalid) {
+            const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             stage[lpos[it]] = rec[it];
-            dig[base + e] = (uint8_t)((key[it] >> shift) & (kDigits - 1));   // for k_unrank
+            ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
         }
     }
     __syncthreads();
@@ -1431,14 +1438,8 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     }
 }
 
-// Inverse of one partition pass (k_unrank, below): out[i] = in[pos(i)], pos(i) the
-// position the pass wrote input element i to.  The pass keeps no permutation: it writes
-// each input element's digit (one byte, input order), and the inverse re-ranks the same
-// tile from those bytes -- the stable rank of an element among the tile's elements of
-// its digit depends on the digits alone, whichever ranking order the pass used -- and
-// adds the pass's own histogram offsets: pos = goff[d] + lpos - lstart[d].  One byte per
-// element read instead of a 4-byte permutation entry (and one written by the pass
-// instead of four); the gathers read each tile's digit runs, ~16 consecutive positions.
+// Inverse of one k_scatter pass: out[i] = in[perm[i]] with perm the positions that pass
+// wrote (runs of ~32 consecutive positions per digit and tile, so the gather coalesces).
 // FINAL: unpack into granted/status (u8) and remaining (i32) in arrival order.
 // WAIT: queueing-kind reply packing (see pack_wait).
 constexpr uint32_t kRemNone = 0x3FFFFFFFu;
@@ -1457,35 +1458,33 @@ __device__ __forceinline__ void put_wait(uint32_t *res, uint32_t q, uint32_t sta
 }
 
 template <bool FINAL, bool WAIT, bool NARROW = false>
-__global__ __launch_bounds__(kPartBlock) void k_unrank(
-    uint64_t n, const uint8_t *__restrict__ dig, const uint32_t *__restrict__ tileprefix,
-    const uint32_t *__restrict__ blockprefix, const uint32_t *__restrict__ digit_total,
-    uint32_t tiles_per_blk, const uint32_t *__restrict__ res_in, uint32_t *__restrict__ res_out,
-    uint8_t *__restrict__ granted, int32_t *__restrict__ remaining) {
-    __shared__ RankLds<kPartBlock> L;
-    __shared__ uint32_t goff[kDigits];
-    __shared__ uint32_t wcnt[(kPartBlock / 64) * kDigits];
-    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);   // the pass's own tile placement
-    const uint64_t base = (uint64_t)tile * kTile;
-    const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    uint32_t dv[kPartItems], lpos[kPartItems];
+__global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
+                                                          const uint32_t *__restrict__ res_in,
+                                                          uint32_t *__restrict__ res_out,
+                                                          uint8_t *__restrict__ granted,
+                                                          int32_t *__restrict__ remaining) {
+    // One workgroup per 8192 positions, XCD-aware like k_scatter: the tile's gathers land
+    // in the digit runs of the partition tiles it covers, which stay in this XCD's L2.
+    const int tid = threadIdx.x;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kUnTile;
+    const int nvalid = (int)min<uint64_t>(kUnTile, n - base);
+    uint32_t pv[kUnItems], r[kUnItems];
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = wb_elem<kPartBlock, kPartItems>(it);
-        dv[it] = (e < nvalid) ? (uint32_t)dig[base + e] : 0u;
-    }
-    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
-    rank_tile_wb<kPartBlock, kPartItems>(dv, 0, nvalid, L, wcnt, lpos);
-    uint32_t r[kPartItems];
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = wb_elem<kPartBlock, kPartItems>(it);
-        const uint32_t q = goff[dv[it]] + lpos[it] - L.lstart[dv[it]];
-        r[it] = (e < nvalid) ? (NARROW ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[q] : res_in[q]) : 0u;
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
+        pv[it] = (e < nvalid) ? LD_U(perm + base + e) : 0u;
     }
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = wb_elem<kPartBlock, kPartItems>(it);
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
+        r[it] = (e < nvalid) ? (NARROW ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[pv[it]]
+                                       : res_in[pv[it]])
+                             : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kUnItems; ++it) {
+        const int e = it * kUnBlock + tid;
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
         if (FINAL && WAIT && NARROW) {
@@ -2725,7 +2724,7 @@ struct PassBufs {
     int32_t *permits = nullptr;
     int64_t *ts = nullptr;
     uint32_t *idx = nullptr;     // arrival index (queueing kind only)
-    uint8_t *dig = nullptr;      // digit of each input element of the pass (k_unrank)
+    uint32_t *perm = nullptr;    // output position of each input element of the pass
     uint32_t *tileprefix = nullptr;
     uint32_t *blockprefix = nullptr;
     uint32_t *digit_total = nullptr;
@@ -2880,7 +2879,7 @@ void free_workspace(Workspace &w) {
         dfree(pb.permits);
         dfree(pb.ts);
         dfree(pb.idx);
-        dfree(pb.dig);
+        dfree(pb.perm);
         dfree(pb.tileprefix);
         dfree(pb.blockprefix);
         dfree(pb.digit_total);
@@ -2930,7 +2929,7 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
             HIP_TRY(e, hipMalloc(&pb.permits, cap * sizeof(int32_t)));
             HIP_TRY(e, hipMalloc(&pb.ts, cap * sizeof(int64_t)));
         }
-        HIP_TRY(e, hipMalloc(&pb.dig, cap * sizeof(uint8_t)));
+        HIP_TRY(e, hipMalloc(&pb.perm, cap * sizeof(uint32_t)));
         if (e->cfg.kind != TBE_KIND_TOKEN_BUCKET) HIP_TRY(e, hipMalloc(&pb.idx, cap * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.tileprefix, (uint64_t)ntiles * kDigits * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&pb.blockprefix, (uint64_t)kMaxHistBlocks * kDigits * sizeof(uint32_t)));
@@ -3070,59 +3069,59 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         if (e->packed && approx && p == 0)
             k_scatter_rec<true, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, nullptr, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.dig, w.err);
+                out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed && approx)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
-                out.blockprefix, out.digit_total, tpb, out.rec, out.dig, w.err);
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.dig, w.err, nullptr, 0, 0, nullptr, out.idx);
+                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
         else if (e->packed && wait)
             k_scatter_rec<false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
-                out.blockprefix, out.digit_total, tpb, out.rec, out.dig, w.err, nullptr, 0, 0,
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0,
                 w.pass[p - 1].idx, out.idx);
         else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.dig, w.err, hot, e->nbuckets, e->r_bits);
+                out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits);
         else if (e->packed && p == 0)
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.dig, w.err);
+                out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
-                out.blockprefix, out.digit_total, tpb, out.rec, out.dig, w.err);
+                out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (approx && p == 0)
             k_scatter<uint64_t, true, false><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, nullptr, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.dig, w.err, 1);
+                out.digit_total, tpb, out.keys, out.permits, nullptr, out.idx, out.perm, w.err, 1);
         else if (approx)
             k_scatter<uint32_t, true, false><<<ntiles, kPartBlock, 0, sp>>>(
                 w.pass[p - 1].keys, w.pass[p - 1].permits, nullptr, w.pass[p - 1].idx, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits, nullptr,
-                out.idx, out.dig, w.err, 0);
+                out.idx, out.perm, w.err, 0);
         else if (p == 0 && !wait)
             k_scatter<uint64_t, false><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.dig, w.err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, nullptr, out.perm, w.err, 1);
         else if (p == 0)
             k_scatter<uint64_t, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, out.dig, w.err, 1);
+                out.digit_total, tpb, out.keys, out.permits, out.ts, out.idx, out.perm, w.err, 1);
         else if (!wait)
             k_scatter<uint32_t, false><<<ntiles, kPartBlock, 0, sp>>>(
                 w.pass[p - 1].keys, w.pass[p - 1].permits, w.pass[p - 1].ts, nullptr, n, shift,
                 out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys, out.permits,
-                out.ts, nullptr, out.dig, w.err, 0);
+                out.ts, nullptr, out.perm, w.err, 0);
         else
             k_scatter<uint32_t, true><<<ntiles, kPartBlock, 0, sp>>>(
                 w.pass[p - 1].keys, w.pass[p - 1].permits, w.pass[p - 1].ts, w.pass[p - 1].idx,
                 n, shift, out.tileprefix, out.blockprefix, out.digit_total, tpb, out.keys,
-                out.permits, out.ts, out.idx, out.dig, w.err, 0);
+                out.permits, out.ts, out.idx, out.perm, w.err, 0);
         stage_end(e, ST_SCATTER, sp);
     }
     const PassBufs &sorted = w.pass[e->passes - 1];
@@ -3212,31 +3211,29 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         stage_end(e, ST_HOT, sf);
     }
     stage_begin(e, ST_UNSCATTER, sf);
+    const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
-    for (int p = e->passes - 1; p >= 0; --p) {
-        const PassBufs &pb = w.pass[p];
-        const uint8_t *dg = pb.dig;
-        const uint32_t *tp = pb.tileprefix, *bp = pb.blockprefix, *dt = pb.digit_total;
-        uint32_t *in = w.res[cur], *out = w.res[cur ^ 1];
-        if (p >= 1 && e->narrow && !approx)
-            k_unrank<false, false, true><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, out, nullptr,
-                                                                      nullptr);
-        else if (p >= 1)
-            k_unrank<false, false><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, out, nullptr, nullptr);
-        else if (e->narrow && !wait && !approx)
-            k_unrank<true, false, true><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, nullptr, granted,
-                                                                     remaining);
-        else if (wait && e->narrow)
-            k_unrank<true, true, true><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, nullptr, granted,
-                                                                    remaining);
-        else if (wait)
-            k_unrank<true, true><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, nullptr, granted,
-                                                              remaining);
+    for (int p = e->passes - 1; p >= 1; --p) {
+        if (e->narrow && !approx)
+            k_unscatter<false, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                      w.res[cur ^ 1], nullptr, nullptr);
         else
-            k_unrank<true, false><<<ntiles, kPartBlock, 0, sf>>>(n, dg, tp, bp, dt, tpb, in, nullptr, granted,
-                                                               remaining);
+            k_unscatter<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                    w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
+    if (e->narrow && !wait && !approx)
+        k_unscatter<true, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                     nullptr, granted, remaining);
+    else if (wait && e->narrow)
+        k_unscatter<true, true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                    nullptr, granted, remaining);
+    else if (wait)
+        k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                              nullptr, granted, remaining);
+    else
+        k_unscatter<true, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                               nullptr, granted, remaining);
     stage_end(e, ST_UNSCATTER, sf);
     k_sticky<<<1, 64, 0, sf>>>(w.err, e->sticky);
     HIP_TRY(e, hipGetLastError());
