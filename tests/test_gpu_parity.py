@@ -414,3 +414,27 @@ def test_config_struct_size_versions(engine_lib, gpu):
             lib.tbe_destroy(h)
         else:
             assert st == _capi.TBE_EINVAL
+
+
+@pytest.mark.parametrize("n_keys,n,batches", [(3_000_000, 2_000_000, 3), (600_000, 50_000, 4),
+                                               (1 << 24, 300_000, 2), (70_000, 1_200_000, 3)])
+def test_two_pass_partition_shapes(engine_lib, gpu, n_keys, n, batches):
+    """Two LSD passes over many tiles, one partial tile, and tiles that straddle the first
+    pass's digit boundaries (small key spaces), mixed permits: replies and table against
+    the C restatement."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
+    eng = TokenBucketEngine(n_keys, 6, 2, 10_000_000, device=0)
+    assert eng.layout()["passes"] >= 2
+    ref = cref.CTokenBucket(n_keys, 6, fill_rate(2, 10_000_000))
+    for b in range(batches):
+        keys, permits, ts = trace.make_batch(0x100C + n, n_keys, b, n, 900_000, 0, 3)
+        g, r = eng.acquire_batch(keys, permits, ts)
+        g_ref, r_ref = ref.acquire_batch(keys, permits, ts)
+        assert np.array_equal(g, g_ref) and np.array_equal(r, r_ref), b
+    v, t = eng.export_state()
+    v_ref, t_ref = ref.export_state()
+    touched = t_ref != np.iinfo(np.int64).min
+    assert np.array_equal(t, t_ref)
+    assert np.array_equal(v[touched].view(np.uint64), v_ref[touched].view(np.uint64))
+    eng.close()
+    ref.close()
