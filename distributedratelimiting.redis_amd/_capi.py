@@ -197,6 +197,8 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_sdir_key_of.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]
     lib.tbe_sdir_set_hash_bits.restype = c_int32
     lib.tbe_sdir_set_hash_bits.argtypes = [c_void_p, ctypes.c_uint32]
+    lib.tbe_sdir_set_mode.restype = c_int32
+    lib.tbe_sdir_set_mode.argtypes = [c_void_p, c_int32]
     lib.tbe_numfmt_device.restype = c_int32
     lib.tbe_numfmt_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p]
     lib.tbe_layout.restype = c_int32

@@ -168,6 +168,9 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
 // counted (the loads, not the LDS counting, bound this kernel).
 constexpr int kHBlock = 512;
 constexpr int kHItems = kTile / kHBlock;              // 8
+#ifndef TBE_HIST_AHEAD
+#define TBE_HIST_AHEAD 1                     // tiles of keys in flight ahead of the one counted
+#endif
 #ifndef TBE_HIST_WAVES
 #define TBE_HIST_WAVES 8                     // minimum waves per SIMD (register budget)
 #endif
@@ -197,19 +200,31 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
     uint32_t acc = 0, acc_lo = 0;   // bucket counting (last pass): this thread's digit
     bool bad = false;
     KeyT kn[kHItems];
-    auto load = [&](uint32_t t) {
+#if TBE_HIST_AHEAD >= 2
+    KeyT kn2[kHItems];
+#endif
+    auto load_into = [&](KeyT (&dst)[kHItems], uint32_t t) {
 #pragma unroll
         for (int it = 0; it < kHItems; ++it) {
             const uint64_t i = (uint64_t)t * kTile + it * kHBlock + tid;
-            kn[it] = (t < t1 && i < n) ? LD_P(keys + i) : (KeyT)0;
+            dst[it] = (t < t1 && i < n) ? LD_P(keys + i) : (KeyT)0;
         }
     };
-    load(t0);
+    load_into(kn, t0);
+#if TBE_HIST_AHEAD >= 2
+    load_into(kn2, t0 + 1);
+#endif
     for (uint32_t t = t0; t < t1; ++t) {
         KeyT kv[kHItems];
 #pragma unroll
         for (int it = 0; it < kHItems; ++it) kv[it] = kn[it];
-        load(t + 1);                                 // in flight while this tile is counted
+#if TBE_HIST_AHEAD >= 2
+#pragma unroll
+        for (int it = 0; it < kHItems; ++it) kn[it] = kn2[it];
+        load_into(kn2, t + 2);                       // two tiles in flight while this one is counted
+#else
+        load_into(kn, t + 1);                        // in flight while this tile is counted
+#endif
 #pragma unroll
         for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
         __syncthreads();
@@ -470,35 +485,47 @@ __global__ __launch_bounds__(1024) void k_bscan(const uint32_t *__restrict__ bco
     __shared__ uint32_t tile[1024 * kScanPer];
     __shared__ uint32_t wsum[16];
     const uint32_t t = threadIdx.x;
+    constexpr uint32_t kRow = 1024 * kScanPer;
+    constexpr int kGroup = 4;   // rows whose loads are all issued before the first is scanned
     uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < nbt; r0 += 1024 * kScanPer) {
+    for (uint32_t g0 = 0; g0 < nbt; g0 += kGroup * kRow) {
+        uint32_t ld[kGroup][kScanPer];
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const uint32_t j = r0 + k * 1024 + t;
-            tile[k * 1024 + t] = j < nbt ? bcount[j] : 0u;
-        }
-        __syncthreads();
-        uint32_t v[kScanPer], sum = 0;
+        for (int r = 0; r < kGroup; ++r)
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            v[k] = tile[t * kScanPer + k];
-            sum += v[k];
-        }
-        uint32_t total;
-        uint32_t pre = carry + block_excl_scan<1024>(sum, wsum, &total);
+            for (int k = 0; k < kScanPer; ++k) {
+                const uint32_t j = g0 + r * kRow + k * 1024 + t;
+                ld[r][k] = j < nbt ? bcount[j] : 0u;
+            }
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            tile[t * kScanPer + k] = pre;
-            pre += v[k];
-        }
-        __syncthreads();
+        for (int r = 0; r < kGroup; ++r) {
+            const uint32_t r0 = g0 + r * kRow;
+            if (r0 >= nbt) break;                      // uniform across the block
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const uint32_t j = r0 + k * 1024 + t;
-            if (j < nbt) bstart[j] = tile[k * 1024 + t];
+            for (int k = 0; k < kScanPer; ++k) tile[k * 1024 + t] = ld[r][k];
+            __syncthreads();
+            uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+            for (int k = 0; k < kScanPer; ++k) {
+                v[k] = tile[t * kScanPer + k];
+                sum += v[k];
+            }
+            uint32_t total;
+            uint32_t pre = carry + block_excl_scan<1024>(sum, wsum, &total);
+#pragma unroll
+            for (int k = 0; k < kScanPer; ++k) {
+                tile[t * kScanPer + k] = pre;
+                pre += v[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kScanPer; ++k) {
+                const uint32_t j = r0 + k * 1024 + t;
+                if (j < nbt) bstart[j] = tile[k * 1024 + t];
+            }
+            carry += total;
+            __syncthreads();
         }
-        carry += total;
-        __syncthreads();
     }
     if (t == 0) bstart[nbt] = carry;
 }
@@ -1449,15 +1476,28 @@ __device__ __forceinline__ uint32_t pack_wait(uint32_t status, bool evaluated, u
 // Queueing kind with TokenLimit <= 62: one byte, status in bits 6-7 and remaining in bits
 // 0-5 (63 = no script call), through the fold and the un-partition passes.
 constexpr uint32_t kRemNone8 = 63u;
+// Queueing and approximate kinds with TokenLimit <= 16382 (remaining / AvailableTokens
+// never exceeds TokenLimit): two bytes, status in bits 14-15 and the count in bits 0-13
+// (16383 = no script call).
+constexpr uint32_t kRemNone16 = 0x3FFFu;
+// rw: reply width code of the wait kinds -- 1 one byte, 2 two bytes, otherwise four.
 __device__ __forceinline__ void put_wait(uint32_t *res, uint32_t q, uint32_t status, bool evaluated, uint32_t rem,
-                                         uint32_t narrow) {
-    if (narrow)
+                                         uint32_t rw) {
+    if (rw == 1)
         reinterpret_cast<uint8_t *>(res)[q] = (uint8_t)((status << 6) | (evaluated ? (rem & 63u) : kRemNone8));
+    else if (rw == 2)
+        reinterpret_cast<uint16_t *>(res)[q] =
+            (uint16_t)((status << 14) | (evaluated ? (rem & kRemNone16) : kRemNone16));
     else
         res[q] = pack_wait(status, evaluated, rem);
 }
+// A four-byte wait reply (pack_wait) in the two-byte form.
+__device__ __forceinline__ uint16_t wait16(uint32_t v) {
+    const uint32_t rem = v & kRemNone;
+    return (uint16_t)(((v >> 30) << 14) | (rem == kRemNone ? kRemNone16 : (rem & kRemNone16)));
+}
 
-template <bool FINAL, bool WAIT, bool NARROW = false>
+template <bool FINAL, bool WAIT, int W = 4>
 __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32_t *__restrict__ perm,
                                                           const uint32_t *__restrict__ res_in,
                                                           uint32_t *__restrict__ res_out,
@@ -1478,8 +1518,9 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
 #pragma unroll
     for (int it = 0; it < kUnItems; ++it) {
         const int e = it * kUnBlock + tid;
-        r[it] = (e < nvalid) ? (NARROW ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[pv[it]]
-                                       : res_in[pv[it]])
+        r[it] = (e < nvalid) ? (W == 1 ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[pv[it]]
+                                : W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(res_in)[pv[it]]
+                                         : res_in[pv[it]])
                              : 0u;
     }
 #pragma unroll
@@ -1487,22 +1528,28 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
         const int e = it * kUnBlock + tid;
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
-        if (FINAL && WAIT && NARROW) {
+        if (FINAL && WAIT && W == 1) {
             ST_U(granted + i, (uint8_t)(r[it] >> 6));
             const uint32_t rem = r[it] & 63u;
             ST_U(remaining + i, (rem == kRemNone8) ? -1 : (int32_t)rem);
+        } else if (FINAL && WAIT && W == 2) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 14));
+            const uint32_t rem = r[it] & kRemNone16;
+            ST_U(remaining + i, (rem == kRemNone16) ? -1 : (int32_t)rem);
         } else if (FINAL && WAIT) {
             ST_U(granted + i, (uint8_t)(r[it] >> 30));
             const uint32_t rem = r[it] & kRemNone;
             ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
-        } else if (FINAL && NARROW) {
+        } else if (FINAL && W == 1) {
             ST_U(granted + i, (uint8_t)(r[it] >> 7));
             ST_U(remaining + i, (int32_t)(r[it] & 0x7Fu));
         } else if (FINAL) {
             ST_U(granted + i, (uint8_t)(r[it] >> 31));
             ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
-        } else if (NARROW) {
+        } else if (W == 1) {
             ST_U(reinterpret_cast<uint8_t *>(res_out) + i, (uint8_t)r[it]);
+        } else if (W == 2) {
+            ST_U(reinterpret_cast<uint16_t *>(res_out) + i, (uint16_t)r[it]);
         } else {
             ST_U(res_out + i, r[it]);
         }
@@ -1928,6 +1975,72 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     status = TBE_WAIT_QUEUED;
 }
 
+// One key's share of a replenish tick (Q:237-271): grant the head (OldestFirst) or tail
+// (NewestFirst) entry while the script grants at the tick.  Every queued entry holds >= 1
+// permit, so when one permit is denied the entry is too, with the same state change (a
+// denial only ever deletes a lapsed key): a one-permit probe decides that case without
+// reading the ring.  WRITE = false counts the grants and changes nothing; WRITE = true
+// applies them to (st, h) and logs them at at, at + 1, ... (key << 16 | drain position,
+// request id, remaining).  Both forms take the same decisions, so a count pass followed by
+// one reservation per workgroup and a writing pass logs exactly the grants -- one global
+// atomic per workgroup instead of one per grant (a single log counter shared by every
+// grant of the tick serialised them: 23M grants took 15 ms).
+struct DrainLog {
+    uint64_t *keyseq;
+    int64_t *id;
+    int32_t *rem;
+    uint32_t cap;
+};
+template <bool WRITE>
+__device__ __forceinline__ uint32_t drain_key(uint64_t key, Slot &st, uint64_t &h, bool &smod,
+                                              const uint64_t *__restrict__ kr, const ReqTime &rqT, const TbParams &P,
+                                              const QParams &Q, const DrainLog &L, uint32_t at) {
+    uint32_t cnt = (uint32_t)((h >> 16) & 0xFFFFu);
+    if (cnt == 0) return 0;
+    uint32_t head = (uint32_t)(h & 0xFFFFu);
+    int64_t qsum = (int64_t)(h >> 32);
+    Slot s = st;
+    bool m_any = false;
+    uint32_t seq = 0;
+    while (cnt > 0) {
+        {
+            Slot probe = s;
+            bool pm;
+            if (!(tb_step(probe, 1, rqT, P, pm) >> 31)) {
+                s = probe;
+                m_any |= pm;
+                break;
+            }
+        }
+        uint32_t idx = head;
+        if (Q.order == 1) {
+            idx = head + cnt - 1;
+            if (idx >= Q.cap) idx -= Q.cap;
+        }
+        const uint64_t ent = kr[idx];
+        const int32_t p = (int32_t)(ent & 0xFFFFu);
+        bool m;
+        const uint32_t reply = tb_step(s, p, rqT, P, m);
+        m_any |= m;
+        if (!(reply >> 31)) break;
+        if (WRITE && at + seq < L.cap) {
+            L.keyseq[at + seq] = (key << 16) | seq;
+            L.id[at + seq] = (int64_t)(ent >> 16);
+            L.rem[at + seq] = (int32_t)(reply & 0x7FFFFFFFu);
+        }
+        ++seq;
+        qsum -= p;
+        if (Q.order == 0) head = (head + 1 == Q.cap) ? 0 : head + 1;
+        --cnt;
+    }
+    if (WRITE) {
+        st = s;
+        smod |= m_any;
+        if (seq) h = qh_pack(head, cnt, qsum);
+    }
+    return seq;
+}
+
 // A replenish tick fused into a queue batch (tbe_wait_batch_tick_device): after the
 // batch's requests, every key of the bucket is drained at `ts` exactly as k_drain does,
 // on the rows and headers already in LDS.  ts < 0: no tick.
@@ -2200,55 +2313,45 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     }
     __syncthreads();
     if (tick) {
-        // The fused replenish tick (Q:237-271, as k_drain): head (OldestFirst) or tail
-        // (NewestFirst) entries granted while the script grants at T.ts; a one-permit
-        // probe first, so a denied key reads no ring entry.
+        // The fused replenish tick (Q:237-271, as k_drain) on the rows and headers in LDS:
+        // count this workgroup's grants, reserve them in the log with one atomic, then
+        // drain and log (drain_key).
         const ReqTime rqT = req_time(T.ts, P.ttl_ms);
-        for (uint32_t j = tid; j < nrows; j += kQBlock) {
-            const uint64_t h0 = qh[j];
-            uint32_t cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
-            if (cnt == 0) continue;
-            uint32_t head = (uint32_t)(h0 & 0xFFFFu);
-            int64_t qsum = (int64_t)(h0 >> 32);
-            Slot st = slot[j];
-            bool smod = false;
-            uint32_t seq = 0;
-            const uint64_t *__restrict__ kr = ring + (row0 + j) * (uint64_t)Q.cap;
-            while (cnt > 0) {
-                {
-                    Slot probe = st;
-                    bool pm;
-                    if (!(tb_step(probe, 1, rqT, P, pm) >> 31)) {
-                        st = probe;
-                        smod |= pm;
-                        break;
-                    }
-                }
-                uint32_t idx = head;
-                if (Q.order == 1) {
-                    idx = head + cnt - 1;
-                    if (idx >= Q.cap) idx -= Q.cap;
-                }
-                const uint64_t ent = kr[idx];
-                const int32_t p = (int32_t)(ent & 0xFFFFu);
-                bool m;
-                const uint32_t reply = tb_step(st, p, rqT, P, m);
-                smod |= m;
-                if (!(reply >> 31)) break;
-                const uint32_t at = atomicAdd(T.count, 1u);
-                if (at < T.cap) {
-                    T.keyseq[at] = ((row0 + j) << 16) | seq;
-                    T.id[at] = (int64_t)(ent >> 16);
-                    T.rem[at] = (int32_t)(reply & 0x7FFFFFFFu);
-                }
-                ++seq;
-                qsum -= p;
-                if (Q.order == 0) head = (head + 1 == Q.cap) ? 0 : head + 1;
-                --cnt;
+        const DrainLog L{T.keyseq, T.id, T.rem, T.cap};
+        constexpr uint32_t kRowsPer = (kMaxRows + kQBlock - 1) / kQBlock;
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kRowsPer; ++u) {
+            const uint32_t j = tid + u * kQBlock;
+            if (j < nrows) {
+                Slot st = slot[j];
+                uint64_t h = qh[j];
+                bool sm = false;
+                mine += drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P, Q, L, 0);
             }
-            if (smod) slot[j] = st;
-            if (seq) qh[j] = qh_pack(head, cnt, qsum);
-            if (smod || seq) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+        }
+        uint32_t total;
+        __shared__ uint32_t tick_wsum[kQBlock / 64];
+        const uint32_t off = block_excl_scan<kQBlock>(mine, tick_wsum, &total);
+        __shared__ uint32_t log_base;
+        if (tid == 0) log_base = total ? atomicAdd(T.count, total) : 0u;
+        __syncthreads();
+        uint32_t at = log_base + off;
+#pragma unroll
+        for (uint32_t u = 0; u < kRowsPer; ++u) {
+            const uint32_t j = tid + u * kQBlock;
+            if (j < nrows) {
+                Slot st = slot[j];
+                uint64_t h = qh[j];
+                const uint64_t h0 = h;
+                bool smod = false;
+                const uint32_t g = drain_key<true>(row0 + j, st, h, smod, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P,
+                                                   Q, L, at);
+                at += g;
+                if (smod) slot[j] = st;
+                if (h != h0) qh[j] = h;
+                if (smod || h != h0) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+            }
         }
         __syncthreads();
     }
@@ -2267,54 +2370,35 @@ __global__ __launch_bounds__(kBlock) void k_drain(
     const uint64_t *__restrict__ ring, TbParams P, QParams Q, int64_t ts_us,
     uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
     uint32_t *__restrict__ log_count, uint32_t log_cap) {
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t log_base;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t key = (uint64_t)blockIdx.x * kBlock + threadIdx.x; key < n_keys; key += stride) {
-        const uint64_t h0 = qhdr[key];
-        uint32_t cnt = (uint32_t)((h0 >> 16) & 0xFFFFu);
-        if (cnt == 0) continue;
-        uint32_t head = (uint32_t)(h0 & 0xFFFFu);
-        int64_t qsum = (int64_t)(h0 >> 32);
-        Slot st = table[key];
-        bool smod = false;
-        uint32_t seq = 0;
+    const ReqTime rqT = req_time(ts_us, P.ttl_ms);
+    const DrainLog L{log_keyseq, log_id, log_rem, log_cap};
+    // block-uniform trip count (the log reservation below is a block-wide scan)
+    for (uint64_t k0 = (uint64_t)blockIdx.x * kBlock; k0 < n_keys; k0 += stride) {
+        const uint64_t key = k0 + threadIdx.x;
+        const bool valid = key < n_keys;
+        uint64_t h = valid ? qhdr[key] : 0ull;
+        const bool queued = ((h >> 16) & 0xFFFFu) != 0;
+        Slot st = (valid && queued) ? table[key] : Slot{0.0, 0};
         const uint64_t *__restrict__ kr = ring + key * (uint64_t)Q.cap;
-        while (cnt > 0) {
-            // Every queued entry holds >= 1 permit, so when one permit is denied the entry
-            // is too, with the same state change (a denial only ever deletes a lapsed
-            // key, whatever the permits): decide that case without reading the ring.
-            {
-                Slot probe = st;
-                bool pm;
-                if (!(tb_acquire(probe, 1, ts_us, P, pm) >> 31)) {
-                    st = probe;
-                    smod |= pm;
-                    break;
-                }
-            }
-            uint32_t idx = head;
-            if (Q.order == 1) {
-                idx = head + cnt - 1;
-                if (idx >= Q.cap) idx -= Q.cap;
-            }
-            const uint64_t ent = kr[idx];
-            const int32_t p = (int32_t)(ent & 0xFFFFu);
-            bool m;
-            const uint32_t reply = tb_acquire(st, p, ts_us, P, m);
-            smod |= m;
-            if (!(reply >> 31)) break;
-            const uint32_t at = atomicAdd(log_count, 1u);
-            if (at < log_cap) {
-                log_keyseq[at] = (key << 16) | seq;
-                log_id[at] = (int64_t)(ent >> 16);
-                log_rem[at] = (int32_t)(reply & 0x7FFFFFFFu);
-            }
-            ++seq;
-            qsum -= p;
-            if (Q.order == 0) head = (head + 1 == Q.cap) ? 0 : head + 1;
-            --cnt;
+        bool sm = false;
+        Slot st0 = st;
+        uint64_t h0 = h;
+        const uint32_t mine = queued ? drain_key<false>(key, st0, h0, sm, kr, rqT, P, Q, L, 0) : 0u;
+        uint32_t total;
+        const uint32_t off = block_excl_scan<kBlock>(mine, wsum, &total);
+        if (threadIdx.x == 0) log_base = total ? atomicAdd(log_count, total) : 0u;
+        __syncthreads();
+        if (queued) {
+            bool smod = false;
+            const uint64_t hb = h;
+            drain_key<true>(key, st, h, smod, kr, rqT, P, Q, L, log_base + off);
+            if (smod) table[key] = st;
+            if (h != hb) qhdr[key] = h;
         }
-        if (smod) table[key] = st;
-        if (seq) qhdr[key] = qh_pack(head, cnt, qsum);
+        __syncthreads();   // log_base is rewritten by the next trip
     }
 }
 
@@ -2375,7 +2459,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
     const uint32_t *__restrict__ bstart, int r_bits,
     uint64_t n_keys, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring, AParams A,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
-    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err) {
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t rw) {
     __shared__ ALocal sl[kMaxRows];
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t rbuf[kFoldChunk];
@@ -2557,7 +2641,10 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
 #pragma unroll
         for (int r = 0; r < kFoldPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
-            if (q < e) res[q] = rbuf[r * kFoldBlock + tid];
+            if (q < e) {
+                if (rw == 2) reinterpret_cast<uint16_t *>(res)[q] = wait16(rbuf[r * kFoldBlock + tid]);
+                else res[q] = rbuf[r * kFoldBlock + tid];
+            }
         }
     }
     __syncthreads();
@@ -2770,6 +2857,9 @@ struct tbe_engine {
     bool packed = false;     // token bucket and queueing kinds: passes move packed u64 records (PackFmt)
     bool narrow = false;     // one-byte replies: token bucket (packed, TokenLimit <= 127, put_reply),
                              // queueing kind (TokenLimit <= 62, put_wait)
+    bool medium = false;     // two-byte replies: queueing and approximate kinds, TokenLimit <= 16382
+    // reply width code of the wait kinds' folds (put_wait): 1, 2 or 4 (as 0) bytes
+    uint32_t wait_rw() const { return narrow ? 1u : (medium ? 2u : 0u); }
     PackFmt pf{};
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
@@ -3144,12 +3234,12 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             k_fold_a<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, e->pf, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
                 e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
-                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw());
         else
             k_fold_a<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.idx, nullptr, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
                 e->alocal, e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
-                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err);
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw());
     } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
@@ -3159,14 +3249,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
                 e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
-                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->narrow ? 1u : 0u,
+                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(),
                 e->qtick);
         else
             k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
                 e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
                 e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
-                e->narrow ? 1u : 0u, e->qtick);
+                e->wait_rw(), e->qtick);
     } else if (e->packed) {
         // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
@@ -3215,19 +3305,25 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     int cur = 0;
     for (int p = e->passes - 1; p >= 1; --p) {
         if (e->narrow && !approx)
-            k_unscatter<false, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
-                                                                      w.res[cur ^ 1], nullptr, nullptr);
+            k_unscatter<false, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                   w.res[cur ^ 1], nullptr, nullptr);
+        else if (e->medium)
+            k_unscatter<false, false, 2><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
+                                                                   w.res[cur ^ 1], nullptr, nullptr);
         else
             k_unscatter<false, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
                                                                     w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
     if (e->narrow && !wait && !approx)
-        k_unscatter<true, false, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                                     nullptr, granted, remaining);
+        k_unscatter<true, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                  nullptr, granted, remaining);
     else if (wait && e->narrow)
-        k_unscatter<true, true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                                    nullptr, granted, remaining);
+        k_unscatter<true, true, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                 nullptr, granted, remaining);
+    else if (wait && e->medium)
+        k_unscatter<true, true, 2><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
+                                                                 nullptr, granted, remaining);
     else if (wait)
         k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                               nullptr, granted, remaining);
@@ -3358,6 +3454,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
+        e->medium = (c.flags & TBE_FLAG_NO_NARROW) == 0 && !e->narrow && c.token_limit <= (int32_t)kRemNone16 - 1 &&
+                    (c.kind == TBE_KIND_QUEUEING || c.kind == TBE_KIND_APPROXIMATE);
     }
 
     auto bail = [&](tbe_status st) {
@@ -4387,7 +4485,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *passes = (uint32_t)e->passes;
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
-              (e->narrow ? 8u : 0u);
+              (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u);
     return TBE_OK;
 }
 

@@ -42,6 +42,7 @@ constexpr int kSdTile = 1024;            // requests per count/assign block (4 p
 constexpr int kSdScan = 1024;
 constexpr unsigned kListGrid = 1024;     // workgroups of a probe round over the collided list
 constexpr uint64_t kLocValid = 1ull << 63;
+constexpr double kWarmShare = 0.5;       // warm path while the last batch's new keys stay below this share
 
 __device__ __host__ __forceinline__ uint32_t loc_len(uint64_t loc) { return (uint32_t)(loc & (2 * kMaxLen - 1)); }
 __device__ __host__ __forceinline__ uint64_t loc_off(uint64_t loc) { return (loc >> 17) & ((1ull << 46) - 1); }
@@ -235,18 +236,31 @@ __device__ __forceinline__ uint32_t sd_room(const uint64_t *offs, uint64_t i) {
     return (uint32_t)((offs[i + 1] - offs[i] + 7) & ~7ull);
 }
 
-// New keys and their arena bytes per block of kSdTile requests.
+// Request at position t of a pass over the batch: t itself, or list[t] when the pass
+// runs over an ordered list of requests (the warm path's misses, in arrival order).
+__device__ __forceinline__ bool sd_at(const uint32_t *__restrict__ list, uint64_t count, uint64_t t, uint64_t &i) {
+    if (t >= count) return false;
+    i = list ? list[t] : t;
+    return true;
+}
+
+// New keys and their arena bytes per block of kSdTile requests (of the batch, or of the
+// ordered list: list / list_n).
 __global__ __launch_bounds__(kSdBlock) void k_sd_count(const uint64_t *__restrict__ offs, uint64_t n,
                                                        const uint32_t *__restrict__ slot_of,
                                                        const uint32_t *__restrict__ sid,
                                                        const uint32_t *__restrict__ sfirst,
-                                                       uint32_t *__restrict__ bsum, uint32_t *__restrict__ bbytes) {
+                                                       uint32_t *__restrict__ bsum, uint32_t *__restrict__ bbytes,
+                                                       const uint32_t *__restrict__ list = nullptr,
+                                                       const uint32_t *__restrict__ list_n = nullptr) {
     __shared__ uint32_t wsum[kSdBlock / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kSdTile;
+    const uint64_t count = list ? *list_n : n;
     uint32_t c = 0, nb = 0;
     for (int k = 0; k < kSdTile / kSdBlock; ++k) {
-        const uint64_t i = base + (uint64_t)threadIdx.x * (kSdTile / kSdBlock) + k;
-        if (i < n && sd_is_new(slot_of, sid, sfirst, i)) {
+        uint64_t i;
+        if (sd_at(list, count, base + (uint64_t)threadIdx.x * (kSdTile / kSdBlock) + k, i) &&
+            sd_is_new(slot_of, sid, sfirst, i)) {
             ++c;
             nb += sd_room(offs, i);
         }
@@ -335,18 +349,21 @@ __global__ __launch_bounds__(kSdBlock) void k_sd_assign(SdBatch B, uint64_t n, c
                                                         const uint64_t *__restrict__ bbase,
                                                         const unsigned long long *__restrict__ state,
                                                         uint64_t capacity, uint64_t arena_bytes, uint64_t imask,
-                                                        uint32_t ish) {
+                                                        uint32_t ish, const uint32_t *__restrict__ list = nullptr,
+                                                        const uint32_t *__restrict__ list_n = nullptr) {
     __shared__ uint32_t wsum[kSdBlock / 64];
     constexpr int PER = kSdTile / kSdBlock;
     const uint64_t base = (uint64_t)blockIdx.x * kSdTile;
+    const uint64_t count = list ? *list_n : n;
     bool nw[PER];
+    uint64_t iv[PER];
     uint32_t c = 0, nb = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const uint64_t i = base + (uint64_t)threadIdx.x * PER + k;
-        nw[k] = i < n && sd_is_new(slot_of, sid, sfirst, i);
+        nw[k] = sd_at(list, count, base + (uint64_t)threadIdx.x * PER + k, iv[k]) &&
+                sd_is_new(slot_of, sid, sfirst, iv[k]);
         c += nw[k];
-        nb += nw[k] ? sd_room(B.offs, i) : 0u;
+        nb += nw[k] ? sd_room(B.offs, iv[k]) : 0u;
     }
     uint32_t tc, tb;
     uint32_t r = block_excl_scan<kSdBlock>(c, wsum, &tc);   // every thread has read sid before it returns
@@ -357,7 +374,7 @@ __global__ __launch_bounds__(kSdBlock) void k_sd_assign(SdBatch B, uint64_t n, c
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         if (!nw[k]) continue;
-        const uint64_t i = base + (uint64_t)threadIdx.x * PER + k;
+        const uint64_t i = iv[k];
         const uint64_t counter = c0 + r++;
         const uint64_t off = B.offs[i];
         const uint32_t len = (uint32_t)(B.offs[i + 1] - off);
@@ -375,9 +392,12 @@ __global__ __launch_bounds__(kSdBlock) void k_sd_assign(SdBatch B, uint64_t n, c
 }
 
 __global__ void k_sd_gather(const uint32_t *__restrict__ slot_of, uint64_t n, const uint32_t *__restrict__ sid,
-                            uint64_t *__restrict__ ids) {
+                            uint64_t *__restrict__ ids, const uint32_t *__restrict__ list = nullptr,
+                            const uint32_t *__restrict__ list_n = nullptr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t count = list ? *list_n : n;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
+        const uint64_t i = list ? list[t] : t;
         const uint32_t sl = slot_of[i];
         const uint32_t id = sl == kNoId ? kNoId : sid[sl];
         ids[i] = id == kNoId ? ~0ull : (uint64_t)id;
@@ -421,6 +441,110 @@ __global__ __launch_bounds__(kSdBlock) void k_sd_lookup(SdBatch B, uint64_t n, S
         }
         ids[i] = id;
     }
+}
+
+// ---------------------------------------------------------------- warm path
+// Most strings of a steady-state batch are already known.  k_sd_resolve answers them the
+// way a lookup does (every probe round, byte compare with the stored text) and leaves
+// UINT64_MAX for the misses; a stable compaction lists the misses in arrival order, and
+// the assign machinery (claim / verify rounds, count, scan, assign, gather) runs over that
+// list only.  Ids are unchanged: the known strings keep theirs, and the new ones get
+// counters in arrival order, exactly as a full pass assigns them.
+__device__ __forceinline__ uint64_t sd_find(const SdBatch &B, uint64_t i, const SdParams &P,
+                                            const uint64_t *__restrict__ stag, const uint32_t *__restrict__ sid,
+                                            const uint64_t *__restrict__ sloc, uint64_t smask, const SdArena &A) {
+    uint64_t off;
+    uint32_t len;
+    if (!sd_span(B.offs, i, B.n_bytes, off, len)) return ~0ull;   // the claim round flags it
+    for (uint32_t round = 0; round < (uint32_t)kRounds; ++round) {
+        const uint64_t tag = sd_tag(round, sd_hash(B.bytes, B.safe, off, len, P.seed[round]), P.hmask);
+        uint64_t h = mix64(tag) & smask;
+        for (uint64_t probe = 0; probe <= smask; ++probe) {
+            const uint64_t cur = stag[h];
+            if (cur == kEmptyTag) return ~0ull;       // never assigned
+            if (cur == tag) {
+                const uint32_t s_id = sid[h];
+                const uint64_t loc = sloc[h];
+                if (s_id != kNoId && loc_len(loc) == len &&
+                    sd_equal(A.bytes, A.safe, loc_off(loc), B.bytes, B.safe, off, len))
+                    return s_id;
+                break;                                // tags are unique: the next round's
+            }
+            h = (h + 1) & smask;
+        }
+    }
+    return ~0ull;
+}
+
+// ids[i] = the id of a known string, UINT64_MAX for a miss; bmiss[block] = its misses.
+// Requests are thread-contiguous within a block (as k_sd_count), kSdTile per block.
+__global__ __launch_bounds__(kSdBlock) void k_sd_resolve(SdBatch B, uint64_t n, SdParams P,
+                                                         const uint64_t *__restrict__ stag,
+                                                         const uint32_t *__restrict__ sid,
+                                                         const uint64_t *__restrict__ sloc, uint64_t smask, SdArena A,
+                                                         uint64_t *__restrict__ ids, uint32_t *__restrict__ bmiss) {
+    __shared__ uint32_t wsum[kSdBlock / 64];
+    constexpr int PER = kSdTile / kSdBlock;
+    const uint64_t base = (uint64_t)blockIdx.x * kSdTile;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * PER + k;
+        if (i < n) {
+            const uint64_t id = sd_find(B, i, P, stag, sid, sloc, smask, A);
+            ids[i] = id;
+            c += id == ~0ull;
+        }
+    }
+    uint32_t tot;
+    (void)block_excl_scan<kSdBlock>(c, wsum, &tot);
+    if (threadIdx.x == 0) bmiss[blockIdx.x] = tot;
+}
+
+// Exclusive scan of the per-block miss counts in place; *total = all misses.
+__global__ __launch_bounds__(kSdScan) void k_sd_xscan(uint32_t *__restrict__ v, uint32_t nblk,
+                                                      uint32_t *__restrict__ total) {
+    __shared__ uint32_t wsum[kSdScan / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nblk + kSdScan - 1) / kSdScan;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t j = t * per + k;
+        if (j < nblk) sum += v[j];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<kSdScan>(sum, wsum, &tot);
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t j = t * per + k;
+        if (j < nblk) {
+            const uint32_t c = v[j];
+            v[j] = run;
+            run += c;
+        }
+    }
+    if (t == 0) *total = tot;
+}
+
+// The misses in arrival order: list[bmiss[block] + rank in block] = i.
+__global__ __launch_bounds__(kSdBlock) void k_sd_compact(uint64_t n, const uint64_t *__restrict__ ids,
+                                                         const uint32_t *__restrict__ bmiss,
+                                                         uint32_t *__restrict__ list) {
+    __shared__ uint32_t wsum[kSdBlock / 64];
+    constexpr int PER = kSdTile / kSdBlock;
+    const uint64_t base = (uint64_t)blockIdx.x * kSdTile;
+    bool miss[PER];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const uint64_t i = base + (uint64_t)threadIdx.x * PER + k;
+        miss[k] = i < n && ids[i] == ~0ull;
+        c += miss[k];
+    }
+    uint32_t tot;
+    uint32_t at = bmiss[blockIdx.x] + block_excl_scan<kSdBlock>(c, wsum, &tot);
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (miss[k]) list[at++] = (uint32_t)(base + (uint64_t)threadIdx.x * PER + k);
 }
 
 __global__ void k_sd_init(uint64_t *__restrict__ stag, uint32_t *__restrict__ sid, uint32_t *__restrict__ sfirst,
@@ -472,6 +596,16 @@ struct tbe_string_directory {
     uint32_t *list_n = nullptr;            // [kRounds]
     uint32_t *bsum = nullptr, *bbytes = nullptr;
     uint64_t *bbase = nullptr;
+    uint32_t *miss = nullptr;              // warm path: the batch's misses, arrival order
+    uint32_t *bmiss = nullptr;             // warm path: misses per block (scanned)
+    // warm-path choice: 0 auto (the last observed batch's new-key share), 1 full pass, 2 warm
+    int mode = 0;
+    unsigned long long *h_state = nullptr; // pinned: state[0] after the last assign (async copy)
+    hipEvent_t ev_state = nullptr;
+    bool state_pending = false;
+    unsigned long long last_ids = 0;       // ids before the batch whose count is in flight
+    uint64_t last_n = 0;                   // that batch's size
+    double new_share = 1.0;                // new keys / requests of the last observed batch
     // host-buffer staging
     uint64_t st_bytes = 0, st_n = 0;
     uint8_t *d_bytes = nullptr;
@@ -482,9 +616,9 @@ namespace {
 
 void sd_free_scratch(tbe_string_directory *d) {
     for (void *p : {(void *)d->slot_of, (void *)d->list[0], (void *)d->list[1], (void *)d->bsum, (void *)d->bbytes,
-                    (void *)d->bbase})
+                    (void *)d->bbase, (void *)d->miss, (void *)d->bmiss})
         if (p) (void)hipFree(p);
-    d->slot_of = d->list[0] = d->list[1] = d->bsum = d->bbytes = nullptr;
+    d->slot_of = d->list[0] = d->list[1] = d->bsum = d->bbytes = d->miss = d->bmiss = nullptr;
     d->bbase = nullptr;
     d->tmp_cap = 0;
 }
@@ -500,7 +634,9 @@ tbe_status sd_scratch(tbe_string_directory *d, uint64_t n) {
         hipMalloc(&d->list[1], cap * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&d->bsum, nblk * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&d->bbytes, nblk * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&d->bbase, nblk * sizeof(uint64_t)) != hipSuccess) {
+        hipMalloc(&d->bbase, nblk * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&d->miss, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&d->bmiss, nblk * sizeof(uint32_t)) != hipSuccess) {
         sd_free_scratch(d);
         return TBE_ENOMEM;
     }
@@ -550,7 +686,9 @@ tbe_status tbe_sdir_create(uint64_t capacity, uint64_t arena_bytes, const char *
               hipMalloc(&d->iloc, capacity * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&d->arena, d->arena_alloc) == hipSuccess &&
               hipMalloc(&d->state, 8 * sizeof(unsigned long long)) == hipSuccess &&
-              hipMalloc(&d->list_n, kRounds * sizeof(uint32_t)) == hipSuccess;
+              hipMalloc(&d->list_n, (kRounds + 1) * sizeof(uint32_t)) == hipSuccess &&
+              hipHostMalloc(&d->h_state, sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess &&
+              hipEventCreateWithFlags(&d->ev_state, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         tbe_sdir_destroy(d);
         return TBE_ENOMEM;
@@ -571,6 +709,8 @@ void tbe_sdir_destroy(tbe_string_directory *d) {
     (void)hipSetDevice(d->device);
     (void)hipDeviceSynchronize();
     sd_free_scratch(d);
+    if (d->h_state) (void)hipHostFree(d->h_state);
+    if (d->ev_state) (void)hipEventDestroy(d->ev_state);
     for (void *p : {(void *)d->stag, (void *)d->sid, (void *)d->sfirst, (void *)d->sloc, (void *)d->iloc,
                     (void *)d->arena, (void *)d->state, (void *)d->list_n, (void *)d->d_bytes, (void *)d->d_offs,
                     (void *)d->d_ids})
@@ -597,25 +737,57 @@ tbe_status tbe_sdir_assign_device(tbe_string_directory *d, const uint8_t *d_byte
     const SdBatch B{d_bytes, d_offs, n_bytes, n_bytes & ~7ull};
     const SdArena A{d->arena, d->arena_alloc & ~7ull};
     unsigned long long *err = d->state + 1;
-    if (hipMemsetAsync(d->list_n, 0, kRounds * sizeof(uint32_t), st) != hipSuccess) return TBE_EDEVICE;
+    if (hipMemsetAsync(d->list_n, 0, (kRounds + 1) * sizeof(uint32_t), st) != hipSuccess) return TBE_EDEVICE;
     const uint64_t smask = d->nslots - 1;
+    const uint32_t nblk = (uint32_t)((n + kSdTile - 1) / kSdTile);
+    // The warm path pays one lookup pass over the batch to run the assign machinery over
+    // its misses only: chosen while the last observed batch brought few new keys (its id
+    // count is copied back asynchronously; the choice never waits for it).
+    if (d->state_pending && hipEventQuery(d->ev_state) == hipSuccess) {
+        d->new_share = d->last_n ? (double)(*d->h_state - d->last_ids) / (double)d->last_n : 1.0;
+        d->last_ids = *d->h_state;
+        d->state_pending = false;
+    }
+    const bool warm = d->mode == 2 || (d->mode == 0 && d->new_share < kWarmShare);
+    const uint32_t *miss = warm ? d->miss : nullptr;
+    const uint32_t *miss_n = warm ? d->list_n + kRounds : nullptr;
+    if (warm) {
+        k_sd_resolve<<<nblk, kSdBlock, 0, st>>>(B, n, d->P, d->stag, d->sid, d->sloc, smask, A, d_ids, d->bmiss);
+        k_sd_xscan<<<1, kSdScan, 0, st>>>(d->bmiss, nblk, d->list_n + kRounds);
+        k_sd_compact<<<nblk, kSdBlock, 0, st>>>(n, d_ids, d->bmiss, d->miss);
+    }
     for (int round = 0; round < kRounds; ++round) {
-        const uint32_t *in = round ? d->list[(round - 1) & 1] : nullptr;
-        const uint32_t *in_n = round ? d->list_n + (round - 1) : nullptr;
+        const uint32_t *in = round ? d->list[(round - 1) & 1] : miss;
+        const uint32_t *in_n = round ? d->list_n + (round - 1) : miss_n;
         uint32_t *nx = (round + 1 < kRounds) ? d->list[round & 1] : nullptr;
         uint32_t *nx_n = (round + 1 < kRounds) ? d->list_n + round : nullptr;
-        const unsigned g = round ? kListGrid : sd_grid(n, kSdBlock);
+        const unsigned g = in ? (round ? kListGrid : sd_grid(n, kSdBlock)) : sd_grid(n, kSdBlock);
         k_sd_claim<<<g, kSdBlock, 0, st>>>(B, n, in, in_n, (uint32_t)round, d->P, d->stag, d->sid, d->sfirst, smask,
                                            d->slot_of, err);
         k_sd_verify<<<g, kSdBlock, 0, st>>>(B, n, in, in_n, A, d->sid, d->sfirst, d->sloc, d->slot_of, nx, nx_n, err);
     }
-    const uint32_t nblk = (uint32_t)((n + kSdTile - 1) / kSdTile);
-    k_sd_count<<<nblk, kSdBlock, 0, st>>>(d_offs, n, d->slot_of, d->sid, d->sfirst, d->bsum, d->bbytes);
+    k_sd_count<<<nblk, kSdBlock, 0, st>>>(d_offs, n, d->slot_of, d->sid, d->sfirst, d->bsum, d->bbytes, miss,
+                                          miss_n);
     k_sd_scan<<<1, kSdScan, 0, st>>>(d->bsum, d->bbytes, d->bbase, nblk, d->state, d->capacity, d->arena_bytes);
     k_sd_assign<<<nblk, kSdBlock, 0, st>>>(B, n, d->slot_of, d->sid, d->sfirst, d->sloc, d->iloc, d->arena, d->bsum,
-                                           d->bbase, d->state, d->capacity, d->arena_bytes, d->imask, d->ish);
-    k_sd_gather<<<sd_grid(n, 256), 256, 0, st>>>(d->slot_of, n, d->sid, d_ids);
+                                           d->bbase, d->state, d->capacity, d->arena_bytes, d->imask, d->ish, miss,
+                                           miss_n);
+    k_sd_gather<<<sd_grid(n, 256), 256, 0, st>>>(d->slot_of, n, d->sid, d_ids, miss, miss_n);
+    if (!d->state_pending) {
+        // the batch's id count, for the next call's choice
+        if (hipMemcpyAsync(d->h_state, d->state, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(d->ev_state, st) != hipSuccess)
+            return TBE_EDEVICE;
+        d->state_pending = true;
+        d->last_n = n;
+    }
     return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
+}
+
+tbe_status tbe_sdir_set_mode(tbe_string_directory *d, int32_t mode) {
+    if (!d || mode < 0 || mode > 2) return TBE_EINVAL;
+    d->mode = mode;
+    return TBE_OK;
 }
 
 tbe_status tbe_sdir_lookup_device(tbe_string_directory *d, const uint8_t *d_bytes, uint64_t n_bytes,

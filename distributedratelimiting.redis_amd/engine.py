@@ -173,7 +173,8 @@ class TokenBucketEngine:
         a, b, c = c_uint32(), c_uint32(), c_uint32()
         self._check(self._lib.tbe_layout(self.handle, byref(a), byref(b), byref(c)))
         return {"passes": a.value, "r_bits": b.value, "packed": bool(c.value & 1),
-                "hot": bool(c.value & 2), "pipeline": bool(c.value & 4), "narrow": bool(c.value & 8)}
+                "hot": bool(c.value & 2), "pipeline": bool(c.value & 4), "narrow": bool(c.value & 8),
+                "medium": bool(c.value & 16)}
 
     def stage_times(self) -> dict:
         out = (c_double * len(_capi.STAGES))()

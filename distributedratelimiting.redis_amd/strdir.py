@@ -73,8 +73,11 @@ class HostStringDirectory:
 class StringDirectory:
     """The device string directory of one limiter (prefix = its InstanceName)."""
 
+    MODES = {"auto": 0, "full": 1, "warm": 2}
+
     def __init__(self, capacity: int, arena_bytes: int, prefix: str = "", device: int = -1,
-                 hash_bits: int = None):
+                 hash_bits: int = None, mode: str = "auto"):
+        """mode: the assign path (tbe_sdir_set_mode): "auto" (default), "full", "warm"."""
         import ctypes
         from . import _capi
         self._lib = _capi.load()
@@ -89,6 +92,13 @@ class StringDirectory:
             st = self._lib.tbe_sdir_set_hash_bits(self._h, int(hash_bits))
             if st != _capi.TBE_OK:
                 raise _capi.TbeError(st, "tbe_sdir_set_hash_bits failed")
+        self.set_mode(mode)
+
+    def set_mode(self, mode: str) -> None:
+        from . import _capi
+        st = self._lib.tbe_sdir_set_mode(self._h, self.MODES[mode])
+        if st != _capi.TBE_OK:
+            raise _capi.TbeError(st, "tbe_sdir_set_mode failed")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

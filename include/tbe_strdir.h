@@ -66,6 +66,14 @@ tbe_status tbe_sdir_size(tbe_string_directory *dir, uint64_t *n_ids);
  * min(len, cap) bytes to buf.  TBE_EINVAL for an id never assigned.  Synchronises. */
 tbe_status tbe_sdir_key_of(tbe_string_directory *dir, uint64_t id, uint8_t *buf, uint64_t cap, uint64_t *len);
 
+/* Assign path: 0 = automatic (default), 1 = full pass, 2 = warm path.  The warm path first
+ * resolves every string of the batch that is already known (one lookup pass: hash,
+ * probe, byte compare with the stored text) and runs the assign passes over the misses
+ * only, listed in arrival order; automatic takes it while the last batch whose id count
+ * has come back brought new keys for less than half of its requests.  Ids, errors and
+ * the directory's state are the same on either path. */
+tbe_status tbe_sdir_set_mode(tbe_string_directory *dir, int32_t mode);
+
 /* Test hook: keep only the low `bits` (1..62) bits of every string hash, so that distinct
  * strings share hashes often and the byte comparison and re-probe rounds run.  Ids do not
  * change (they depend only on first occurrence).  Only before the first assign. */

@@ -170,3 +170,30 @@ def test_strings_to_decisions(engine_lib, gpu):
             assert np.array_equal(ids.cpu().numpy().view(np.uint64), hid), b
             g_ref, r_ref = ref.acquire_batch(hid, p, t)
             assert np.array_equal(g.cpu().numpy(), g_ref) and np.array_equal(r.cpu().numpy(), r_ref), b
+
+
+@pytest.mark.parametrize("mode", ["full", "warm", "auto"])
+@pytest.mark.parametrize("hash_bits", [None, 22])
+def test_assign_paths_match_host(engine_lib, gpu, mode, hash_bits):
+    """The full pass, the warm path (lookup of the known strings, assign passes over the
+    misses only) and the automatic choice give the host mirror's ids batch after batch:
+    a cold batch, batches mostly known, a batch of only known strings, one of only new
+    strings; with full hashes and with hashes cut to 22 bits (hundreds of shared tags, so
+    misses re-probe, while no string collides in all four rounds)."""
+    from distributedratelimiting.redis_amd.strdir import HostStringDirectory, StringDirectory, to_device
+    rng = np.random.default_rng(5 + (hash_bits or 0))
+    pool = [b"res/%06d/" % j + bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
+            for j in range(50_000)]
+    with _side_stream(gpu):
+        d = StringDirectory(100_000, 8 << 20, prefix="gw:", device=0, hash_bits=hash_bits, mode=mode)
+        h = HostStringDirectory(100_000)
+        plan = [(0, 20_000), (0, 25_000), (0, 26_000), (0, 26_000), (30_000, 40_000), (0, 50_000)]
+        for b, (lo, hi) in enumerate(plan):
+            s = [pool[k] for k in rng.integers(lo, hi, 30_000)]
+            buf, offs, nb = to_device(s, gpu)
+            ids = d.assign(buf, offs, nb).cpu().numpy().view(np.uint64)
+            assert np.array_equal(ids, h.assign(s)), (mode, b)
+        assert d.size() == h.size()
+        s = [pool[k] for k in rng.integers(0, 50_000, 5_000)]
+        buf, offs, nb = to_device(s, gpu)
+        assert np.array_equal(d.lookup(buf, offs, nb).cpu().numpy().view(np.uint64), h.lookup(s))

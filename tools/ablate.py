@@ -14,15 +14,22 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTDIR = os.path.join(ROOT, "tools", "ablate_libs")
-VARIANTS = {
-    # name: (build defines, extra bench args)
-    "base_z": ([], ["--workload", "zipf"]),
-    "ws7_z": (["TBE_WIDE_MIN_SHIFT=7"], ["--workload", "zipf"]),
-    "ws11_z": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "zipf"]),
-    "base_t": ([], ["--workload", "testapp"]),
-    "ws11_t": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "testapp"]),
-    "ws1_t": (["TBE_WIDE_MIN_SHIFT=1"], ["--workload", "testapp"]),
+VARIANT_SETS = {
+    "queue": {
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
+        "r1only_q": (["TBE_Q_R1_ONLY"], ["--workload", "queue", "--no-drain-variant"]),
+        "sepTick_q": ([], ["--workload", "queue", "--no-drain-variant", "--no-fuse-tick"]),
+    },
+    "uniform": {
+        "base_u": ([], ["--workload", "uniform"]),
+        "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
+        "wb768_u": (["TBE_WIDE_BLOCK=768", "TBE_WIDE_PER=2"], ["--workload", "uniform"]),
+        "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform"]),
+    },
 }
+# name: (build defines, extra bench args); ABLATE_SET picks the set (default: queue)
+VARIANTS = VARIANT_SETS[os.environ.get("ABLATE_SET", "queue")]
 
 
 def build():

@@ -12,5 +12,5 @@ if [ -n "${TESTS:-}" ]; then
     timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/${TAG}_tests.log" 2>&1
     rc=$?; tail -3 "$OUT/${TAG}_tests.log"; [ $rc -ne 0 ] && exit $rc
 fi
-timeout -k 10 900 python -u tools/ablate.py --run --rounds ${ROUNDS:-1} --steps ${STEPS:-10} > "$OUT/${TAG}_ablate.log" 2>&1
+timeout -k 10 900 env ABLATE_SET=${ABLATE_SET:-queue} python -u tools/ablate.py --run --rounds ${ROUNDS:-1} --steps ${STEPS:-10} > "$OUT/${TAG}_ablate.log" 2>&1
 rc=$?; grep -E "^[0-9] |FAILED" "$OUT/${TAG}_ablate.log" | cut -c1-600; exit $rc
