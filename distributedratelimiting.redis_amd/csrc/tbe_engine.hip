@@ -1963,7 +1963,14 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
     }
     uint32_t tail = head + cnt;                                // Q:117-132
     if (tail >= Q.cap) tail -= Q.cap;
-#if !defined(TBE_Q_NO_RING_WRITE)
+#if defined(TBE_Q_RING_SECTOR_AB)
+    {   // A/B timing only (wrong queues): a whole aligned 32-byte sector per enqueue, so
+        // the store needs no read-modify-write below L2
+        typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+        const uint64_t v = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
+        *reinterpret_cast<u64x4 *>(kr + (tail & ~3u)) = u64x4{v, v, v, v};
+    }
+#elif !defined(TBE_Q_NO_RING_WRITE)
     kr[tail] = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
 #else
     (void)kr;   // A/B timing only (wrong queues): the cost of the ring stores
@@ -2084,7 +2091,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     __shared__ __attribute__((aligned(16))) uint64_t qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
     __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
-    __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];
+    __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];    // rows modified (smod)
+    __shared__ uint32_t hdirty[(1 << kMaxRBits) / 32];   // queue headers modified (hmod)
 #if TBE_Q_WALK
     __shared__ uint16_t wsorted[kQChunk];         // the chunk's request indices by row
     __shared__ uint32_t wsum_q[kQBlock / 64];
@@ -2138,6 +2146,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     for (uint32_t j = tid; j < (R + 31) / 32; j += kQBlock) {
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
+        hdirty[j] = 0;
     }
     lds_dma_wait();    // this wave's slice and header DMA landed
     __syncthreads();
@@ -2267,7 +2276,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 }
                 if (smod) slot[j] = st;
                 if (hmod) qh[j] = h;
-                if (smod || hmod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+                if (smod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+                if (hmod) atomicOr(&hdirty[j >> 5], 1u << (j & 31));
             }
             __syncthreads();   // the chunk's rows are settled before the next chunk reads them
             continue;
@@ -2302,7 +2312,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
                 if (hmod) qh[kl[r]] = h;
-                if (smod || hmod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                if (smod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
+                if (hmod) atomicOr(&hdirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
             pend &= ~won;
 #ifdef TBE_Q_R1_ONLY
@@ -2350,15 +2361,19 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 at += g;
                 if (smod) slot[j] = st;
                 if (h != h0) qh[j] = h;
-                if (smod || h != h0) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+                if (smod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
+                if (h != h0) atomicOr(&hdirty[j >> 5], 1u << (j & 31));
             }
         }
         __syncthreads();
     }
-    // dense: whole dirty lines of rows (8 per line) and of headers (16 per line)
+    // dense: whole dirty lines of rows (8 per line) and of headers (16 per line).  Rows and
+    // headers keep separate dirty bits: in config D's steady state nearly every request
+    // queues or fails, which changes a header but not the row, and one shared bit wrote
+    // the whole 1.6 GB row table back every batch.
     for (uint32_t j = tid; j < nrows; j += kQBlock) {
         if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
-        if (dense ? ((dirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(dirty, j)) ST_U(hrows + j, qh[j]);
+        if (dense ? ((hdirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(hdirty, j)) ST_U(hrows + j, qh[j]);
     }
 }
 

@@ -21,6 +21,11 @@ VARIANT_SETS = {
         "r1only_q": (["TBE_Q_R1_ONLY"], ["--workload", "queue", "--no-drain-variant"]),
         "sepTick_q": ([], ["--workload", "queue", "--no-drain-variant", "--no-fuse-tick"]),
     },
+    "ring": {
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
+        "sector_q": (["TBE_Q_RING_SECTOR_AB"], ["--workload", "queue", "--no-drain-variant"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
