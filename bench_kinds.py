@@ -51,7 +51,7 @@ def _pmc_traffic(workload, kernels):
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f).get("workloads", {}).get(workload, {})
+            d = json.load(f).get("workloads", {}).get(workload, {}).get("kernels", {})
     except (OSError, ValueError):
         return None
     v = [d[k]["hbm_bytes_per_launch"] for k in kernels if "hbm_bytes_per_launch" in d.get(k, {})]
@@ -61,9 +61,9 @@ def _pmc_traffic(workload, kernels):
 PMC_KERNELS = {
     ("queue", "fold"): ["k_fold_q<true>"],
     ("queue", "drain"): ["k_drain"],
-    ("queue", "scatter"): ["k_scatter_rec<true, false, true>", "k_scatter_rec<false, false, true>"],
-    ("approx", "fold"): ["k_fold_a"],
-    ("approx", "scatter"): ["k_scatter<unsigned long, true, false>", "k_scatter<unsigned int, true, false>"],
+    ("queue", "scatter"): ["k_scatter_rec<true, false, true, false>", "k_scatter_rec<false, false, true, false>"],
+    ("approx", "fold"): ["k_fold_a<true>"],
+    ("approx", "scatter"): ["k_scatter_rec<true, false, false, true>", "k_scatter_rec<false, false, false, false>"],
 }
 
 
@@ -91,7 +91,8 @@ def _step_roofline(line, alg, note, workload):
               "step_frac": round(achieved / HBM_PEAK_GBS, 4)})
     try:
         with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")) as f:
-            r["step_traffic"] = json.load(f).get("step_hbm_bytes", {}).get(workload)
+            st = json.load(f).get("workloads", {}).get(workload, {}).get("step_hbm_bytes")
+        r["step_traffic"] = round(st, 1) if st is not None else None
     except (OSError, ValueError):
         r["step_traffic"] = None
 

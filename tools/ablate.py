@@ -26,6 +26,11 @@ VARIANT_SETS = {
         "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
         "sector_q": (["TBE_Q_RING_SECTOR_AB"], ["--workload", "queue", "--no-drain-variant"]),
     },
+    "fold": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
