@@ -2069,6 +2069,17 @@ struct QTick {
 #if TBE_Q_WALK
 constexpr uint32_t kWalkMax = 32;   // longest per-key run a walking thread sorts
 #endif
+// Tail walk (round 3): after the first owner round, the requests still pending (a key's
+// second, third, ... request of the chunk; about a third of config D's) are sorted by row
+// in LDS and each row's run is decided by one thread in arrival order -- no further
+// workgroup-wide rounds.  Taken when at most kQTail requests are pending and no row has
+// more than kQTailRun of them; otherwise the rounds go on.  Same decisions as the rounds:
+// each key's requests are still taken in arrival order, and keys are independent.
+#ifndef TBE_Q_TAIL_WALK
+#define TBE_Q_TAIL_WALK 1
+#endif
+constexpr uint32_t kQTail = kQBlock;     // one pending request per thread at most
+constexpr uint32_t kQTailRun = 32;       // longest run a walking thread sorts and decides
 
 // WaitAsyncCore (Q:67-134) for every request of one bucket, in arrival order per key:
 // the same bucket/chunk/owner-round structure as k_fold, plus the key's queue header in
@@ -2093,6 +2104,15 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
     __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];    // rows modified (smod)
     __shared__ uint32_t hdirty[(1 << kMaxRBits) / 32];   // queue headers modified (hmod)
+#if TBE_Q_TAIL_WALK
+    __shared__ uint32_t tw_e[kQTail];             // row | chunk index << 16
+    __shared__ int32_t tw_pm[kQTail];
+    __shared__ int64_t tw_ts[kQTail];
+    __shared__ uint32_t tw_ai[kQTail];
+    __shared__ uint16_t tw_sorted[kQTail];        // tail entries by row
+    __shared__ uint32_t tw_sum[kQBlock / 64];
+    __shared__ uint32_t tw_max;
+#endif
 #if TBE_Q_WALK
     __shared__ uint16_t wsorted[kQChunk];         // the chunk's request indices by row
     __shared__ uint32_t wsum_q[kQBlock / 64];
@@ -2318,6 +2338,123 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             pend &= ~won;
 #ifdef TBE_Q_R1_ONLY
             pend = 0;   // A/B timing only (wrong replies): the cost of the rounds after round 1
+#endif
+#if TBE_Q_TAIL_WALK
+            if (round == 1) {
+                uint32_t n_tail;
+                const uint32_t at0 = block_excl_scan<kQBlock>(__popc(pend), tw_sum, &n_tail);
+                if (n_tail == 0) break;                       // block-uniform
+                if (n_tail <= kQTail) {
+                    // the pending requests, compacted (entry i = the i-th pending request)
+                    uint32_t at = at0;
+#pragma unroll
+                    for (int r = 0; r < kQItems; ++r) {
+                        if (pend & (1u << r)) {
+                            tw_e[at] = kl[r] | ((uint32_t)(r * kQBlock + tid) << 16);
+                            tw_pm[at] = pm[r];
+                            tw_ts[at] = ts[r];
+                            tw_ai[at] = ai[r];
+                            ++at;
+                        }
+                    }
+                    for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;   // round-1 tags are read
+                    if (tid == 0) tw_max = 0;
+                    __syncthreads();
+                    // counting sort by row: rank within the row, row starts, placement
+                    const bool te = (uint32_t)tid < n_tail;
+                    uint32_t trow = 0, trk = 0;
+                    if (te) {
+                        trow = tw_e[tid] & 0xFFFFu;
+                        trk = atomicAdd(&own[trow], 1u);
+                    }
+                    __syncthreads();
+                    {
+                        constexpr uint32_t RPT = (kMaxRows + kQBlock - 1) / kQBlock;
+                        uint32_t cn[RPT], sum = 0, mx = 0;
+#pragma unroll
+                        for (uint32_t u = 0; u < RPT; ++u) {
+                            const uint32_t j = tid * RPT + u;
+                            cn[u] = j < R ? own[j] : 0u;
+                            sum += cn[u];
+                            mx = cn[u] > mx ? cn[u] : mx;
+                        }
+                        uint32_t tot;
+                        uint32_t st0 = block_excl_scan<kQBlock>(sum, tw_sum, &tot);
+#pragma unroll
+                        for (uint32_t u = 0; u < RPT; ++u) {
+                            const uint32_t j = tid * RPT + u;
+                            if (j < R) own[j] = st0;
+                            st0 += cn[u];
+                        }
+                        if (mx) atomicMax(&tw_max, mx);
+                    }
+                    __syncthreads();
+                    if (te) tw_sorted[own[trow] + trk] = (uint16_t)tid;
+                    __syncthreads();
+                    if (tw_max <= kQTailRun) {
+                        // thread t takes sorted position t; the first position of a row's run
+                        // walks the run
+                        if (te) {
+                            const uint32_t e0 = tw_sorted[tid];
+                            const uint32_t row = tw_e[e0] & 0xFFFFu;
+                            const uint32_t start = own[row];
+                            if ((uint32_t)tid == start) {
+                                const uint32_t stop = (row + 1 < R) ? own[row + 1] : n_tail;
+                                // arrival order inside the run (insertion sort by chunk index)
+                                for (uint32_t x = start + 1; x < stop; ++x) {
+                                    const uint16_t v = tw_sorted[x];
+                                    const uint32_t vl = tw_e[v] >> 16;
+                                    uint32_t y = x;
+                                    while (y > start && (tw_e[tw_sorted[y - 1]] >> 16) > vl) {
+                                        tw_sorted[y] = tw_sorted[y - 1];
+                                        --y;
+                                    }
+                                    tw_sorted[y] = v;
+                                }
+                                Slot st = slot[row];
+                                uint64_t h = qh[row];
+                                bool smod = false, hmod = false;
+                                uint64_t *__restrict__ kr = ring + (row0 + row) * (uint64_t)Q.cap;
+                                for (uint32_t x = start; x < stop; ++x) {
+                                    const uint32_t en = tw_sorted[x];
+                                    uint32_t status, rem;
+                                    bool evaluated;
+                                    const ReqTime rq1 = req_time_rel(tw_ts[en], TB, P.ttl_ms);
+                                    q_step(st, h, smod, hmod, tw_pm[en], rq1, TB, tw_ai[en], kr, P, Q, ev_cause, ev_id,
+                                           ev_count, ev_cap, status, rem, evaluated);
+                                    put_wait(res, c + (tw_e[en] >> 16), status, evaluated, rem, narrow);
+                                }
+                                if (smod) {
+                                    slot[row] = st;
+                                    atomicOr(&dirty[row >> 5], 1u << (row & 31));
+                                }
+                                if (hmod) {
+                                    qh[row] = h;
+                                    atomicOr(&hdirty[row >> 5], 1u << (row & 31));
+                                }
+                            }
+                        }
+                        __syncthreads();   // the chunk's rows are settled before the next chunk
+                        break;             // block-uniform (tw_max)
+                    }
+                    // a long run: the rounds go on from the list (the round-1 registers of the
+                    // pending requests are reloaded, so they need not live through the walk;
+                    // own[] holds row starts < 2 << 12, below every tag of round 2 on)
+                    {
+                        uint32_t at1 = at0;
+#pragma unroll
+                        for (int r = 0; r < kQItems; ++r) {
+                            if (pend & (1u << r)) {
+                                kl[r] = tw_e[at1] & 0xFFFFu;
+                                pm[r] = tw_pm[at1];
+                                ts[r] = tw_ts[at1];
+                                ai[r] = tw_ai[at1];
+                                ++at1;
+                            }
+                        }
+                    }
+                }
+            }
 #endif
             if (!__syncthreads_or(pend != 0)) break;
         }

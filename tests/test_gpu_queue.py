@@ -53,6 +53,32 @@ def test_wait_and_refresh(engine_lib, gpu, order, n_keys, qlimit, n, rounds):
     assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
 
 
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("hot_share", [0.0, 0.01, 0.08, 0.5])
+def test_tail_paths(engine_lib, gpu, order, hot_share):
+    # k_fold_q after the first owner round (DESIGN.md §5 "tail walk"): few pending requests
+    # and short runs take the walk; one key with tens to hundreds of requests per chunk
+    # takes the rounds from the compacted list; more pending requests than threads keep
+    # the register rounds.  Uniform keys plus one hot key at the given share.
+    rng = np.random.default_rng(int(hot_share * 1000) + 7 * order)
+    n_keys, n = 6000, 40_000
+    eng, ref = pair(n_keys, 4, 1, 10_000_000, 16, order)
+    t, rid = S_US, 0
+    for _ in range(3):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        keys[rng.random(n) < hot_share] = 1234
+        permits = rng.choice([0, 1, 1, 2, 3, 5], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        check_round(eng, ref, keys, permits, ts, rid)
+        rid += n
+        t += 2_000_000
+        k1, i1, r1 = eng.refresh(t)
+        k2, i2, r2 = ref.refresh(t)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+    for k in [1234] + list(range(40)):
+        assert eng.queue_of(k) == ref.queue_of(k)
+
+
 def test_config_d_shape_small(engine_lib, gpu):
     # Config D shape: QueueLimit 16, OldestFirst, permits 1, TokenLimit 4, 1 ms batches,
     # demand >> fill so queues saturate; refresh at every batch boundary.

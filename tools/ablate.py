@@ -26,6 +26,16 @@ VARIANT_SETS = {
         "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
         "sector_q": (["TBE_Q_RING_SECTOR_AB"], ["--workload", "queue", "--no-drain-variant"]),
     },
+    "qfold": {
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "r1only_q": (["TBE_Q_R1_ONLY"], ["--workload", "queue", "--no-drain-variant"]),
+        "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
+        "r1noring_q": (["TBE_Q_R1_ONLY", "TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
+    },
+    "qwalk": {
+        "walk_q": ([], ["--workload", "queue"]),
+        "rounds_q": (["TBE_Q_TAIL_WALK=0"], ["--workload", "queue"]),
+    },
     "fold": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
