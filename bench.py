@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from bench_kinds import gather_floats, mark, reduce_max  # noqa: E402
+from bench_kinds import cpu_model, gather_floats, mark, reduce_max  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED_B = 0x5EED000B
@@ -639,7 +639,7 @@ def cpu_baseline(args, n_keys: int, zkeys=(), seed_b: int = SEED_B):
     out = {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
            "sample": f"first {sample} requests of each of {b} {what} batches "
                      f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c single thread",
-           "host_cpus": os.cpu_count()}
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
     if CPU_THREADS > 1 and args.cpu_seconds > 0:
         done_t, spent_t, b_t = timed(CPU_THREADS, min(args.cpu_seconds, 4.0))
         out["sharded"] = {"value": round(done_t / spent_t, 1), "unit": "decisions/s", "cores": CPU_THREADS,

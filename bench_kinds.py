@@ -40,6 +40,18 @@ def _gen(lib, seed, n_keys, s, n, interval_us, dev):
     return k, p, t
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _distinct(n: int, k: int) -> float:
     return k * (1.0 - np.exp(-n / k))
 
@@ -336,7 +348,7 @@ def cpu_queue(args, kl):
     return {"value": round(done / spent, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} requests of each of {b} config-D batches + their ticks "
                       f"({done} decisions, {spent:.1f} s), oracle/tb_ref.c tbrq_* single thread",
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
 
 
 def run_approx(args, lib, dev, world, rank, dist):
@@ -493,4 +505,4 @@ def cpu_approx(args, kshared):
             "sample": f"first {sample} requests of each of {b} config-E batches, each followed by a "
                       f"refresh epoch over all {kshared} keys ({done} decisions, {spent:.1f} s), "
                       f"oracle/tb_ref.c tba_* single thread",
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}

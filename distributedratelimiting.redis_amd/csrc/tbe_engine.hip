@@ -96,7 +96,11 @@ constexpr int kMaxRBits = 11;                          // <= 2048 rows per bucke
 
 // Hot keys (see the "hot keys" section below for how their runs are decided).
 constexpr uint32_t kHotKeysMax = 1024;
-constexpr uint32_t kHotSlots = 4096;             // hash slots: power of two, load <= 1/4
+#ifndef TBE_HOT_SLOT_BITS
+#define TBE_HOT_SLOT_BITS 12
+#endif
+constexpr uint32_t kHotSlots = 1u << TBE_HOT_SLOT_BITS;   // hash slots: power of two, load <= kHotKeysMax / kHotSlots
+static_assert(kHotSlots >= 2 * kHotKeysMax, "hot table load factor <= 1/2");
 constexpr uint32_t kHotEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kHotMin = 2048;               // requests in one batch that make a key hot
 constexpr uint32_t kHotCandMax = 4096;           // nominations kept per batch (the busiest win)
@@ -109,7 +113,7 @@ struct HotSet {
     uint64_t slot[kHotSlots];        // open-addressing hash table: (index << 32) | key
 };
 
-__device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 20; }
+__device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - TBE_HOT_SLOT_BITS); }
 constexpr uint64_t kHotSlotEmpty = 0xFFFFFFFFFFFFFFFFull;
 
 // Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns

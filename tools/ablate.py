@@ -32,6 +32,10 @@ VARIANT_SETS = {
         "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
         "r1noring_q": (["TBE_Q_R1_ONLY", "TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-drain-variant"]),
     },
+    "hot": {
+        "slots4096_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "slots2048_z": (["TBE_HOT_SLOT_BITS=11"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "qwalk": {
         "walk_q": ([], ["--workload", "queue"]),
         "rounds_q": (["TBE_Q_TAIL_WALK=0"], ["--workload", "queue"]),
