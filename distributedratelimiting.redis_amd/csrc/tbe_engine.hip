@@ -118,13 +118,24 @@ constexpr uint64_t kHotSlotEmpty = 0xFFFFFFFFFFFFFFFFull;
 
 // Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns
 // whether any key is hot.
+// TBE_HOT_PROBE_GLOBAL (A/B): no LDS copy; the probes read the table through the caches.
+#ifndef TBE_HOT_PROBE_GLOBAL
+#define TBE_HOT_PROBE_GLOBAL 0
+#endif
+constexpr uint32_t kHotLds = TBE_HOT_PROBE_GLOBAL ? 1u : kHotSlots;   // LDS copy of the table
 template <int BLOCK>
 __device__ __forceinline__ bool hot_load(const HotSet *__restrict__ hot, uint64_t *slots) {
     const bool any = hot != nullptr && hot->count != 0;
+#if !TBE_HOT_PROBE_GLOBAL
     if (any)
         for (int j = threadIdx.x; j < (int)kHotSlots; j += BLOCK) slots[j] = hot->slot[j];
     __syncthreads();
+#endif
     return any;
+}
+// The table the probes read: the workgroup's LDS copy, or the global table itself.
+__device__ __forceinline__ const uint64_t *hot_table(const HotSet *__restrict__ hot, const uint64_t *lds) {
+    return TBE_HOT_PROBE_GLOBAL ? hot->slot : lds;
 }
 
 // Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
@@ -194,7 +205,7 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
     __shared__ uint32_t h8[kDigits * 8];
     __shared__ uint32_t tile_lo[2];
     static_assert(kHBlock == 2 * kDigits && kDigits * 8 == 4 * kHBlock, "two threads per digit; 4 counters each");
-    __shared__ uint64_t hs[HOT ? kHotSlots : 1];
+    __shared__ uint64_t hs[HOT ? kHotLds : 1];
     const int tid = threadIdx.x;
     const bool dig = tid < kDigits;                  // this thread owns digit `tid`'s totals
     const bool any_hot = HOT && hot_load<kHBlock>(hot, hs);
@@ -236,7 +247,7 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
         const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
         uint32_t skv[kHItems];
         if (HOT && any_hot) {
-            hot_sortkeys<kHItems>(kv, hs, nb, r_bits, skv);
+            hot_sortkeys<kHItems>(kv, hot_table(hot, hs), nb, r_bits, skv);
         } else {
 #pragma unroll
             for (int it = 0; it < kHItems; ++it) skv[it] = (uint32_t)((uint64_t)kv[it] & kmask);
@@ -598,7 +609,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
-    __shared__ uint64_t hs[HOT ? kHotSlots : 1];
+    __shared__ uint64_t hs[HOT ? kHotLds : 1];
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
     const int tid = threadIdx.x;
@@ -627,7 +638,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         const int64_t tbase = NOTS ? 0 : pack_base(tin, F);
         uint32_t skv[kPartItems];
         if (HOT && any_hot) {
-            hot_sortkeys<kPartItems>(kv, hs, nb, r_bits, skv);
+            hot_sortkeys<kPartItems>(kv, hot_table(hot, hs), nb, r_bits, skv);
         } else {
 #pragma unroll
             for (int it = 0; it < kPartItems; ++it) skv[it] = (uint32_t)(kv[it] & F.kmask);
@@ -794,6 +805,14 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 // fold them faster than k_fold's 12 (config C fold 0.89 -> 0.69 ms; R/2 .. R/2048 measured,
 // profiles/r02_ablate_wide_threshold*.log)
 constexpr int kWideMinShift = TBE_WIDE_MIN_SHIFT;
+// Tail walk (round 3, as k_fold_q's): the requests still pending after round 1 are
+// counting-sorted by row and each row's run is decided by one thread in arrival order,
+// instead of further workgroup-wide speculative rounds; runs longer than kWideTailRun keep
+// the rounds.
+#ifndef TBE_WIDE_TAIL_WALK
+#define TBE_WIDE_TAIL_WALK 1
+#endif
+constexpr uint32_t kWideTailRun = 32;
 static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and tail list");
 // The rows' field t (TB:203 of the stored t_us): cached in LDS, or derived per evaluation
 #if TBE_WIDE_FT
@@ -832,6 +851,10 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t loaded[kMaxRows / 32];
     __shared__ uint32_t dirty[kMaxRows / 32];
+#if TBE_WIDE_TAIL_WALK
+    __shared__ uint16_t tw_sorted[kWideTail];   // tail entries by row
+    __shared__ uint32_t tw_max;
+#endif
 
     if (*err) return;
     const int tid = threadIdx.x;
@@ -1032,6 +1055,77 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             pend = 0;
             __syncthreads();
             bool tp = (uint32_t)tid < n_tail;
+#if TBE_WIDE_TAIL_WALK
+            // counting sort of the list by row (own[] is free: round 1's tags were read
+            // before the scan above), then one walking thread per row's run
+            for (uint32_t j = tid; j < R; j += kWideBlock) own[j] = 0;
+            if (tid == 0) tw_max = 0;
+            __syncthreads();
+            uint32_t trow = 0, trk = 0;
+            if (tp) {
+                trow = t_kl_lid[tid] & 0xFFFFu;
+                trk = atomicAdd(&own[trow], 1u);
+            }
+            __syncthreads();
+            {
+                constexpr uint32_t RPT = (kMaxRows + kWideBlock - 1) / kWideBlock;
+                uint32_t cn[RPT], sum = 0, mx = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < RPT; ++u) {
+                    const uint32_t j = tid * RPT + u;
+                    cn[u] = j < R ? own[j] : 0u;
+                    sum += cn[u];
+                    mx = cn[u] > mx ? cn[u] : mx;
+                }
+                uint32_t tot;
+                uint32_t st0 = block_excl_scan<kWideBlock>(sum, wsum, &tot);
+#pragma unroll
+                for (uint32_t u = 0; u < RPT; ++u) {
+                    const uint32_t j = tid * RPT + u;
+                    if (j < R) own[j] = st0;
+                    st0 += cn[u];
+                }
+                if (mx) atomicMax(&tw_max, mx);
+            }
+            __syncthreads();
+            if (tp) tw_sorted[own[trow] + trk] = (uint16_t)tid;
+            __syncthreads();
+            if (tw_max <= kWideTailRun) {
+                if (tp) {
+                    const uint32_t rw = t_kl_lid[tw_sorted[tid]] & 0xFFFFu;
+                    const uint32_t start = own[rw];
+                    if ((uint32_t)tid == start) {
+                        const uint32_t stop = (rw + 1 < R) ? own[rw + 1] : n_tail;
+                        for (uint32_t x = start + 1; x < stop; ++x) {   // arrival order
+                            const uint16_t v = tw_sorted[x];
+                            const uint32_t vl = t_kl_lid[v] >> 16;
+                            uint32_t y = x;
+                            while (y > start && (t_kl_lid[tw_sorted[y - 1]] >> 16) > vl) {
+                                tw_sorted[y] = tw_sorted[y - 1];
+                                --y;
+                            }
+                            tw_sorted[y] = v;
+                        }
+                        Slot st = row[rw];
+                        bool mod = false;
+                        for (uint32_t x = start; x < stop; ++x) {
+                            const uint32_t en = tw_sorted[x];
+                            const ReqTime rq1 = PACKED ? req_time_rel(t_ts[en], TB, P.ttl_ms) : req_time(t_ts[en], P.ttl_ms);
+                            bool m;
+                            const uint32_t rp = tb_step_ft(st, WIDE_FT_GET(rw, st), t_pm[en], rq1, P, m);
+                            mod |= m;
+                            put_reply(res, c + (t_kl_lid[en] >> 16), rp, narrow);
+                        }
+                        if (mod) {
+                            row[rw] = st;
+                            atomicOr(&dirty[rw >> 5], 1u << (rw & 31));
+                        }
+                    }
+                }
+                tp = false;
+                n_tail = 0;    // block-uniform: skip the rounds below
+            }
+#endif
             uint32_t tkl = 0, tlid = 0, trep = 0;
             int32_t tpm = 0;
             int64_t tts = 0;
@@ -1049,6 +1143,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             // later rounds run on fewer waves (the fold is VALU-issue bound).
             uint32_t in_use = n_tail;
             for (uint32_t round = 2;; ++round) {
+                if (n_tail == 0) break;   // block-uniform: the tail walk settled the list
                 const uint32_t tag = (round << 12) | (4095u - tlid);
                 Slot nr = Slot{0.0, 0};
                 if (tp) {
@@ -3418,16 +3513,18 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
-        k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
-            nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
+        if (((1u << e->r_bits) >> kWideMinShift) > 1u)   // else k_fold_wide takes every bucket
+            k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
+                nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
     } else {
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
             e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
-        k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
-            sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
+        if (((1u << e->r_bits) >> kWideMinShift) > 1u)
+            k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
+                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
+                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {

@@ -43,7 +43,7 @@ def run(n_keys, cap, tokens, period, batches, narrow=True, p_choices=(1,), sprea
 
 
 @pytest.mark.parametrize("case", ["config_b_like", "small_rows", "busy_rows", "partial_last", "mixed_permits",
-                                  "fast_refill_wide", "skew_hot", "jitter_expiry"])
+                                  "fast_refill_wide", "skew_hot", "jitter_expiry", "tail_long_run"])
 def test_fold_shapes(engine_lib, gpu, case):
     if case == "config_b_like":      # R = 2048, ~1400 requests per bucket: all full
         run(3_000_000, 10, 1, 10_000_000, [1 << 21] * 3)
@@ -59,6 +59,10 @@ def test_fold_shapes(engine_lib, gpu, case):
         run(400_000, 1000, 40_000, 10_000_000, [350_000] * 3, narrow=False, p_choices=(1, 7, 50))
     elif case == "skew_hot":         # a few keys take 30%: their buckets go multi-chunk
         run(1_000_000, 10, 1, 10_000_000, [600_000] * 4, skew=0.3)
+    elif case == "tail_long_run":    # 4 keys with ~60 requests each in config-B-like buckets:
+        # after round 1 their runs exceed the tail walk's 32 (the rounds over the sorted list
+        # take them) while every other bucket's tail is walked
+        run(3_000_000, 10, 1, 10_000_000, [1 << 21] * 3, skew=240 / (1 << 21))
     elif case == "jitter_expiry":    # unsorted timestamps, TTL 3 s, batches 4 s apart
         run(300_000, 5, 2, 10_000_000, [250_000] * 4, spread_us=4_000_000, ts_jitter=900_000,
             p_choices=(0, 1, 3, 6))

@@ -35,6 +35,12 @@ VARIANT_SETS = {
     "hot": {
         "slots4096_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "slots2048_z": (["TBE_HOT_SLOT_BITS=11"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "wideall_z": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "gprobe_z": (["TBE_HOT_PROBE_GLOBAL=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "wideall_u": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "qwalk": {
         "walk_q": ([], ["--workload", "queue"]),
