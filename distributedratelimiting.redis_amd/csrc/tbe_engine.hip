@@ -798,21 +798,28 @@ constexpr int kWidePer = TBE_WIDE_PER;
 constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_WIDE_MIN_SHIFT
-#define TBE_WIDE_MIN_SHIFT 5
+#define TBE_WIDE_MIN_SHIFT 11
 #endif
-// k_fold_wide takes buckets of >= R >> kWideMinShift requests (64 of 2048 rows): on a Zipf
-// slice, whose buckets hold fewer requests once the hot keys run apart, its 24 waves per CU
-// fold them faster than k_fold's 12 (config C fold 0.89 -> 0.69 ms; R/2 .. R/2048 measured,
-// profiles/r02_ablate_wide_threshold*.log)
+// k_fold_wide takes buckets of >= R >> kWideMinShift requests: on a Zipf slice, whose
+// buckets hold fewer requests once the hot keys run apart, its 24 waves per CU fold them
+// faster than k_fold's 12 (round 2, R/32: config C fold 0.89 -> 0.69 ms; R/2 .. R/2048
+// measured, profiles/r02_ablate_wide_threshold*.log).  Round 3: every nonempty bucket
+// (R >> 11 = 1 at the largest buckets), and k_fold is then not launched at all -- its
+// 48828 workgroups that only read their bucket bounds and exit cost 0.03 ms per batch
+// (fold 0.76 -> 0.73 ms on Zipf, 0.89 -> 0.86 on uniform, profiles/r03_ablate_hot_wide_walk.log).
 constexpr int kWideMinShift = TBE_WIDE_MIN_SHIFT;
-// Tail walk (round 3, as k_fold_q's): the requests still pending after round 1 are
-// counting-sorted by row and each row's run is decided by one thread in arrival order,
+// Tail walk (round 3, as k_fold_q's; A/B only): the requests still pending after round 1
+// are counting-sorted by row and each row's run is decided by one thread in arrival order,
 // instead of further workgroup-wide speculative rounds; runs longer than kWideTailRun keep
-// the rounds.
+// the rounds.  Slower here (config B fold 0.77 -> 0.88 ms, Zipf 0.67 -> 0.76,
+// profiles/r03_ablate_hot_wide_walk.log): a speculative round settles most of the tail at
+// once, while the sort's barriers and the serial FP64 chains of the walkers do not pay off.
 #ifndef TBE_WIDE_TAIL_WALK
-#define TBE_WIDE_TAIL_WALK 1
+#define TBE_WIDE_TAIL_WALK 0
 #endif
+#if TBE_WIDE_TAIL_WALK
 constexpr uint32_t kWideTailRun = 32;
+#endif
 static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and tail list");
 // The rows' field t (TB:203 of the stored t_us): cached in LDS, or derived per evaluation
 #if TBE_WIDE_FT
@@ -1122,6 +1129,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                         }
                     }
                 }
+                // the walkers' rows, replies and their reads of own[] are done before the
+                // next chunk resets own[] and reads the rows
+                __syncthreads();
                 tp = false;
                 n_tail = 0;    // block-uniform: skip the rounds below
             }
