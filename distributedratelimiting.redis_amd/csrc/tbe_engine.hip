@@ -156,6 +156,12 @@ __device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *sl
 template <int N, typename KeyT>
 __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t *slots, uint32_t nb,
                                              int r_bits, uint32_t (&sk)[N]) {
+#ifdef TBE_HOT_NOPROBE_AB
+    // A/B timing only (wrong partition): the cost of the hot-set probes
+#pragma unroll
+    for (int it = 0; it < N; ++it) sk[it] = (uint32_t)kv[it] ^ ((uint32_t)slots[it & 7] & 1u);
+    return;
+#endif
     uint64_t v[N];
 #pragma unroll
     for (int it = 0; it < N; ++it) v[it] = slots[hot_hash((uint32_t)kv[it])];
