@@ -42,6 +42,12 @@ VARIANT_SETS = {
         "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "hidx": {
+        "hidx_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "probe_z": (["TBE_HOT_HIDX=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "hidx_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "probe_u": (["TBE_HOT_HIDX=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+    },
     "probe": {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "noprobe_z": (["TBE_HOT_NOPROBE_AB"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
