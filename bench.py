@@ -183,6 +183,8 @@ def main():
     if args.workload in ("queue", "approx"):
         import bench_kinds
         line = bench_kinds.run(args, lib, dev, world, rank, dist)
+        if args.share_device:
+            line["rehearsal"] = REHEARSAL_NOTE
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist:

@@ -1,5 +1,6 @@
 """bench.py's workload table and its algorithmic-byte model,
 checked without a GPU."""
+import json
 import os
 import sys
 
@@ -85,3 +86,25 @@ def test_gpus_n_spawns_n_ranks():
     p = _bench(["--gpus", "2", "--share-device", "--steps", "1", "--warmup", "0"])
     assert p.returncode != 0 and not p.stdout.strip()
     assert "bench.py: rank 0 of 2" in p.stderr and "bench.py: rank 1 of 2" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("workload", ["uniform", "queue", "approx"])
+def test_gpus_2_rehearsal_on_one_gpu(workload):
+    """The multi-rank bench path as the driver launches it (--gpus 2 spawns two ranks),
+    rehearsed on the one GPU of the test box: both ranks on cuda:0 over gloo, the HIP
+    engine deciding on each, the device path's collectives staged through host memory.
+    One JSON line, for two GPUs' worth of work, marked as a rehearsal."""
+    argv = ["--gpus", "2", "--share-device", "--workload", workload, "--keys", "2000000",
+            "--batch", str(1 << 20), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0",
+            "--no-host-buffer", "--no-strdir"]
+    if workload == "queue":
+        argv.append("--no-drain-variant")
+    p = _bench(argv, timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 2
+    assert "rehearsal" in json.dumps(d)
