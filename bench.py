@@ -312,6 +312,7 @@ def main():
     # stream, pipeline off) of exactly the same warm-up + timed batches on a second engine,
     # right after the timed region; its replies must equal the pipelined run's.
     stages, replay_check = stages_overlapped, None
+    line_read = line_written = None
     if layout.get("pipeline") and not args.no_stage_timing and not raw:
         eng.close()
         ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
@@ -335,10 +336,15 @@ def main():
         # step's B_alg is their mean, not just the last batch's (the table ages from
         # grant- to denial-dominated across the timed batches)
         uw = []
+        lines = []   # 128-byte table lines (8 rows) touched / holding a written row, per batch
         for i, s in enumerate(range(args.warmup, total_steps)):
             k = bufs[s][0]
-            uw.append((int(torch.unique(k).numel()), int(torch.unique(k[g_all[i].bool()]).numel())))
+            kw = k[g_all[i].bool()]
+            uw.append((int(torch.unique(k).numel()), int(torch.unique(kw).numel())))
+            lines.append((int(torch.unique(k // 8).numel()), int(torch.unique(kw // 8).numel())))
         del g_all
+        line_read = float(np.mean([a for a, _ in lines]))
+        line_written = float(np.mean([b for _, b in lines]))
         u_mean = float(np.mean([u for u, _ in uw]))
         w_mean = float(np.mean([w for _, w in uw]))
         step_alg = int(n * 25 + u_mean * 16 + w_mean * 16)
@@ -381,6 +387,18 @@ def main():
                     "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
                                "engine stream" if replay_check is not None else
                                "HIP events on the engine stream over the timed region")}
+        if name == "fold" and line_read is not None:
+            # The fold's floor at the memory's own granularity: a 16-byte row costs its whole
+            # 128-byte line, read if any row of the line is requested and written if any is
+            # granted (nearly every line at config B's key/batch ratio), plus the records and
+            # replies.  SURVEY §8(d) prices 16 B per distinct key instead.
+            line_floor = int(round((line_read + line_written) * 128 +
+                                   n * ((8 if layout["packed"] else 16) + (1 if layout.get("narrow") else 4))))
+            roofline.update({
+                "line_floor_bytes": line_floor,
+                "line_frac": round(line_floor / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "line_note": (f"128 B x (lines read {line_read:.4g} + lines written {line_written:.4g}, "
+                              "per-batch means of the timed batches) + records and replies")})
         if replay_check is not None:
             roofline["overlapped_avg_launch_ms"] = round(
                 stages_overlapped.get(name, 0.0) / (args.steps * launches[name]), 4)

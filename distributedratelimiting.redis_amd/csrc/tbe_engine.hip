@@ -84,8 +84,14 @@ constexpr int kPartItems = TBE_PART_ITEMS;             // elements per thread pe
 constexpr int kTile = kPartBlock * kPartItems;         // 4096 requests per partition tile
 // k_unscatter's own tiles (any size is correct; 8192 keeps each workgroup's gathers in
 // the digit runs of two partition tiles)
-constexpr int kUnBlock = 1024;
-constexpr int kUnItems = 8;
+#ifndef TBE_UN_BLOCK
+#define TBE_UN_BLOCK 1024
+#endif
+#ifndef TBE_UN_ITEMS
+#define TBE_UN_ITEMS 8
+#endif
+constexpr int kUnBlock = TBE_UN_BLOCK;
+constexpr int kUnItems = TBE_UN_ITEMS;
 constexpr int kUnTile = kUnBlock * kUnItems;
 #ifndef TBE_HIST_BLOCKS
 #define TBE_HIST_BLOCKS 1024

@@ -42,6 +42,13 @@ VARIANT_SETS = {
         "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "unscatter": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "b512i16_u": (["TBE_UN_BLOCK=512", "TBE_UN_ITEMS=16"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "b1024i16_u": (["TBE_UN_BLOCK=1024", "TBE_UN_ITEMS=16"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "b256i16_u": (["TBE_UN_BLOCK=256", "TBE_UN_ITEMS=16"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "b512i8_u": (["TBE_UN_BLOCK=512", "TBE_UN_ITEMS=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+    },
     "hidx": {
         "hidx_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "probe_z": (["TBE_HOT_HIDX=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
