@@ -90,7 +90,7 @@ def test_gpus_n_spawns_n_ranks():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("workload", ["uniform", "queue", "approx"])
+@pytest.mark.parametrize("workload", ["uniform", "zipf", "queue", "approx"])
 def test_gpus_2_rehearsal_on_one_gpu(workload):
     """The multi-rank bench path as the driver launches it (--gpus 2 spawns two ranks),
     rehearsed on the one GPU of the test box: both ranks on cuda:0 over gloo, the HIP
@@ -101,6 +101,8 @@ def test_gpus_2_rehearsal_on_one_gpu(workload):
             "--no-host-buffer", "--no-strdir"]
     if workload == "queue":
         argv.append("--no-drain-variant")
+    if workload == "zipf":   # config C's form: one global Zipf stream, hash-sharded to its owners
+        argv[argv.index("--keys") + 1] = "3000000"
     p = _bench(argv, timeout=540)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
