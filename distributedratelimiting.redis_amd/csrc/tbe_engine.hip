@@ -2908,6 +2908,9 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
                     atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                 }
             }
+#ifdef TBE_A_R1_ONLY
+            pend = 0;   // A/B timing only (wrong replies): the cost of the rounds after round 1
+#endif
             if (!__syncthreads_or(pend != 0)) break;
         }
         __syncthreads();

@@ -42,6 +42,16 @@ VARIANT_SETS = {
         "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "afold": {
+        "base_a": ([], ["--workload", "approx"]),
+        "r1only_a": (["TBE_A_R1_ONLY"], ["--workload", "approx"]),
+    },
+    "hist": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "a2w6_u": (["TBE_HIST_AHEAD=2", "TBE_HIST_WAVES=6"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "blk2048_u": (["TBE_HIST_BLOCKS=2048"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "blk512_u": (["TBE_HIST_BLOCKS=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+    },
     "unscatter": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "b512i16_u": (["TBE_UN_BLOCK=512", "TBE_UN_ITEMS=16"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
