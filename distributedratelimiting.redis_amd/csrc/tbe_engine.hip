@@ -2804,79 +2804,6 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
             const uint32_t q = c + r * kFoldBlock + tid;
             return PACKED ? (uint32_t)(srec[q] >> (F.kb + F.pb + 1)) : sidx[q];
         };
-        // One request against its key's local-tier row (A:84-214), shared by the round
-        // winners of every round.
-        auto a_step = [&](ALocal &a, const int32_t p, const uint32_t krow, auto &&arrival_q, uint32_t &status,
-                          bool &modified, bool &evaluated) {
-            modified = false;
-            evaluated = true;
-            const int32_t avail = avail_of(a);
-            if (p > A.token_limit) {                                   // A:87-90 / A:119-122
-                status = TBE_WAIT_REJECTED;
-                evaluated = false;
-            } else if (p == 0 && (avail > 0 || !A.wait)) {            // A:93-102 / A:127-130
-                status = (avail > 0) ? TBE_WAIT_GRANTED : TBE_WAIT_FAILED;
-            } else if (p == 0) {
-                // WaitAsync(0) while throttled: TryLease fails (A:191, availableTokens
-                // != 0) and QueueLimit - _queueCount < 0 never holds (A:141), so the
-                // registration queues with Count 0 (A:166-181) and completes at the
-                // next drain that reaches it (A:474: AvailableTokens >= 0).  The
-                // reference bounds such registrations by nothing; the ring gives each
-                // key zero_slots of them, beyond which the wait fails.
-                if (a.zc < A.zero_slots) {
-                    uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
-                    uint32_t tail = head + cnt;
-                    if (tail >= A.cap) tail -= A.cap;
-                    ring[(row0 + krow) * (uint64_t)A.cap + tail] = (uint64_t)(A.id_base + arrival_q()) << 16;
-                    a.hc = (head & 0xFFFFu) | ((cnt + 1) << 16);
-                    a.zc = (uint16_t)(a.zc + 1);
-                    modified = true;
-                    status = TBE_WAIT_QUEUED;
-                } else {
-                    status = TBE_WAIT_FAILED;
-                }
-            } else if (avail >= p && avail != 0 && (a.qsum == 0 || A.order == 1)) {  // A:191-209
-                a.local = (int32_t)((uint32_t)a.local + (uint32_t)p);
-                modified = true;
-                status = TBE_WAIT_GRANTED;
-            } else if (!A.wait) {
-                status = TBE_WAIT_FAILED;                              // A:111
-            } else {
-                uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
-                uint64_t *__restrict__ kr = ring + (row0 + krow) * (uint64_t)A.cap;
-                bool fail = false;
-                if ((int64_t)A.queue_limit - a.qsum < p) {             // A:141
-                    if (A.order == 1 && p <= A.queue_limit) {          // A:143-158
-                        while ((int64_t)A.queue_limit - a.qsum < p) {
-                            const uint64_t ent = kr[head];
-                            const uint32_t at = atomicAdd(ev_count, 1u);
-                            if (at < ev_cap) {
-                                ev_cause[at] = arrival_q() + A.ai_base;
-                                ev_id[at] = (int64_t)(ent >> 16);
-                            }
-                            a.qsum = (uint16_t)(a.qsum - (uint32_t)(ent & 0xFFFFu));
-                            if ((ent & 0xFFFFu) == 0) a.zc = (uint16_t)(a.zc - 1);   // DequeueHead takes it too
-                            head = (head + 1 == A.cap) ? 0 : head + 1;
-                            --cnt;
-                        }
-                    } else {
-                        fail = true;                                   // A:159-163
-                    }
-                }
-                if (fail) {
-                    status = TBE_WAIT_FAILED;
-                } else {                                               // A:166-181
-                    uint32_t tail = head + cnt;
-                    if (tail >= A.cap) tail -= A.cap;
-                    kr[tail] = ((uint64_t)(A.id_base + arrival_q()) << 16) | (uint32_t)p;
-                    ++cnt;
-                    a.qsum = (uint16_t)(a.qsum + (uint32_t)p);
-                    status = TBE_WAIT_QUEUED;
-                }
-                a.hc = (head & 0xFFFFu) | (cnt << 16);
-                modified = true;
-            }
-        };
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();
         uint32_t mine = 0;
@@ -2911,9 +2838,75 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
                 if (!((pend & (1u << r)) && own[kl[r]] == tag)) continue;
                 pend &= ~(1u << r);
                 ALocal a = sl[kl[r]];
+                const int32_t p = pm[r];
                 uint32_t status;
-                bool modified, evaluated;
-                a_step(a, pm[r], kl[r], [&] { return arrival(r); }, status, modified, evaluated);
+                bool modified = false, evaluated = true;
+                const int32_t avail = avail_of(a);
+                if (p > A.token_limit) {                                   // A:87-90 / A:119-122
+                    status = TBE_WAIT_REJECTED;
+                    evaluated = false;
+                } else if (p == 0 && (avail > 0 || !A.wait)) {            // A:93-102 / A:127-130
+                    status = (avail > 0) ? TBE_WAIT_GRANTED : TBE_WAIT_FAILED;
+                } else if (p == 0) {
+                    // WaitAsync(0) while throttled: TryLease fails (A:191, availableTokens
+                    // != 0) and QueueLimit - _queueCount < 0 never holds (A:141), so the
+                    // registration queues with Count 0 (A:166-181) and completes at the
+                    // next drain that reaches it (A:474: AvailableTokens >= 0).  The
+                    // reference bounds such registrations by nothing; the ring gives each
+                    // key zero_slots of them, beyond which the wait fails.
+                    if (a.zc < A.zero_slots) {
+                        uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
+                        uint32_t tail = head + cnt;
+                        if (tail >= A.cap) tail -= A.cap;
+                        ring[(row0 + kl[r]) * (uint64_t)A.cap + tail] = (uint64_t)(A.id_base + arrival(r)) << 16;
+                        a.hc = (head & 0xFFFFu) | ((cnt + 1) << 16);
+                        a.zc = (uint16_t)(a.zc + 1);
+                        modified = true;
+                        status = TBE_WAIT_QUEUED;
+                    } else {
+                        status = TBE_WAIT_FAILED;
+                    }
+                } else if (avail >= p && avail != 0 && (a.qsum == 0 || A.order == 1)) {  // A:191-209
+                    a.local = (int32_t)((uint32_t)a.local + (uint32_t)p);
+                    modified = true;
+                    status = TBE_WAIT_GRANTED;
+                } else if (!A.wait) {
+                    status = TBE_WAIT_FAILED;                              // A:111
+                } else {
+                    uint32_t head = a.hc & 0xFFFFu, cnt = a.hc >> 16;
+                    uint64_t *__restrict__ kr = ring + (row0 + kl[r]) * (uint64_t)A.cap;
+                    bool fail = false;
+                    if ((int64_t)A.queue_limit - a.qsum < p) {             // A:141
+                        if (A.order == 1 && p <= A.queue_limit) {          // A:143-158
+                            while ((int64_t)A.queue_limit - a.qsum < p) {
+                                const uint64_t ent = kr[head];
+                                const uint32_t at = atomicAdd(ev_count, 1u);
+                                if (at < ev_cap) {
+                                    ev_cause[at] = arrival(r) + A.ai_base;
+                                    ev_id[at] = (int64_t)(ent >> 16);
+                                }
+                                a.qsum = (uint16_t)(a.qsum - (uint32_t)(ent & 0xFFFFu));
+                                if ((ent & 0xFFFFu) == 0) a.zc = (uint16_t)(a.zc - 1);   // DequeueHead takes it too
+                                head = (head + 1 == A.cap) ? 0 : head + 1;
+                                --cnt;
+                            }
+                        } else {
+                            fail = true;                                   // A:159-163
+                        }
+                    }
+                    if (fail) {
+                        status = TBE_WAIT_FAILED;
+                    } else {                                               // A:166-181
+                        uint32_t tail = head + cnt;
+                        if (tail >= A.cap) tail -= A.cap;
+                        kr[tail] = ((uint64_t)(A.id_base + arrival(r)) << 16) | (uint32_t)p;
+                        ++cnt;
+                        a.qsum = (uint16_t)(a.qsum + (uint32_t)p);
+                        status = TBE_WAIT_QUEUED;
+                    }
+                    a.hc = (head & 0xFFFFu) | (cnt << 16);
+                    modified = true;
+                }
                 rbuf[r * kFoldBlock + tid] = pack_wait(status, evaluated, (uint32_t)avail_of(a));
                 if (modified) {
                     sl[kl[r]] = a;
