@@ -42,6 +42,16 @@ VARIANT_SETS = {
         "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "qshape": {
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "b1024i2w8_q": (["TBE_Q_BLOCK=1024", "TBE_Q_ITEMS=2", "TBE_Q_WAVES=8"], ["--workload", "queue", "--no-drain-variant"]),
+        "b1024i1w8_q": (["TBE_Q_BLOCK=1024", "TBE_Q_ITEMS=1", "TBE_Q_WAVES=8"], ["--workload", "queue", "--no-drain-variant"]),
+    },
+    "histhot": {
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "hotw8_z": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "hotw4_z": (["TBE_HIST_HOT_WAVES=4"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "afold": {
         "base_a": ([], ["--workload", "approx"]),
         "r1only_a": (["TBE_A_R1_ONLY"], ["--workload", "approx"]),
