@@ -71,7 +71,11 @@ namespace {
 #define LD_S(p) (*(p))
 #define ST_S(p, v) (*(p) = (v))
 #endif
+#ifdef TBE_FOLD_REC_NT
+#define LD_F(p) ld_nt(p)   // A/B: the fold's sorted records streamed
+#else
 #define LD_F(p) (*(p))
+#endif
 #define ST_F(p, v) (*(p) = (v))
 
 #define TBE_PART_BLOCK 512

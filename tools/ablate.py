@@ -42,6 +42,12 @@ VARIANT_SETS = {
         "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "recnt": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "recnt_u": (["TBE_FOLD_REC_NT"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "recnt_z": (["TBE_FOLD_REC_NT"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "qshape": {
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
         "b1024i2w8_q": (["TBE_Q_BLOCK=1024", "TBE_Q_ITEMS=2", "TBE_Q_WAVES=8"], ["--workload", "queue", "--no-drain-variant"]),
