@@ -2730,6 +2730,14 @@ __device__ __forceinline__ int32_t dotnet_to_int(double x) {
 // thread after an LDS counting sort (fold 1.22 against 0.76 ms), and deciding whole runs at
 // once when all of a key's requests in the chunk lease (A:191-209; 0.91 ms: the sort, the run
 // sums and the registers they spill cost more than the rounds they save).
+// Requests per thread per chunk (A/B: a larger chunk means fewer chunks per bucket and
+// fewer owner rounds in total, at more registers).
+#ifndef TBE_A_PER
+#define TBE_A_PER 4
+#endif
+constexpr int kAPer = TBE_A_PER;
+constexpr int kAChunk = kFoldBlock * kAPer;
+static_assert(kAChunk <= 4096, "election tags");
 #ifndef TBE_A_WAVES
 #define TBE_A_WAVES 6                        // minimum waves per SIMD: 80 VGPRs, 3 workgroups per CU
                                              // (0.867 -> 0.688 ms, profiles/r02_ablate_queue_dma_approx_waves.log)
@@ -2744,7 +2752,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t rw) {
     __shared__ ALocal sl[kMaxRows];
     __shared__ uint32_t own[kMaxRows];
-    __shared__ uint32_t rbuf[kFoldChunk];
+    __shared__ uint32_t rbuf[kAChunk];
     __shared__ uint32_t loaded[kMaxRows / 32];
     __shared__ uint32_t dirty[kMaxRows / 32];
 
@@ -2781,13 +2789,13 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
-    for (uint32_t c = s; c < e; c += kFoldChunk) {
+    for (uint32_t c = s; c < e; c += kAChunk) {
         for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
-        uint32_t kl[kFoldPer];
-        int32_t pm[kFoldPer];
+        uint32_t kl[kAPer];
+        int32_t pm[kAPer];
         uint32_t pend = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
+        for (int r = 0; r < kAPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
             kl[r] = 0; pm[r] = 0;
             if (q < e) {
@@ -2812,32 +2820,32 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         __syncthreads();
         uint32_t mine = 0;
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
+        for (int r = 0; r < kAPer; ++r) {
             if (pend & (1u << r)) {
                 const uint32_t bit = 1u << (kl[r] & 31);
                 if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
             }
         }
         if (mine) {   // sparse buckets only (a dense slice is all loaded)
-            ALocal tmp[kFoldPer];
+            ALocal tmp[kAPer];
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kAPer; ++r) {
                 tmp[r] = ALocal{0, 0, 0, 0, 0u};
                 if (mine & (1u << r)) tmp[r] = rows[kl[r]];
             }
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
+            for (int r = 0; r < kAPer; ++r)
                 if (mine & (1u << r)) sl[kl[r]] = tmp[r];
         }
         __syncthreads();
         for (uint32_t round = 1;; ++round) {
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r)
+            for (int r = 0; r < kAPer; ++r)
                 if (pend & (1u << r))
                     atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid)));
             __syncthreads();
 #pragma unroll
-            for (int r = 0; r < kFoldPer; ++r) {
+            for (int r = 0; r < kAPer; ++r) {
                 const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kFoldBlock + tid));
                 if (!((pend & (1u << r)) && own[kl[r]] == tag)) continue;
                 pend &= ~(1u << r);
@@ -2924,7 +2932,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < kFoldPer; ++r) {
+        for (int r = 0; r < kAPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
             if (q < e) {
                 if (rw == 2) reinterpret_cast<uint16_t *>(res)[q] = wait16(rbuf[r * kFoldBlock + tid]);

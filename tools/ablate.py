@@ -58,6 +58,12 @@ VARIANT_SETS = {
         "hotw8_z": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "hotw4_z": (["TBE_HIST_HOT_WAVES=4"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "aper": {
+        "base_a": ([], ["--workload", "approx"]),
+        "per8w5_a": (["TBE_A_PER=8", "TBE_A_WAVES=5"], ["--workload", "approx"]),
+        "per8w4_a": (["TBE_A_PER=8", "TBE_A_WAVES=4"], ["--workload", "approx"]),
+        "per6w5_a": (["TBE_A_PER=6", "TBE_A_WAVES=5"], ["--workload", "approx"]),
+    },
     "afold": {
         "base_a": ([], ["--workload", "approx"]),
         "r1only_a": (["TBE_A_R1_ONLY"], ["--workload", "approx"]),
