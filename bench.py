@@ -37,7 +37,8 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from bench_kinds import cpu_model, gather_floats, mark, reduce_max  # noqa: E402
+from bench_kinds import (cpu_model, gather_floats, mark, pmc_workload, reduce_max,  # noqa: E402
+                         run_fingerprint, write_fingerprint)
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED_B = 0x5EED000B
@@ -95,6 +96,8 @@ def parse():
     ap.add_argument("--no-hot", action="store_true", help="no hot-key runs (A/B)")
     ap.add_argument("--no-narrow", action="store_true",
                     help="4-byte replies even where TokenLimit <= 127 allows 1-byte ones (A/B)")
+    ap.add_argument("--no-sparse", action="store_true",
+                    help="skip the sparse-batch leg (2^20-request batches over config B's keys)")
     ap.add_argument("--no-strdir", action="store_true",
                     help="skip the string-key directory leg (config B batches as key text)")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -213,7 +216,9 @@ def main():
     if routed:   # the device path orders the engine on a real stream (cluster.device_stream)
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B)
-    directory = cluster.DeviceDirectory(keys_local, device=dev.index) if routed else None
+    # --route timed: the directory's overflow check must not synchronise inside a step
+    directory = cluster.DeviceDirectory(keys_local, device=dev.index, strict=args.route != "timed") \
+        if routed else None
     bufs, raw = [], []
     # generate on the current stream: the routing kernels run on it too (a torch stream does
     # not wait for the legacy NULL stream)
@@ -244,6 +249,8 @@ def main():
                             pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                             pipeline=not args.no_pipeline)
     layout = eng.layout()
+    if rank == 0:
+        write_fingerprint(run_fingerprint(args, world, keys_local, layout))
     granted = torch.empty(m_max if not raw else n, dtype=torch.uint8, device=dev)
     remaining = torch.empty(m_max if not raw else n, dtype=torch.int32, device=dev)
     zkeys = [bufs[s][0].cpu().numpy().view(np.uint64) for s in range(min(2, len(bufs)))] \
@@ -369,10 +376,16 @@ def main():
                                       1 if layout.get("narrow") else 4, w_meas)
         achieved = own_bytes / (per_launch_ms * 1e-3) / 1e9
         step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
-        pmc = pmc_stage(args.workload, name)
+        fp = run_fingerprint(args, world, keys_local, layout)
+        w_pmc, pmc_why = pmc_workload(args.workload, fp)
+        pmc = pmc_stage(w_pmc, name)
+        if w_pmc is not None and pmc is None:
+            pmc_why = f"no PMC bytes for the {name} stage"
+        step_pmc = pmc_step_traffic(w_pmc)
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (round(pmc / launches[name], 1) if pmc is not None else None),
+                    **({"traffic_null_reason": pmc_why} if pmc is None else {}),
                     "alg_bytes_per_launch": own_bytes,
                     "alg_bytes_note": algorithmic_note(name, layout, u_meas, w_meas),
                     "distinct_keys_U": u_meas, "written_keys_W": w_meas,
@@ -381,8 +394,11 @@ def main():
                                      "+ 16 B per distinct key written; " + uw_note,
                     "step_achieved": round(step_achieved, 1),
                     "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
-                    "step_traffic": pmc_step_traffic(args.workload),
+                    "step_traffic": step_pmc,
+                    **({"step_traffic_null_reason": pmc_why or "no step bytes in the PMC summary"}
+                       if step_pmc is None else {}),
                     "traffic_source": PMC_SOURCE,
+                    "fingerprint": fp,
                     "avg_launch_ms": round(per_launch_ms, 4),
                     "timing": ("serial replay of the timed batches (pipeline off), HIP events on the "
                                "engine stream" if replay_check is not None else
@@ -443,6 +459,13 @@ def main():
     if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_strdir:
         strdir = bench_strdir(bufs[:6], keys_local, dev)
 
+    # a sparse batch on the same key space: 2^20 requests over 1e8 keys touch
+    # ~1% of the table's lines, so the fold gathers the rows of its sparse buckets
+    # (k_fold) instead of pulling every slice whole
+    sparse = None
+    if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_sparse:
+        sparse = bench_sparse(args, lib, keys_local, dev)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, keys_local, zkeys,
@@ -482,6 +505,7 @@ def main():
             **({"host_buffer_pinned_decisions_per_s": host_rate_pinned}
                if host_rate_pinned is not None else {}),
             **({"string_directory": strdir} if strdir is not None else {}),
+            **({"sparse_batch": sparse} if sparse is not None else {}),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}
@@ -493,6 +517,44 @@ def main():
     eng.close()
     if dist:
         td.destroy_process_group()
+
+
+def bench_sparse(args, lib, n_keys: int, dev, n: int = 1 << 20, warm: int = 3, timed: int = 10):
+    """Batches of `n` requests (config B's trace shape, keys uniform over the same key
+    space) on a fresh engine, after the timed region: HIP-event stage times per batch.
+    Shows the fold's density gate (fold_wide_min): the sparse buckets' rows are gathered,
+    not their whole slices."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine
+    eng = TokenBucketEngine(n_keys, args.token_limit, args.tokens_per_period, args.period_ticks,
+                            device=dev.index, stage_timing=True, max_batch=n, pipeline=False)
+    gen_stream = torch.cuda.current_stream(dev).cuda_stream or None
+    bufs = []
+    for s in range(warm + timed):
+        k = torch.empty(n, dtype=torch.int64, device=dev)
+        p = torch.empty(n, dtype=torch.int32, device=dev)
+        t = torch.empty(n, dtype=torch.int64, device=dev)
+        assert lib.tbe_gen_batch_device(SEED_B ^ 0x5A, n_keys, s * n, n, 1, 1, T0_US + s * args.interval_us,
+                                        args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), gen_stream) == 0
+        bufs.append((k, p, t))
+    g = torch.empty(n, dtype=torch.uint8, device=dev)
+    r = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    for s in range(warm):
+        eng.acquire_batch_device(*bufs[s], g, r)
+    eng.synchronize()
+    eng.stage_times()
+    t0 = time.perf_counter()
+    for s in range(warm, warm + timed):
+        eng.acquire_batch_device(*bufs[s], g, r)
+    eng.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = eng.stage_times()
+    eng.close()
+    return {"batch": n, "batches_timed": timed, "ms_per_batch": round(elapsed / timed * 1e3, 4),
+            "decisions_per_s": round(n * timed / elapsed, 1),
+            "stage_ms_per_batch": {k: round(v / timed, 4) for k, v in st.items()},
+            "note": f"2^{n.bit_length() - 1} uniform requests over the same {n_keys} keys on a fresh engine, "
+                    "one stream; buckets below R/8 requests take the sparse fold (k_fold: touched rows only)"}
 
 
 def bench_strdir(batches, n_keys: int, dev):
@@ -592,27 +654,16 @@ PMC_SOURCE = ("profiles/pmc_summary.json: rocprofv3 --pmc passes of tools/pmc_pa
               "calibrated read/write models")
 
 
-def _pmc_workload(workload: str):
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get("workloads", {}).get(workload)
-    except (OSError, ValueError):
-        return None
-
-
-def pmc_stage(workload: str, stage: str):
-    """HBM bytes per step of one bench stage (all its kernels' timed launches), from the
-    committed PMC summary, if present."""
-    w = _pmc_workload(workload)
+def pmc_stage(w, stage: str):
+    """HBM bytes per step of one bench stage (all its kernels' timed launches), from a PMC
+    summary entry matched to this run (bench_kinds.pmc_workload), if any."""
     st = (w or {}).get("stages", {}).get(stage)
     return st.get("hbm_bytes_per_step") if st else None
 
 
-def pmc_step_traffic(workload: str = "uniform"):
-    """HBM bytes of one whole step (every kernel of one timed batch), from the committed
-    PMC summary, if present."""
-    w = _pmc_workload(workload)
+def pmc_step_traffic(w):
+    """HBM bytes of one whole step (every kernel of one timed batch), from a matched PMC
+    summary entry, if any."""
     return round(w["step_hbm_bytes"], 1) if w and "step_hbm_bytes" in w else None
 
 

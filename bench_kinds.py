@@ -56,16 +56,65 @@ def _distinct(n: int, k: int) -> float:
     return k * (1.0 - np.exp(-n / k))
 
 
-def _pmc_traffic(workload, kernels):
-    """HBM bytes per launch of the named kernels (mean over them) in `workload`'s runs,
-    from the committed PMC summary (tools/pmc_summary.py --write), or None."""
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")
+# what makes two runs move the same bytes per step: the fingerprint of a bench run, written
+# by the PMC passes' own bench runs (tools/pmc_passes.sh sets TBE_PMC_FINGERPRINT) into
+# profiles/pmc_summary.json and compared key by key with the run that reports the bytes
+FINGERPRINT_KEYS = ("workload", "world", "keys_per_gpu", "batch", "steps", "warmup", "token_limit",
+                    "tokens_per_period", "period_ticks", "interval_us", "queue_limit", "route",
+                    "share_device", "layout", "engine_sources_sha256")
+
+
+def run_fingerprint(args, world: int, keys_per_gpu: int, layout: dict) -> dict:
+    """The fingerprint of this bench run (FINGERPRINT_KEYS); the engine's sources by the
+    same SHA-256 the build stamps beside libtbe.so (sources + compiler flags)."""
+    from distributedratelimiting.redis_amd.build import DEPS, HIPCC_FLAGS, _digest
+    return {"workload": args.workload, "world": int(world), "keys_per_gpu": int(keys_per_gpu),
+            "batch": int(args.batch), "steps": int(args.steps), "warmup": int(args.warmup),
+            "token_limit": int(args.token_limit), "tokens_per_period": int(args.tokens_per_period),
+            "period_ticks": int(args.period_ticks), "interval_us": int(args.interval_us),
+            "queue_limit": int(args.queue_limit) if args.workload == "queue" else None,
+            "route": args.route if world > 1 else None, "share_device": bool(args.share_device),
+            "layout": {k: layout[k] for k in sorted(layout)},
+            "engine_sources_sha256": _digest(DEPS, HIPCC_FLAGS)}
+
+
+def write_fingerprint(fp: dict) -> None:
+    """bench runs under tools/pmc_passes.sh record what they ran (TBE_PMC_FINGERPRINT)."""
     import json
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")
+    path = os.environ.get("TBE_PMC_FINGERPRINT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(fp, f, indent=1, sort_keys=True)
+
+
+def pmc_workload(workload: str, fp: dict, path: str = PMC_SUMMARY):
+    """(the PMC summary's entry for `workload`, None) when it was measured on a run with
+    exactly this fingerprint, else (None, reason).  A run whose configuration differs
+    (keys per GPU, batch, world, schedule, layout, engine sources...) gets no bytes."""
+    import json
     try:
         with open(path) as f:
-            d = json.load(f).get("workloads", {}).get(workload, {}).get("kernels", {})
-    except (OSError, ValueError):
+            w = json.load(f).get("workloads", {}).get(workload)
+    except (OSError, ValueError) as e:
+        return None, f"no PMC summary ({type(e).__name__})"
+    if w is None:
+        return None, f"no PMC passes for workload {workload!r}"
+    got = w.get("fingerprint")
+    if got is None:
+        return None, "the PMC passes recorded no run fingerprint"
+    diff = [k for k in FINGERPRINT_KEYS if got.get(k) != fp.get(k)]
+    if diff:
+        return None, "PMC passes ran a different configuration: " + ", ".join(
+            f"{k} {got.get(k)!r} != {fp.get(k)!r}" if k != "layout" else "layout" for k in diff)
+    return w, None
+
+
+def _pmc_traffic(w, kernels):
+    """HBM bytes per launch of the named kernels (mean over them) in a matched PMC entry."""
+    if w is None:
         return None
+    d = w.get("kernels", {})
     v = [d[k]["hbm_bytes_per_launch"] for k in kernels if "hbm_bytes_per_launch" in d.get(k, {})]
     return round(sum(v) / len(v), 1) if len(v) == len(kernels) and v else None
 
@@ -79,34 +128,38 @@ PMC_KERNELS = {
 }
 
 
-def _roofline(name, alg_bytes, ms, note, workload=None):
+def _roofline(name, alg_bytes, ms, note, workload, fp):
     if not ms > 0:    # --no-stage-timing: no kernel times
         return None
     achieved = alg_bytes / (ms * 1e-3) / 1e9
-    traffic = _pmc_traffic(workload, PMC_KERNELS[(workload, name)]) if (workload, name) in PMC_KERNELS else None
+    w, why = pmc_workload(workload, fp)
+    traffic = _pmc_traffic(w, PMC_KERNELS[(workload, name)]) if (workload, name) in PMC_KERNELS else None
+    if w is not None and traffic is None:
+        why = f"no PMC bytes for the {name} kernels"
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            **({"traffic_null_reason": why} if traffic is None else {}),
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4),
             "alg_bytes_note": note,
-            "timing": "HIP events on the engine's launch stream over the timed region"}
+            "timing": "HIP events on the engine's launch stream over the timed region",
+            "fingerprint": fp}
 
 
-def _step_roofline(line, alg, note, workload):
+def _step_roofline(line, alg, note, workload, fp):
     """Whole-step figures beside the dominant kernel's: §8(d)'s algorithmic bytes over the
-    timed ms_per_step, and the PMC bytes of one step (tools/pmc_summary.py), if committed."""
+    timed ms_per_step, and the PMC bytes of one step (tools/pmc_summary.py), if committed
+    for a run of exactly this configuration."""
     r = line.get("roofline")
     if r is None:
         return
-    import json
     achieved = alg / (line["ms_per_step"] * 1e-3) / 1e9
     r.update({"step_alg_bytes": int(alg), "step_alg_note": note, "step_achieved": round(achieved, 1),
               "step_frac": round(achieved / HBM_PEAK_GBS, 4)})
-    try:
-        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_summary.json")) as f:
-            st = json.load(f).get("workloads", {}).get(workload, {}).get("step_hbm_bytes")
-        r["step_traffic"] = round(st, 1) if st is not None else None
-    except (OSError, ValueError):
-        r["step_traffic"] = None
+    w, why = pmc_workload(workload, fp)
+    st = w.get("step_hbm_bytes") if w is not None else None
+    r["step_traffic"] = round(st, 1) if st is not None else None
+    if st is None:
+        r["step_traffic_null_reason"] = why or "no step bytes in the PMC summary"
 
 
 def run(args, lib, dev, world, rank, dist):
@@ -249,6 +302,9 @@ def run_queue(args, lib, dev, world, rank, dist):
     fused = not args.no_fuse_tick
     r = _queue_pass(args, lib, dev, world, dist, kl, args.period_ticks, seed, marked=True)
     elapsed, stages, granted, q_last, d_last = r["elapsed"], r["stages"], r["granted"], r["q_last"], r["d_last"]
+    fp = run_fingerprint(args, world, kl, r["layout"])
+    if rank == 0:
+        write_fingerprint(fp)
 
     value = n * steps * world / elapsed
     passes = r["layout"]["passes"]
@@ -295,13 +351,13 @@ def run_queue(args, lib, dev, world, rank, dist):
         "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
         "tick_grants_per_step": r["tick_grants_per_step"],
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
-        "roofline": _roofline(name, alg, ms, note, "queue"),
+        "roofline": _roofline(name, alg, ms, note, "queue", fp),
         "cpu_baseline": None,
     }
     # SURVEY.md §8(d) config D, whole step: the B formula (W ~ distinct keys x grant share)
     # + 8 B per enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
     _step_roofline(line, n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8,
-                   "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)", "queue")
+                   "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)", "queue", fp)
     if not args.no_drain_variant:
         # The same schedule with ticks that grant: at 1 token/s a saturated key frees one
         # queue entry per ~1000 ticks, so config D's ticks drain nothing within a run.  With
@@ -429,6 +485,9 @@ def run_approx(args, lib, dev, world, rank, dist):
     xbytes = {"node": int(2 * (world - 1) * kshared * 4 // world), "clients": int((world - 1) * kshared * 4)}
 
     value = n * steps * world / elapsed
+    fp = run_fingerprint(args, world, kshared, eng.layout())
+    if rank == 0:
+        write_fingerprint(fp)
     passes = eng.layout()["passes"]
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
                 "unscatter": passes, "hot": 1}
@@ -468,12 +527,12 @@ def run_approx(args, lib, dev, world, rank, dist):
                               "timed": "in the timed steps" if m == args.approx_mode else
                                        f"{min(steps, 5)} epochs after the timed region"}
                           for m in ("node", "clients")},
-        "roofline": _roofline(name, alg, ms, note, "approx"),
+        "roofline": _roofline(name, alg, ms, note, "approx", fp),
         "cpu_baseline": None,
     }
     # SURVEY.md §8(d) config E, whole step: 8+4+1 in/out + 8 local-tier state per decision,
     # K_shared * (4 count + 24 v,p,t) per refresh
-    _step_roofline(line, n * 21 + kshared * 28, "21*N + 28*K_shared (one refresh per batch)", "approx")
+    _step_roofline(line, n * 21 + kshared * 28, "21*N + 28*K_shared (one refresh per batch)", "approx", fp)
     eng.close()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_approx(args, kshared)

@@ -176,6 +176,8 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_dir_lookup_device.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
     lib.tbe_dir_size.restype = c_int32
     lib.tbe_dir_size.argtypes = [c_void_p, POINTER(c_uint64)]
+    lib.tbe_dir_state_async.restype = c_int32
+    lib.tbe_dir_state_async.argtypes = [c_void_p, c_void_p, c_void_p]
     lib.tbe_key_text_lengths_device.restype = c_int32
     lib.tbe_key_text_lengths_device.argtypes = [c_void_p, c_uint64, ctypes.c_uint32, c_void_p, c_void_p]
     lib.tbe_key_text_device.restype = c_int32

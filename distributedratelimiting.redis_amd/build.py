@@ -11,7 +11,7 @@ import shutil
 import subprocess
 import sys
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.realpath(__file__))   # also when imported through the distributedratelimiting/ symlink
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", n) for n in ("tbe_engine.hip", "tbe_tools.hip", "tbe_cluster.hip", "tbe_strdir.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", n) for n in ("tbe_device.hpp", "tbe_numfmt.hpp", "tbe_hash.hpp")] + \

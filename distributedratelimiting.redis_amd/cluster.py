@@ -137,9 +137,17 @@ class HostDirectory:
 
 
 class DeviceDirectory:
-    """The owner's key directory in HBM (include/tbe_cluster.h tbe_dir_*)."""
+    """The owner's key directory in HBM (include/tbe_cluster.h tbe_dir_*).
 
-    def __init__(self, capacity: int, device: int = -1):
+    ``strict`` (default): ``check()`` raises TBE_ERANGE for the very batch that overflowed,
+    before anything is decided -- near capacity that costs a device synchronisation per
+    batch.  ``strict=False``: near capacity each check enqueues an asynchronous copy of the
+    directory's state (tbe_dir_state_async) and inspects the previous one, so an overflow
+    raises one batch later without synchronising; the overflowing batch itself is still
+    refused, by the engine (its keys beyond capacity get UINT64_MAX ids, an invalid batch).
+    bench.py --route timed uses it, so no synchronisation sits inside a timed step."""
+
+    def __init__(self, capacity: int, device: int = -1, strict: bool = True):
         import ctypes
         from . import _capi
         self._lib = _capi.load()
@@ -153,6 +161,8 @@ class DeviceDirectory:
         # one): while it stays below capacity no batch can have overflowed, so the exact
         # count (a device synchronisation) is fetched only once the bound reaches it
         self._bound = 0
+        self.strict = strict
+        self._pending = None     # (pinned state copy, event) of the last asynchronous check
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -162,8 +172,27 @@ class DeviceDirectory:
     def check(self) -> None:
         """Raise TbeError(TBE_ERANGE) if an assign batch overflowed the directory; free
         (no device synchronisation) while the assigned-id bound stays below capacity."""
-        if self._bound >= self.capacity:
+        if self._bound < self.capacity:
+            return
+        if self.strict:
             self._bound = self.size()      # raises TBE_ERANGE on overflow
+            return
+        import torch
+        from . import _capi
+        if self._pending is not None and self._pending[1].query():
+            st = self._pending[0]
+            self._pending = None
+            if int(st[1]) != 0:
+                raise _capi.TbeError(_capi.TBE_ERANGE, f"key directory over capacity ({self.capacity} ids)")
+        if self._pending is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            st = torch.zeros(2, dtype=torch.int64, pin_memory=True)
+            rc = self._lib.tbe_dir_state_async(self._h, st.data_ptr(), device_stream(dev))
+            if rc != _capi.TBE_OK:
+                raise _capi.TbeError(rc, "tbe_dir_state_async failed")
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._pending = (st, ev)
 
     def __del__(self):
         try:

@@ -461,6 +461,14 @@ tbe_status tbe_dir_lookup_device(tbe_directory *d, const uint64_t *d_keys, uint6
     return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
 }
 
+tbe_status tbe_dir_state_async(tbe_directory *d, uint64_t *out2, void *stream) {
+    if (!d || !out2) return TBE_EINVAL;
+    if (hipSetDevice(d->device) != hipSuccess) return TBE_EDEVICE;
+    return hipMemcpyAsync(out2, d->state, 2 * sizeof(uint64_t), hipMemcpyDefault, (hipStream_t)stream) == hipSuccess
+               ? TBE_OK
+               : TBE_EDEVICE;
+}
+
 tbe_status tbe_dir_size(tbe_directory *d, uint64_t *n_ids) {
     if (!d || !n_ids) return TBE_EINVAL;
     if (hipSetDevice(d->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return TBE_EDEVICE;

@@ -753,8 +753,9 @@ __device__ __forceinline__ void slot_store_nt(Slot *p, const Slot &s) {
 }
 
 // 16 bytes per lane from global memory straight into LDS (global_load_lds_dwordx4, nt):
-// the LDS destination is the wave-uniform `lds_wave` + 16 * lane.  Visible to the
-// workgroup after the next __syncthreads() (which waits for it).
+// the LDS destination is the wave-uniform `lds_wave` + 16 * lane.  A barrier alone does
+// NOT wait for it: every issuing wave runs lds_dma_wait() before the __syncthreads() that
+// publishes the slice to the workgroup.
 typedef __attribute__((address_space(1))) const void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
 __device__ __forceinline__ void lds_dma16(const void *src, void *lds_wave) {
@@ -816,13 +817,20 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_WIDE_MIN_SHIFT
 #define TBE_WIDE_MIN_SHIFT 11
 #endif
-// k_fold_wide takes buckets of >= R >> kWideMinShift requests: on a Zipf slice, whose
-// buckets hold fewer requests once the hot keys run apart, its 24 waves per CU fold them
-// faster than k_fold's 12 (round 2, R/32: config C fold 0.89 -> 0.69 ms; R/2 .. R/2048
-// measured, profiles/r02_ablate_wide_threshold*.log).  Round 3: every nonempty bucket
-// (R >> 11 = 1 at the largest buckets), and k_fold is then not launched at all -- its
-// 48828 workgroups that only read their bucket bounds and exit cost 0.03 ms per batch
-// (fold 0.76 -> 0.73 ms on Zipf, 0.89 -> 0.86 on uniform, profiles/r03_ablate_hot_wide_walk.log).
+// Which buckets k_fold_wide takes is decided per launch (wide_min, fold_wide_min below):
+// the buckets of at least `wide_min` requests.  k_fold_wide pulls its whole 16*R-byte
+// slice by LDS-DMA, k_fold only the rows a bucket touches.
+//  - Dense batches (at least R/32 requests per bucket on average: configs B and C):
+//    every nonempty bucket (wide_min = R >> kWideMinShift = 1 at R = 2048).  On a Zipf
+//    slice, whose buckets hold fewer requests once the hot keys run apart, the wide fold's
+//    24 waves per CU beat k_fold's 12 (round 2, R/32: config C fold 0.89 -> 0.69 ms;
+//    R/2 .. R/2048 measured, profiles/r02_ablate_wide_threshold*.log); round 3 gave it every
+//    bucket and stopped launching k_fold, whose 48828 workgroups that only read their
+//    bucket bounds and exit cost 0.03 ms per batch (profiles/r03_ablate_hot_wide_walk.log).
+//  - Sparse batches (e.g. 2^20 requests over 1e8 keys, ~21 per bucket): k_fold_wide only
+//    for buckets of at least R/8 requests, the rule k_fold's own dense test uses; the others
+//    go to k_fold, which gathers just their rows instead of the whole slice (ADVICE r03:
+//    a dense-only fold reads the whole 1.6 GB table for a batch that touches 16 MB of it).
 constexpr int kWideMinShift = TBE_WIDE_MIN_SHIFT;
 // Tail walk (round 3, as k_fold_q's; A/B only): the requests still pending after round 1
 // are counting-sorted by row and each row's run is decided by one thread in arrival order,
@@ -846,8 +854,8 @@ static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and 
 #define WIDE_FT_SET(j, v) ((void)0)
 #endif
 
-// Buckets of >= R/32 requests (every bucket of uniform traffic), shaped as above (three workgroups per
-// CU, chunks of 1024 requests).  k_fold below takes the other buckets.
+// Buckets of >= wide_min requests (every nonempty bucket of a dense batch), shaped as above
+// (three workgroups per CU, chunks of 1536 requests).  k_fold below takes the other buckets.
 template <bool PACKED>
 __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
@@ -855,7 +863,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow) {
+    uint32_t narrow, uint32_t wide_min) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -889,12 +897,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-    // Buckets with >= R/32 requests only (k_fold takes the others): the whole slice is
-    // pulled in (LDS-DMA) and only its dirty lines are written back.
-#ifdef TBE_FOLD_NARROW_ONLY
-    return;   // A/B: k_fold takes every bucket
-#endif
-    if (e - s < (R >> kWideMinShift)) return;
+    // Buckets with >= wide_min requests only (k_fold takes the others): the whole slice
+    // is pulled in (LDS-DMA) and only its dirty lines are written back.
+    if (e - s < wide_min) return;
     const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
@@ -1307,7 +1312,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow) {
+    uint32_t narrow, uint32_t wide_min) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -1333,9 +1338,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-#ifndef TBE_FOLD_NARROW_ONLY
-    if (e - s >= (R >> kWideMinShift)) return;   // k_fold_wide's
-#endif
+    if (e - s >= wide_min) return;   // k_fold_wide's
     // Whole slice (dense) or touched rows only (sparse), decided below.
     bool dense = false;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
@@ -3370,6 +3373,23 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
     (void)hipEventRecord(e->ev_pool[e->ev_marks.back().second + 1], st);
 }
 
+// The token-bucket fold's density gate (see kWideMinShift): k_fold_wide takes the buckets
+// of at least the returned number of requests, k_fold the rest (launched only when this is
+// above 1).  Dense batches give every nonempty bucket to k_fold_wide; sparse ones only the
+// buckets of >= R/8 requests.  TBE_FOLD_NARROW_ONLY (A/B): k_fold takes every bucket.
+uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
+#ifdef TBE_FOLD_NARROW_ONLY
+    (void)e;
+    (void)n;
+    return 0xFFFFFFFFu;
+#else
+    const uint32_t R = 1u << e->r_bits;
+    const uint32_t all = std::max(1u, R >> kWideMinShift);
+    if (n >= (uint64_t)e->nbuckets * std::max(1u, R >> 5)) return all;
+    return std::max(all, R >> 3);
+#endif
+}
+
 // Enqueue the whole pipeline for one device-resident batch.  `caller` is the stream the
 // inputs were produced on and the replies are awaited on; NULL: the inputs are complete
 // at the call and the replies are ordered on the engine's stream.
@@ -3551,22 +3571,24 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
                 e->wait_rw(), e->qtick);
     } else if (e->packed) {
-        // full buckets in k_fold_wide, the others in k_fold (each skips the other's)
+        // dense buckets in k_fold_wide, the others in k_fold (each skips the other's)
+        const uint32_t wmin = fold_wide_min(e, n);
         k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
-        if (((1u << e->r_bits) >> kWideMinShift) > 1u)   // else k_fold_wide takes every bucket
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin);
+        if (wmin > 1u)   // else k_fold_wide takes every bucket
             k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u);
+                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin);
     } else {
+        const uint32_t wmin = fold_wide_min(e, n);
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
-        if (((1u << e->r_bits) >> kWideMinShift) > 1u)
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin);
+        if (wmin > 1u)
             k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
-                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u);
+                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart,
+                e->r_bits, e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {

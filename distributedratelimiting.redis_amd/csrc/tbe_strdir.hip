@@ -603,9 +603,10 @@ struct tbe_string_directory {
     unsigned long long *h_state = nullptr; // pinned: state[0] after the last assign (async copy)
     hipEvent_t ev_state = nullptr;
     bool state_pending = false;
-    unsigned long long last_ids = 0;       // ids before the batch whose count is in flight
-    uint64_t last_n = 0;                   // that batch's size
-    double new_share = 1.0;                // new keys / requests of the last observed batch
+    unsigned long long last_ids = 0;       // ids at the previous observed copy
+    uint64_t since_n = 0;                  // requests assigned since the last copy was enqueued
+    uint64_t last_n = 0;                   // requests between the previous copy and the one in flight
+    double new_share = 1.0;                // new keys / requests between the last two observed copies
     // host-buffer staging
     uint64_t st_bytes = 0, st_n = 0;
     uint8_t *d_bytes = nullptr;
@@ -743,10 +744,21 @@ tbe_status tbe_sdir_assign_device(tbe_string_directory *d, const uint8_t *d_byte
     // The warm path pays one lookup pass over the batch to run the assign machinery over
     // its misses only: chosen while the last observed batch brought few new keys (its id
     // count is copied back asynchronously; the choice never waits for it).
-    if (d->state_pending && hipEventQuery(d->ev_state) == hipSuccess) {
-        d->new_share = d->last_n ? (double)(*d->h_state - d->last_ids) / (double)d->last_n : 1.0;
-        d->last_ids = *d->h_state;
-        d->state_pending = false;
+    // The copy in flight holds the id count after the batch it followed; last_n counts every
+    // request assigned between that copy and the previous one (several batches when copies
+    // were still pending), so the share is new ids per request over exactly those batches.
+    if (d->state_pending) {
+        const hipError_t q = hipEventQuery(d->ev_state);
+        if (q == hipSuccess) {
+            d->new_share = d->last_n ? (double)(*d->h_state - d->last_ids) / (double)d->last_n : 1.0;
+            d->last_ids = *d->h_state;
+            d->state_pending = false;
+        } else if (q != hipErrorNotReady) {
+            // an unreadable copy: forget it, take the full path, and copy again below
+            (void)hipGetLastError();
+            d->new_share = 1.0;
+            d->state_pending = false;
+        }
     }
     const bool warm = d->mode == 2 || (d->mode == 0 && d->new_share < kWarmShare);
     const uint32_t *miss = warm ? d->miss : nullptr;
@@ -773,13 +785,15 @@ tbe_status tbe_sdir_assign_device(tbe_string_directory *d, const uint8_t *d_byte
                                            d->bbase, d->state, d->capacity, d->arena_bytes, d->imask, d->ish, miss,
                                            miss_n);
     k_sd_gather<<<sd_grid(n, 256), 256, 0, st>>>(d->slot_of, n, d->sid, d_ids, miss, miss_n);
+    d->since_n += n;
     if (!d->state_pending) {
-        // the batch's id count, for the next call's choice
+        // the id count after this batch, for a later call's choice
         if (hipMemcpyAsync(d->h_state, d->state, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipEventRecord(d->ev_state, st) != hipSuccess)
             return TBE_EDEVICE;
         d->state_pending = true;
-        d->last_n = n;
+        d->last_n = d->since_n;
+        d->since_n = 0;
     }
     return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
 }

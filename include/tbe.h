@@ -83,9 +83,13 @@ typedef struct tbe_config {
 #define TBE_FLAG_NO_PIPELINE 0x8u         /* token bucket: run every stage of a batch on one
                                              stream (A/B checks); by default batch b+1's
                                              partition overlaps batch b's fold */
-#define TBE_FLAG_NO_NARROW 0x10u          /* token bucket: keep 4-byte replies through the fold
-                                             and un-partition passes even when TokenLimit
-                                             <= 127 allows 1-byte ones (A/B checks) */
+#define TBE_FLAG_NO_NARROW 0x10u          /* keep 4-byte replies through the fold and the
+                                             un-partition passes (A/B checks) instead of the
+                                             narrower forms: token bucket 1-byte replies
+                                             (packed records, TokenLimit <= 127); queueing kind
+                                             1-byte (TokenLimit <= 62) and 2-byte (<= 16382)
+                                             replies; approximate kind 2-byte replies
+                                             (TokenLimit <= 16382) */
 
 typedef struct tbe_engine tbe_engine;
 

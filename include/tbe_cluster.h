@@ -75,6 +75,13 @@ tbe_status tbe_dir_lookup_device(tbe_directory *dir, const uint64_t *d_keys, uin
                                  void *stream);
 /* Ids assigned so far (synchronises the directory's device). */
 tbe_status tbe_dir_size(tbe_directory *dir, uint64_t *n_ids);
+/* The same without synchronising: enqueues on `stream` a copy of {ids assigned, error
+ * bits} (two u64; error bits != 0 once a batch exceeded the capacity, the condition
+ * tbe_dir_size reports as TBE_ERANGE) into out2, pinned host or device memory.  Lets a
+ * caller notice an overflow a batch later without a device synchronisation per batch;
+ * the batch that overflowed is caught by the engine anyway (its UINT64_MAX ids make the
+ * engine batch invalid). */
+tbe_status tbe_dir_state_async(tbe_directory *dir, uint64_t *out2, void *stream);
 
 #ifdef __cplusplus
 }

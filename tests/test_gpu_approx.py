@@ -14,20 +14,27 @@ pytestmark = pytest.mark.gpu
 S_US = 1_760_572_800 * 1_000_000
 
 
-@pytest.mark.parametrize("n_clients,order,qlimit,wait,pack", [
-    (1, OLDEST_FIRST, 8, True, True), (3, NEWEST_FIRST, 4, True, True), (8, OLDEST_FIRST, 16, True, True),
-    (2, OLDEST_FIRST, 0, False, True),
+@pytest.mark.parametrize("n_clients,order,qlimit,wait,pack,limit", [
+    (1, OLDEST_FIRST, 8, True, True, 20), (3, NEWEST_FIRST, 4, True, True, 20),
+    (8, OLDEST_FIRST, 16, True, True, 20), (2, OLDEST_FIRST, 0, False, True, 20),
     # the SoA partition records (TBE_FLAG_NO_PACK; the default when key + permit code
     # leave less than 32 bits for the arrival index)
-    (3, NEWEST_FIRST, 4, True, False), (2, OLDEST_FIRST, 0, False, False)])
-def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack):
+    (3, NEWEST_FIRST, 4, True, False, 20), (2, OLDEST_FIRST, 0, False, False, 20),
+    # the reply widths' boundary: TokenLimit 16382 is the largest whose
+    # AvailableTokens fit the two-byte replies (14 bits, 16383 = "no script call"); 16383
+    # and above take four-byte replies
+    (2, OLDEST_FIRST, 8, True, True, 16382), (2, NEWEST_FIRST, 8, True, True, 16383),
+    (2, OLDEST_FIRST, 0, False, True, 16382)])
+def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, limit):
     import torch
     from distributedratelimiting.redis_amd import ApproximateEngine
-    n_keys, n, limit, tokens, ticks = 300, 4000, 20, 10, 10_000_000
-    rng = np.random.default_rng(n_clients * 100 + order * 10 + qlimit)
+    n_keys, n, tokens, ticks = 300, 4000, 10, 10_000_000
+    rng = np.random.default_rng(n_clients * 100 + order * 10 + qlimit + limit)
     engines = [ApproximateEngine(n_keys, limit, tokens, ticks, qlimit, order, device=0, pack=pack)
                for _ in range(n_clients)]
     assert engines[0].layout()["packed"] == pack
+    assert engines[0].layout()["medium"] == (limit <= 16382)
+    choices = [0, 1, 1, 2, 3, 25] + ([limit // 3, limit // 2, limit, limit + 1] if limit > 100 else [])
     clients = [ApproxClient(limit, tokens, ticks, qlimit, order) for _ in range(n_clients)]
     table = ApproxGlobalTable(clients[0].decay_rate)
     counts = [torch.zeros(n_keys, dtype=torch.int32, device=gpu) for _ in range(n_clients)]
@@ -36,7 +43,7 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack):
     for epoch in range(6):
         for r in range(n_clients):
             keys = rng.integers(0, n_keys, n).astype(np.uint64)
-            permits = rng.choice([0, 1, 1, 2, 3, 25], n).astype(np.int32)
+            permits = rng.choice(choices, n).astype(np.int32)
             st, av, (cause, ids) = engines[r].acquire_batch(keys, permits, wait=wait, id_base=rid)
             exp = []
             for i, (k, p) in enumerate(zip(keys.tolist(), permits.tolist())):

@@ -226,6 +226,27 @@ def test_route_batch_device_world1(engine_lib, gpu):
                                 torch.ones(1500, dtype=torch.int32, device=gpu),
                                 torch.full((1500,), 1_760_000_000_000_000, dtype=torch.int64, device=gpu), small)
         assert not calls
+        # strict=False (bench.py --route timed): no synchronisation per batch; the engine
+        # refuses the overflowing batch itself (keys beyond capacity get no id) and the next
+        # check raises TBE_ERANGE
+        lax = cluster.DeviceDirectory(1000, device=0, strict=False)
+        eng2 = TokenBucketEngine(1000, 5, 2, 10_000_000, device=0)
+
+        def decide2(lk, lp, lt):
+            g = torch.empty(lk.numel(), dtype=torch.uint8, device=gpu)
+            r = torch.empty(lk.numel(), dtype=torch.int32, device=gpu)
+            eng2.acquire_batch_device(lk, lp, lt, g, r, stream=torch.cuda.current_stream(gpu).cuda_stream)
+            return g, r
+        cols = (torch.ones(1500, dtype=torch.int32, device=gpu),
+                torch.full((1500,), 1_760_000_000_000_000, dtype=torch.int64, device=gpu))
+        cluster.route_batch(decide2, torch.arange(1500, dtype=torch.int64, device=gpu), *cols, lax)
+        with pytest.raises(cluster_error()):
+            eng2.synchronize()                                # the batch with id-less keys was refused
+        torch.cuda.synchronize()
+        with pytest.raises(cluster_error()):
+            cluster.route_batch(decide2, torch.arange(1500, 3000, dtype=torch.int64, device=gpu), *cols, lax)
+        eng2.close()
+        lax.close()
         with pytest.raises(ValueError):                       # the NULL default stream is refused
             torch.cuda.set_stream(torch.cuda.default_stream(gpu))
             cluster.route_batch(decide, torch.zeros(4, dtype=torch.int64, device=gpu),

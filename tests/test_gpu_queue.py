@@ -133,25 +133,30 @@ def test_attempt_mixed_with_wait(engine_lib, gpu, order):
 
 
 @pytest.mark.parametrize("order", [0, 1])
-@pytest.mark.parametrize("layout", ["wide", "packed_wide_reply", "token_limit_100", "escaped_ts"])
+@pytest.mark.parametrize("layout", ["wide", "packed_wide_reply", "token_limit_100", "escaped_ts",
+                                    "token_limit_16382", "token_limit_16383"])
 def test_queue_layouts(engine_lib, gpu, order, layout):
     """The queue path's record and reply layouts against the C restatement: wide pass
     records (TBE_FLAG_NO_PACK), packed records with 4-byte replies (TBE_FLAG_NO_NARROW),
-    TokenLimit 100 (too large for one-byte wait replies), and packed records whose
-    timestamps leave the 32-bit window (escape records: the fold reads ts by index)."""
+    TokenLimit 100 (too large for one-byte wait replies: two-byte ones), packed records whose
+    timestamps leave the 32-bit window (escape records: the fold reads ts by index), and
+    the two-byte replies' boundary: TokenLimit 16382 is the largest whose
+    remaining fits 14 bits beside the "no script call" code 16383; 16383 takes four bytes."""
     from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
-    tl = 100 if layout == "token_limit_100" else 4
+    tl = int(layout.rsplit("_", 1)[1]) if layout.startswith("token_limit") else 4
     kw = {"wide": dict(pack=False, narrow=False), "packed_wide_reply": dict(narrow=False)}.get(layout, {})
     n_keys, n = 5000, 60_000
     eng = QueueingTokenBucketEngine(n_keys, tl, 1, 10_000_000, 16, order, device=0, **kw)
     ref = cref.CQueueingTokenBucket(n_keys, tl, fill_rate(1, 10_000_000), 16, order)
     lay = eng.layout()
     assert lay["packed"] == (layout != "wide") and lay["narrow"] == (layout in ("escaped_ts",))
+    assert lay["medium"] == (layout in ("token_limit_100", "token_limit_16382"))
     rng = np.random.default_rng(hash(layout) % 1000 + order)
     t, rid = S_US, 0
     for _ in range(4):
         keys = rng.integers(0, n_keys, n).astype(np.uint64)
-        permits = rng.choice([0, 1, 1, 2, 3, 5, tl + 1], n).astype(np.int32)
+        big = [tl // 3, tl // 2, tl] if tl > 100 else []
+        permits = rng.choice([0, 1, 1, 2, 3, 5, tl + 1] + big, n).astype(np.int32)
         span = 3 * 3_600_000_000 if layout == "escaped_ts" else 1_000
         ts = (t + np.sort(rng.integers(0, span, n))).astype(np.int64)
         check_round(eng, ref, keys, permits, ts, rid)

@@ -19,7 +19,8 @@ PASSES=(
 run() {   # run <name> <secs> <cmd...>
     local name=$1 secs=$2; shift 2
     for i in "${!PASSES[@]}"; do
-        timeout -s KILL "$secs" rocprofv3 --pmc ${PASSES[$i]} --output-format csv -d "$OUT/pmc3_${name}_p$i" -o run -- \
+        # the bench run records its configuration (bench_kinds.run_fingerprint) for the summary
+        TBE_PMC_FINGERPRINT="$OUT/pmc3_${name}_fingerprint.json" timeout -s KILL "$secs" rocprofv3 --pmc ${PASSES[$i]} --output-format csv -d "$OUT/pmc3_${name}_p$i" -o run -- \
             "$@" > "$OUT/pmc3_${name}_p$i.log" 2>&1
         local rc=$?
         echo "[pmc $name pass $i] rc=$rc"
@@ -29,6 +30,6 @@ run() {   # run <name> <secs> <cmd...>
 [ "${SKIP_CALIB:-0}" = 1 ] || run calib 120 python3 "$ROOT/tools/pmc_calib.py"
 for W in ${WORKLOADS:-uniform}; do
     run $W 240 python3 "$ROOT/bench.py" --workload $W --steps 20 --warmup 5 --cpu-seconds 0 \
-        --no-stage-timing --no-host-buffer --no-strdir --no-drain-variant
+        --no-stage-timing --no-host-buffer --no-strdir --no-sparse --no-drain-variant
 done
 echo pmc-done

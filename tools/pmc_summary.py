@@ -201,6 +201,12 @@ def main():
         w = summarise(wl, rmodel, wmodel)
         if w:
             w["stages"] = stage_bytes(w)
+            # the configuration the passes ran (bench.py writes it under TBE_PMC_FINGERPRINT);
+            # bench.py attaches these bytes only to a run with the same fingerprint
+            fpath = os.path.join(OUT, f"pmc3_{wl}_fingerprint.json")
+            if os.path.exists(fpath):
+                with open(fpath) as f:
+                    w["fingerprint"] = json.load(f)
             res["workloads"][wl] = w
             print(wl, f"step HBM {w['step_hbm_bytes'] / 1e9:.3f} GB (read {w['step_read_bytes'] / 1e9:.3f}, "
                       f"write {w['step_write_bytes'] / 1e9:.3f})")
