@@ -67,6 +67,12 @@ def parse():
                     help="config E with N > 1: the node as one client (RCCL all-reduce of the counts, "
                          "the north star's global tier; default) or every rank a client (all-gather); "
                          "the other mode's refresh epoch is timed after the timed region too")
+    ap.add_argument("--owner-map", choices=("hash", "balanced"), default=None,
+                    help="N > 1: owner of a key = the hash partition (SURVEY.md §8e) or a balanced owner map "
+                         "built from step 0's all-reduced virtual-node loads (DESIGN.md §7; default for zipf)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="zipf, one GPU: emulate config C's owners at this many GPUs one at a time "
+                         "(bench_emul.py; the line is marked as an emulation)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on cuda:0 with the gloo backend (the "
                          "device path's collectives stage through host memory); the line is marked "
@@ -116,6 +122,8 @@ def parse():
         args.period_ticks = args.interval_us * 10 if args.workload == "approx" else 10_000_000
     if args.workload == "approx" and args.tokens_per_period == 1:
         args.tokens_per_period = 10
+    if args.owner_map is None:
+        args.owner_map = "balanced" if args.workload == "zipf" else "hash"
     return args
 
 
@@ -155,12 +163,14 @@ def dist_setup(args):
     if dist:
         print(f"bench.py: rank {rank} of {world}", file=sys.stderr, flush=True)
     gpu = 0 if args.share_device else local_rank
+    if dist and args.share_device:
+        # gloo first: both ranks have reported in before either touches the device
+        import torch.distributed as td
+        td.init_process_group("gloo")
     torch.cuda.set_device(gpu)
     if dist:
         import torch.distributed as td
-        if args.share_device:
-            td.init_process_group("gloo")
-        else:
+        if not args.share_device:
             td.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         if td.get_world_size() != args.gpus:
             print(f"bench.py: process group has {td.get_world_size()} ranks, --gpus {args.gpus}",
@@ -183,6 +193,13 @@ def main():
     lib.tbe_gen_batch_device.restype = ctypes.c_int
     lib.tbe_gen_batch_device.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_int32] * 2 + \
         [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 4
+    if args.emulate_world:
+        import bench_emul
+        if args.workload != "zipf" or world != 1:
+            print("bench.py: --emulate-world needs --workload zipf on one GPU", file=sys.stderr)
+            sys.exit(2)
+        print(json.dumps(bench_emul.run(args, lib, dev)), flush=True)
+        return
     if args.workload in ("queue", "approx"):
         import bench_kinds
         line = bench_kinds.run(args, lib, dev, world, rank, dist)
@@ -209,32 +226,43 @@ def main():
     else:
         keys_total = args.keys or (10_000 if args.workload == "testapp" else 100_000_000)
     from distributedratelimiting.redis_amd import cluster
-    keys_local = cluster.keys_per_rank(keys_total, world)
     n = args.batch
     total_steps = args.warmup + args.steps
     routed = dist and args.workload != "testapp"
     if routed:   # the device path orders the engine on a real stream (cluster.device_stream)
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     seed = {"zipf": SEED_C, "testapp": SEED_A}.get(args.workload, SEED_B)
+    gen_stream = torch.cuda.current_stream(dev).cuda_stream or None
+
+    def gen_batch(s):   # this rank's share of the global stream at step s
+        g0 = (s * world + rank) * n
+        k = torch.empty(n, dtype=torch.int64, device=dev)
+        p = torch.empty(n, dtype=torch.int32, device=dev)
+        t = torch.empty(n, dtype=torch.int64, device=dev)
+        assert lib.tbe_gen_batch_device(seed, keys_total, g0, n, 1, 1, T0_US + s * args.interval_us,
+                                        args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), gen_stream) == 0
+        if args.workload == "zipf":
+            assert lib.tbe_gen_zipf_keys_device(seed, keys_total, args.zipf_s, g0, n, k.data_ptr(), gen_stream) == 0
+        return k, p, t
+
+    # the owner map (N > 1): the hash partition, or balanced from step 0's virtual-node loads
+    # summed over the ranks, so every rank builds the same map before any key is routed
+    omap = None
+    if routed and args.owner_map == "balanced":
+        loads = cluster.vnode_loads(gen_batch(0)[0])
+        cluster._all_reduce_sum(loads)
+        omap = cluster.balanced_owner_map(loads.cpu().numpy(), world)
+    keys_local = cluster.keys_per_rank(keys_total, world, owner_map=omap)
     # --route timed: the directory's overflow check must not synchronise inside a step
     directory = cluster.DeviceDirectory(keys_local, device=dev.index, strict=args.route != "timed") \
         if routed else None
     bufs, raw = [], []
-    # generate on the current stream: the routing kernels run on it too (a torch stream does
+    # generated on the current stream: the routing kernels run on it too (a torch stream does
     # not wait for the legacy NULL stream)
-    gen_stream = torch.cuda.current_stream(dev).cuda_stream or None
     for s in range(total_steps):
-        g0 = (s * world + rank) * n          # this rank's share of the global stream
-        k = torch.empty(n, dtype=torch.int64, device=dev)
-        p = torch.empty(n, dtype=torch.int32, device=dev)
-        t = torch.empty(n, dtype=torch.int64, device=dev)
-        rc = lib.tbe_gen_batch_device(seed, keys_total, g0, n, 1, 1, T0_US + s * args.interval_us,
-                                      args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), gen_stream)
-        assert rc == 0
-        if args.workload == "zipf":
-            assert lib.tbe_gen_zipf_keys_device(seed, keys_total, args.zipf_s, g0, n, k.data_ptr(), gen_stream) == 0
+        k, p, t = gen_batch(s)
         if routed and args.route == "pre":
-            (lk, lp, lt), _ = cluster.route_requests(k, p, t, directory)
+            (lk, lp, lt), _ = cluster.route_requests(k, p, t, directory, owner_map=omap)
             bufs.append((lk, lp, lt))
         elif routed:
             raw.append((k, p, t))
@@ -265,7 +293,7 @@ def main():
 
     def step(s):
         if raw:
-            g, r = cluster.route_batch(decide, *raw[s], directory)
+            g, r = cluster.route_batch(decide, *raw[s], directory, owner_map=omap)
             granted.copy_(g)
             remaining.copy_(r)
         else:
@@ -492,8 +520,10 @@ def main():
                        "token_limit": args.token_limit, "tokens_per_period": args.tokens_per_period,
                        "period_ticks": args.period_ticks, "interval_us": args.interval_us,
                        "partitioning": ("one GPU owns every key" if world == 1 else
-                                        f"owner = mix64(key) >> (64 - log2 {world}); each rank draws its "
-                                        f"share of one global stream, routed to the owners "
+                                        (f"owner = mix64(key) >> (64 - log2 {world})" if omap is None else
+                                         "owner = a balanced owner map (cluster.balanced_owner_map of step 0's "
+                                         "all-reduced virtual-node loads)") +
+                                        "; each rank draws its share of one global stream, routed to the owners "
                                         + ("before the timed region (ingest partitioned, no "
                                            "data-path collective timed)" if args.route == "pre" else
                                            "inside every timed step (RCCL all-to-all both ways)")),

@@ -62,7 +62,7 @@ PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles
 # profiles/pmc_summary.json and compared key by key with the run that reports the bytes
 FINGERPRINT_KEYS = ("workload", "world", "keys_per_gpu", "batch", "steps", "warmup", "token_limit",
                     "tokens_per_period", "period_ticks", "interval_us", "queue_limit", "route",
-                    "share_device", "layout", "engine_sources_sha256")
+                    "owner_map", "share_device", "layout", "engine_sources_sha256")
 
 
 def run_fingerprint(args, world: int, keys_per_gpu: int, layout: dict) -> dict:
@@ -74,7 +74,9 @@ def run_fingerprint(args, world: int, keys_per_gpu: int, layout: dict) -> dict:
             "token_limit": int(args.token_limit), "tokens_per_period": int(args.tokens_per_period),
             "period_ticks": int(args.period_ticks), "interval_us": int(args.interval_us),
             "queue_limit": int(args.queue_limit) if args.workload == "queue" else None,
-            "route": args.route if world > 1 else None, "share_device": bool(args.share_device),
+            "route": args.route if world > 1 else None,
+            "owner_map": getattr(args, "owner_map", None) if world > 1 else None,
+            "share_device": bool(args.share_device),
             "layout": {k: layout[k] for k in sorted(layout)},
             "engine_sources_sha256": _digest(DEPS, HIPCC_FLAGS)}
 

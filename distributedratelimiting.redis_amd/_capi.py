@@ -162,6 +162,13 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_route_workspace_bytes.argtypes = [c_uint64, c_uint32]
     lib.tbe_route_plan_device.restype = c_int32
     lib.tbe_route_plan_device.argtypes = [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.tbe_route_plan_map_device.restype = c_int32
+    lib.tbe_route_plan_map_device.argtypes = [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]
+    lib.tbe_key_vnode.restype = c_uint32
+    lib.tbe_key_vnode.argtypes = [c_uint64]
+    lib.tbe_vnode_count_device.restype = c_int32
+    lib.tbe_vnode_count_device.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p]
     lib.tbe_route_pack_device.restype = c_int32
     lib.tbe_route_pack_device.argtypes = [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.tbe_route_gather_device.restype = c_int32

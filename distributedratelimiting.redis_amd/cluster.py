@@ -6,7 +6,10 @@ has exactly one owner GPU holding its bucket state:
 
     owner(key) = ((mix64(key) >> 32) * world) >> 32      (= mix64(key) >> (64 - log2 world))
 
-and the owner's key directory (``tbe_dir_*``, device-resident and collision-free: it
+or, with an owner map (every routing call takes ``owner_map=``), the map's entry for the
+key's virtual node (the top 12 bits of mix64(key)): ``balanced_owner_map`` builds one from
+observed per-virtual-node loads so that a Zipf stream's hot keys do not overload their
+owners, and the owner's key directory (``tbe_dir_*``, device-resident and collision-free: it
 stores whole keys) turns the keys it owns into dense bucket ids.  The token-bucket paths
 need no collective when ingest is already partitioned (the benchmark's default mode).
 Exchanges:
@@ -60,12 +63,60 @@ def _mix64(z: np.ndarray) -> np.ndarray:
     return z
 
 
-def key_owner(keys, world: int) -> np.ndarray:
+def key_owner(keys, world: int, owner_map=None) -> np.ndarray:
     """Owner rank of each key (csrc/tbe_hash.hpp key_owner): ((mix64(key) >> 32) * world)
-    >> 32, i.e. the top log2(world) bits of mix64(key) for a power-of-two world."""
+    >> 32, i.e. the top log2(world) bits of mix64(key) for a power-of-two world; with an
+    owner map (include/tbe_cluster.h), owner_map[key_vnode(key)]."""
+    if owner_map is not None:
+        return np.asarray(owner_map, dtype=np.int64)[key_vnode(keys)]
     h = _mix64(keys) >> np.uint64(32)
     with np.errstate(over="ignore"):
         return ((h * np.uint64(world)) >> np.uint64(32)).astype(np.int64)
+
+
+# ------------------------------------------------------------------ owner maps
+OWNER_MAP_BITS = 12                  # include/tbe_cluster.h TBE_OWNER_MAP_BITS
+OWNER_MAP_SIZE = 1 << OWNER_MAP_BITS
+
+
+def key_vnode(keys) -> np.ndarray:
+    """Virtual node of each key: the top 12 bits of mix64(key) (tbe_key_vnode)."""
+    return (_mix64(keys) >> np.uint64(64 - OWNER_MAP_BITS)).astype(np.int64)
+
+
+def hash_owner_map(world: int) -> np.ndarray:
+    """The owner map equal to the hash partition for a power-of-two world:
+    v -> (v * world) >> 12."""
+    if world & (world - 1) or not 1 <= world <= OWNER_MAP_SIZE:
+        raise ValueError("the hash owner map needs a power-of-two world <= 4096")
+    return ((np.arange(OWNER_MAP_SIZE, dtype=np.int64) * world) >> OWNER_MAP_BITS).astype(np.uint8)
+
+
+def balanced_owner_map(loads, world: int) -> np.ndarray:
+    """An owner map that evens out the owners' request loads (DESIGN.md §7 "owner maps").
+    loads[v] = requests observed on virtual node v (e.g. all ranks' vnode counts of a
+    batch, all-reduced so that every rank builds the same map).  Longest processing time
+    first: virtual nodes by descending load (ties by index), each to the owner with the
+    least load so far (ties to the lowest rank), virtual nodes without load spread so that
+    every owner ends with about the same number of them (its share of the key space).
+    Deterministic: the same loads give the same map on every rank."""
+    loads = np.asarray(loads, dtype=np.int64).reshape(-1)
+    if loads.size != OWNER_MAP_SIZE or world < 1 or world > 256:
+        raise ValueError("loads must have 4096 entries and 1 <= world <= 256")
+    order = np.lexsort((np.arange(OWNER_MAP_SIZE), -loads))
+    out = np.empty(OWNER_MAP_SIZE, dtype=np.uint8)
+    acc = np.zeros(world, dtype=np.int64)
+    nv = np.zeros(world, dtype=np.int64)
+    cap_v = -(-OWNER_MAP_SIZE // world)
+    for v in order.tolist():
+        if loads[v] > 0:
+            r = int(np.argmin(acc))
+        else:   # no load seen: keep the owners' shares of the key space level
+            r = int(np.argmin(np.where(nv < cap_v, nv, OWNER_MAP_SIZE + 1)))
+        out[v] = r
+        acc[r] += loads[v]
+        nv[r] += 1
+    return out
 
 
 def _scramble_params(n: int):
@@ -233,11 +284,38 @@ class DeviceDirectory:
         return n.value
 
 
-def keys_per_rank(n_keys: int, world: int, slack: float = 0.01) -> int:
+def keys_per_rank(n_keys: int, world: int, slack: float = 0.01, owner_map=None) -> int:
     """Table capacity per rank for n_keys hash-partitioned keys: the expected share plus
-    a margin far above the binomial spread of the owner counts."""
-    share = -(-n_keys // world)
-    return n_keys if world == 1 else min(n_keys, int(share * (1.0 + slack)) + 1024)
+    a margin far above the binomial spread of the owner counts.  With an owner map, the
+    share of the owner with the most virtual nodes (each holds 1/4096 of the keys)."""
+    if world == 1:
+        return n_keys
+    if owner_map is not None:
+        most = int(np.bincount(np.asarray(owner_map, dtype=np.int64), minlength=world).max())
+        share = -(-n_keys * most // OWNER_MAP_SIZE)
+    else:
+        share = -(-n_keys // world)
+    return min(n_keys, int(share * (1.0 + slack)) + 1024)
+
+
+def vnode_loads(d_keys):
+    """Requests per virtual node of a device batch (tbe_vnode_count_device): int64 [4096]."""
+    import torch
+    from . import _capi
+    lib = _capi.load()
+    d_keys = _device_columns(d_keys)[0]
+    out = torch.empty(OWNER_MAP_SIZE, dtype=torch.int64, device=d_keys.device)
+    _check(lib.tbe_vnode_count_device(d_keys.data_ptr(), d_keys.numel(), out.data_ptr(), device_stream(d_keys.device)))
+    return out
+
+
+def _device_map(owner_map, dev):
+    """The owner map as a u8 device tensor (NULL pointer for the hash partition)."""
+    if owner_map is None:
+        return None
+    import torch
+    m = owner_map if _is_cuda(owner_map) else torch.from_numpy(np.ascontiguousarray(owner_map, dtype=np.uint8))
+    return m.to(device=dev, dtype=torch.uint8).contiguous()
 
 
 # ------------------------------------------------------------------ collectives
@@ -291,10 +369,11 @@ def _is_cuda(x) -> bool:
     return hasattr(x, "is_cuda") and x.is_cuda
 
 
-def route_requests(keys, permits, ts_us, directory, group=None):
+def route_requests(keys, permits, ts_us, directory, group=None, owner_map=None):
     """Send this rank's requests to their owners.  Returns ((local ids, permits, ts) of
     the requests this rank owns, in (source rank, arrival) order, and the RoutePlan for
-    route_replies).  CUDA tensors: device kernels + RCCL; numpy: host path + gloo."""
+    route_replies).  CUDA tensors: device kernels + RCCL; numpy: host path + gloo.
+    owner_map: table-driven ownership (balanced_owner_map), the same on every rank."""
     import torch
     import torch.distributed as dist
 
@@ -302,13 +381,13 @@ def route_requests(keys, permits, ts_us, directory, group=None):
     if _is_cuda(keys):
         dev = keys.device
         keys, permits, ts_us = _device_columns(keys, (permits, torch.int32), (ts_us, torch.int64))
-        pos, sc_l, rc_l, recv = _route_device(keys, permits, ts_us, world, group)
+        pos, sc_l, rc_l, recv = _route_device(keys, permits, ts_us, world, group, owner_map)
         local = directory.assign(recv[:, 0])
         directory.check()        # an over-capacity batch raises before anything is decided
         return (local, recv[:, 2].to(torch.int32), recv[:, 1].contiguous()), RoutePlan(pos, sc_l, rc_l, keys.numel())
     keys = np.asarray(keys, dtype=np.uint64)
     n = keys.shape[0]
-    owner = key_owner(keys, world)
+    owner = key_owner(keys, world, owner_map)
     order = np.argsort(owner, kind="stable")
     send_counts = np.bincount(owner, minlength=world).astype(np.int64)
     sc = torch.from_numpy(send_counts)
@@ -346,9 +425,9 @@ def _device_columns(keys, *cols):
     return tuple(out)
 
 
-def _route_device(keys, permits, payload, world, group):
+def _route_device(keys, permits, payload, world, group, owner_map=None):
     """Owner-grouped exchange of {key, payload i64, permits i32} records on the device:
-    tbe_route_plan_device + tbe_route_pack_device, the split sizes by all-to-all, the
+    tbe_route_plan_map_device + tbe_route_pack_device, the split sizes by all-to-all, the
     records by all-to-all.  Returns (pos, send counts, recv counts, recv [m, 3] int64)."""
     import torch
     from . import _capi
@@ -359,8 +438,9 @@ def _route_device(keys, permits, payload, world, group):
     pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     counts = torch.zeros(world, dtype=torch.int64, device=dev)
     work = torch.empty(max(1, lib.tbe_route_workspace_bytes(n, world)), dtype=torch.uint8, device=dev)
-    _check(lib.tbe_route_plan_device(keys.data_ptr(), n, world, work.data_ptr(), pos.data_ptr(),
-                                     counts.data_ptr(), stream))
+    dmap = _device_map(owner_map, dev)
+    _check(lib.tbe_route_plan_map_device(keys.data_ptr(), n, world, dmap.data_ptr() if dmap is not None else None,
+                                         work.data_ptr(), pos.data_ptr(), counts.data_ptr(), stream))
     send = torch.empty((n, 3), dtype=torch.int64, device=dev)
     _check(lib.tbe_route_pack_device(pos.data_ptr(), n, keys.data_ptr(), permits.data_ptr(),
                                      payload.data_ptr(), send.data_ptr(), stream))
@@ -403,7 +483,7 @@ def route_replies(plan: RoutePlan, cols, group=None):
     return tuple(out[:, c] for c in range(k))
 
 
-def route_batch(decide: Callable, keys, permits, ts_us, directory, group=None):
+def route_batch(decide: Callable, keys, permits, ts_us, directory, group=None, owner_map=None):
     """Decide a batch whose requests arrived at this rank but may belong to any rank.
 
     ``decide(local_ids, permits, ts) -> (col0, col1[, ...])`` runs this rank's engine on
@@ -411,7 +491,7 @@ def route_batch(decide: Callable, keys, permits, ts_us, directory, group=None):
     ids it assigns, which a later ``route_cancel`` needs).  Returns the columns for this
     rank's own requests in their arrival order: granted/status as u8, remaining as i32,
     further columns as i64 (host path) or the int64 device tensors (device path)."""
-    (lk, lp, lt), plan = route_requests(keys, permits, ts_us, directory, group)
+    (lk, lp, lt), plan = route_requests(keys, permits, ts_us, directory, group, owner_map)
     cols = decide(lk, lp, lt)
     out = route_replies(plan, cols, group)
     if _is_cuda(out[0]):
@@ -420,7 +500,7 @@ def route_batch(decide: Callable, keys, permits, ts_us, directory, group=None):
     return (out[0].astype(np.uint8), out[1].astype(np.int32)) + tuple(out[2:])
 
 
-def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
+def route_cancel(cancel: Callable, keys, request_ids, directory, group=None, owner_map=None):
     """Cancel queued requests (CancelQueueState.TrySetCanceled, Q:480-506 / A:531-557)
     that may be queued on any rank: ``keys`` are global keys, ``request_ids`` the ids
     their owners assigned (``route_batch``'s extra reply column).  ``cancel(local_ids,
@@ -432,12 +512,12 @@ def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
 
     world = dist.get_world_size(group)
     if _is_cuda(keys):
-        return _route_cancel_device(cancel, keys, request_ids, directory, world, group)
+        return _route_cancel_device(cancel, keys, request_ids, directory, world, group, owner_map)
     if isinstance(directory, DeviceDirectory):
         raise TypeError("route_cancel with a DeviceDirectory takes CUDA tensors of keys and request ids")
     keys = np.asarray(keys, dtype=np.uint64)
     n = keys.shape[0]
-    owner = key_owner(keys, world)
+    owner = key_owner(keys, world, owner_map)
     order = np.argsort(owner, kind="stable")
     send_counts = np.bincount(owner, minlength=world).astype(np.int64)
     sc = torch.from_numpy(send_counts)
@@ -464,7 +544,7 @@ def route_cancel(cancel: Callable, keys, request_ids, directory, group=None):
     return out
 
 
-def _route_cancel_device(cancel, keys, request_ids, directory, world, group):
+def _route_cancel_device(cancel, keys, request_ids, directory, world, group, owner_map=None):
     """route_cancel's device path: (key, request id) pairs go to the owners through the
     route kernels (the id rides in the record's i64 payload), the owner's DeviceDirectory
     looks the keys up (a key it never assigned has nothing queued), ``cancel(local ids,
@@ -477,7 +557,7 @@ def _route_cancel_device(cancel, keys, request_ids, directory, world, group):
     keys, request_ids = _device_columns(keys, (request_ids, torch.int64))
     dev = keys.device
     zero = torch.zeros(keys.numel(), dtype=torch.int32, device=dev)
-    pos, sc_l, rc_l, recv = _route_device(keys, zero, request_ids, world, group)
+    pos, sc_l, rc_l, recv = _route_device(keys, zero, request_ids, world, group, owner_map)
     hit = torch.zeros(recv.shape[0], dtype=torch.int64, device=dev)
     if recv.shape[0]:
         local = directory.lookup(recv[:, 0])

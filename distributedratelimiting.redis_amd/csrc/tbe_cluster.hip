@@ -27,18 +27,35 @@ constexpr int kRtItems = 8;
 constexpr int kRtTile = kRtBlock * kRtItems;   // 4096 requests per routing tile
 constexpr uint32_t kMaxOwners = 256;
 
+// Owner of a key: the hash partition, or the owner map's entry for its virtual node
+// (`m` = the workgroup's LDS copy of the map, filled by load_owner_map).
+__device__ __forceinline__ uint32_t route_owner(uint64_t key, uint32_t G, const uint8_t *m) {
+    return m ? (uint32_t)m[key_vnode(key)] : key_owner(key, G);
+}
+__device__ __forceinline__ const uint8_t *load_owner_map(const uint8_t *__restrict__ omap, uint8_t *lds) {
+    if (!omap) return nullptr;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(omap);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+    for (uint32_t j = threadIdx.x; j < kOwnerMapSize / 4; j += blockDim.x) dst[j] = src[j];
+    __syncthreads();
+    return lds;
+}
+
 // Per-tile request count of every owner.
 __global__ __launch_bounds__(kRtBlock) void k_route_count(const uint64_t *__restrict__ keys, uint64_t n,
-                                                          uint32_t G, uint32_t *__restrict__ tile_counts) {
+                                                          uint32_t G, const uint8_t *__restrict__ omap,
+                                                          uint32_t *__restrict__ tile_counts) {
     __shared__ uint32_t c[kMaxOwners];
+    __shared__ __attribute__((aligned(16))) uint8_t mlds[kOwnerMapSize];
     const int tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kRtTile;
     for (uint32_t j = tid; j < G; j += kRtBlock) c[j] = 0;
+    const uint8_t *m = load_owner_map(omap, mlds);   // (its barrier also publishes c[])
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kRtItems; ++it) {
         const uint64_t i = base + (uint64_t)it * kRtBlock + tid;
-        if (i < n) atomicAdd(&c[key_owner(keys[i], G)], 1u);
+        if (i < n) atomicAdd(&c[route_owner(keys[i], G, m)], 1u);
     }
     __syncthreads();
     for (uint32_t j = tid; j < G; j += kRtBlock) tile_counts[(uint64_t)blockIdx.x * G + j] = c[j];
@@ -87,19 +104,22 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t *__restric
 // in that owner's group + the request's stable rank among the tile's requests of that
 // owner (wave ballot-match ranking, as the partition passes use).
 __global__ __launch_bounds__(kRtBlock) void k_route_pos(const uint64_t *__restrict__ keys, uint64_t n, uint32_t G,
+                                                        const uint8_t *__restrict__ omap,
                                                         const uint32_t *__restrict__ tile_off,
                                                         const uint32_t *__restrict__ owner_base,
                                                         uint32_t *__restrict__ pos) {
     __shared__ RankLds<kRtBlock> L;
     __shared__ uint16_t cnt[kRtItems * (kRtBlock / 64) * kDigits];
+    __shared__ __attribute__((aligned(16))) uint8_t mlds[kOwnerMapSize];
     const int tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kRtTile;
     const int nvalid = (int)min<uint64_t>(kRtTile, n - base);
+    const uint8_t *m = load_owner_map(omap, mlds);
     uint32_t own[kRtItems], lpos[kRtItems];
 #pragma unroll
     for (int it = 0; it < kRtItems; ++it) {
         const int e = it * kRtBlock + tid;
-        own[it] = e < nvalid ? key_owner(keys[base + e], G) : 0u;
+        own[it] = e < nvalid ? route_owner(keys[base + e], G, m) : 0u;
     }
     rank_tile<kRtBlock, kRtItems>(own, 0, nvalid, L, cnt, lpos);
 #pragma unroll
@@ -110,6 +130,21 @@ __global__ __launch_bounds__(kRtBlock) void k_route_pos(const uint64_t *__restri
             pos[base + e] = owner_base[o] + tile_off[(uint64_t)blockIdx.x * G + o] + lpos[it] - L.lstart[o];
         }
     }
+}
+
+// Requests per virtual node (owner-map balancing): an LDS histogram per workgroup over a
+// grid-stride range, added to the 4096 global counters once.
+__global__ __launch_bounds__(kRtBlock) void k_vnode_count(const uint64_t *__restrict__ keys, uint64_t n,
+                                                          unsigned long long *__restrict__ counts) {
+    __shared__ uint32_t h[kOwnerMapSize];
+    for (uint32_t j = threadIdx.x; j < kOwnerMapSize; j += kRtBlock) h[j] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kRtBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kRtBlock + threadIdx.x; i < n; i += stride)
+        atomicAdd(&h[key_vnode(keys[i])], 1u);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kOwnerMapSize; j += kRtBlock)
+        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
 }
 
 __global__ void k_route_pack(const uint32_t *__restrict__ pos, uint64_t n, const uint64_t *__restrict__ keys,
@@ -346,16 +381,35 @@ uint64_t tbe_route_workspace_bytes(uint64_t n, uint32_t n_owners) {
 
 tbe_status tbe_route_plan_device(const uint64_t *d_keys, uint64_t n, uint32_t n_owners, void *d_work,
                                  uint32_t *d_pos, uint64_t *d_counts, void *stream) {
+    return tbe_route_plan_map_device(d_keys, n, n_owners, nullptr, d_work, d_pos, d_counts, stream);
+}
+
+uint32_t tbe_key_vnode(uint64_t key) { return key_vnode(key); }
+
+tbe_status tbe_route_plan_map_device(const uint64_t *d_keys, uint64_t n, uint32_t n_owners,
+                                     const uint8_t *d_owner_map, void *d_work, uint32_t *d_pos,
+                                     uint64_t *d_counts, void *stream) {
     if (n_owners == 0 || n_owners > kMaxOwners || n >= (1ull << 32) || !d_counts) return TBE_EINVAL;
+    if (d_owner_map && (reinterpret_cast<uintptr_t>(d_owner_map) & 3u)) return TBE_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) return hipMemsetAsync(d_counts, 0, n_owners * sizeof(uint64_t), st) == hipSuccess ? TBE_OK : TBE_EDEVICE;
     if (!d_keys || !d_work || !d_pos) return TBE_EINVAL;
     const uint32_t ntiles = (uint32_t)((n + kRtTile - 1) / kRtTile);
     uint32_t *tile = static_cast<uint32_t *>(d_work);
     uint32_t *obase = tile + (uint64_t)ntiles * n_owners;
-    k_route_count<<<ntiles, kRtBlock, 0, st>>>(d_keys, n, n_owners, tile);
+    k_route_count<<<ntiles, kRtBlock, 0, st>>>(d_keys, n, n_owners, d_owner_map, tile);
     k_route_scan<<<1, kScanThreads, 0, st>>>(tile, ntiles, n_owners, d_counts, obase);
-    k_route_pos<<<ntiles, kRtBlock, 0, st>>>(d_keys, n, n_owners, tile, obase, d_pos);
+    k_route_pos<<<ntiles, kRtBlock, 0, st>>>(d_keys, n, n_owners, d_owner_map, tile, obase, d_pos);
+    return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
+}
+
+tbe_status tbe_vnode_count_device(const uint64_t *d_keys, uint64_t n, uint64_t *d_counts, void *stream) {
+    if (!d_counts || (n && !d_keys)) return TBE_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(d_counts, 0, kOwnerMapSize * sizeof(uint64_t), st) != hipSuccess) return TBE_EDEVICE;
+    if (n == 0) return TBE_OK;
+    k_vnode_count<<<grid_for(n, kRtBlock, 1024), kRtBlock, 0, st>>>(
+        d_keys, n, reinterpret_cast<unsigned long long *>(d_counts));
     return hipGetLastError() == hipSuccess ? TBE_OK : TBE_EDEVICE;
 }
 

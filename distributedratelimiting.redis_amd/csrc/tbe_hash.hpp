@@ -26,6 +26,13 @@ TBE_HASH_HD inline uint32_t key_owner(uint64_t key, uint32_t n) {
     return (uint32_t)(((mix64(key) >> 32) * (uint64_t)n) >> 32);
 }
 
+// Virtual node of a key for table-driven ownership (include/tbe_cluster.h owner maps):
+// the top kOwnerMapBits bits of mix64(key).  An owner map assigns each of the 4096 virtual
+// nodes to a GPU; the map v -> (v * n) >> 12 reproduces key_owner for n = 2^g <= 4096.
+constexpr int kOwnerMapBits = 12;
+constexpr uint32_t kOwnerMapSize = 1u << kOwnerMapBits;
+TBE_HASH_HD inline uint32_t key_vnode(uint64_t key) { return (uint32_t)(mix64(key) >> (64 - kOwnerMapBits)); }
+
 // A fixed bijection of [0, 2^bits): odd multiply-add then xorshift, three rounds
 // (workloads.py _scramble); `mask` = 2^bits - 1, `sh` = max(1, bits / 2).
 TBE_HASH_HD inline uint64_t scramble(uint64_t x, uint64_t mask, uint32_t sh) {

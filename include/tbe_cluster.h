@@ -42,6 +42,26 @@ uint64_t tbe_route_workspace_bytes(uint64_t n, uint32_t n_owners);
 tbe_status tbe_route_plan_device(const uint64_t *d_keys, uint64_t n, uint32_t n_owners, void *d_work,
                                  uint32_t *d_pos, uint64_t *d_counts, void *stream);
 
+/* ---------------------------------------------------------------- owner maps
+ * Table-driven ownership (DESIGN.md §7 "owner maps"): owner(key) = map[vnode(key)], with
+ * vnode(key) = mix64(key) >> 52, one of TBE_OWNER_MAP_SIZE virtual nodes, and `map` a u8
+ * array of TBE_OWNER_MAP_SIZE owners (4-byte aligned), the same on every GPU.  The map
+ * v -> (v * n_owners) >> 12 is the hash partition above for a power-of-two n_owners; a
+ * balanced map gives the virtual nodes of hot keys' owners fewer others, so a Zipf
+ * stream's owner loads even out (SURVEY.md §7 hard part iii).  A key still has exactly
+ * one owner; the map must not change while any owner holds state. */
+#define TBE_OWNER_MAP_BITS 12
+#define TBE_OWNER_MAP_SIZE 4096
+uint32_t tbe_key_vnode(uint64_t key);
+/* tbe_route_plan_device with owner = d_owner_map[vnode(key)] (d_owner_map NULL: the hash
+ * partition, exactly tbe_route_plan_device); every map entry must be < n_owners. */
+tbe_status tbe_route_plan_map_device(const uint64_t *d_keys, uint64_t n, uint32_t n_owners,
+                                     const uint8_t *d_owner_map, void *d_work, uint32_t *d_pos,
+                                     uint64_t *d_counts, void *stream);
+/* d_counts[v] (u64, TBE_OWNER_MAP_SIZE of them, zeroed first) = requests of the batch on
+ * virtual node v: the load histogram a balanced map is built from. */
+tbe_status tbe_vnode_count_device(const uint64_t *d_keys, uint64_t n, uint64_t *d_counts, void *stream);
+
 /* Send buffer of the routing all-to-all: out[pos[i]] = {key, ts_us, permits} as three
  * int64 per request (d_out holds 3n). */
 tbe_status tbe_route_pack_device(const uint32_t *d_pos, uint64_t n, const uint64_t *d_keys,

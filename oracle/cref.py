@@ -205,6 +205,13 @@ class CQueueingTokenBucket:
         m = min(nl.value, cap)
         return lk[:m].copy(), lid[:m].copy(), lrem[:m].copy()
 
+    def cancel(self, keys, ids) -> np.ndarray:
+        """tbrq_cancel per (key, request id) pair in order: 1 where it was queued."""
+        self._lib.tbrq_cancel.restype = c_int
+        self._lib.tbrq_cancel.argtypes = [c_void_p, c_uint64, c_int64]
+        return np.array([self._lib.tbrq_cancel(self._h, int(k), int(i))
+                         for k, i in zip(np.asarray(keys).tolist(), np.asarray(ids).tolist())], dtype=np.uint8)
+
     def queue_of(self, key: int):
         ids = np.empty(max(1, self.queue_limit), np.int64)
         ps = np.empty(max(1, self.queue_limit), np.int32)
@@ -305,6 +312,13 @@ class CApprox:
         self._lib.tba_export(self._h, *[out[k].ctypes.data for k in
                                         ("local", "global", "est", "available", "queued", "v", "p", "t_us")])
         return out
+
+    def cancel(self, keys, ids) -> np.ndarray:
+        """tba_cancel per (key, request id) pair in order: 1 where it was queued."""
+        self._lib.tba_cancel.restype = c_int
+        self._lib.tba_cancel.argtypes = [c_void_p, c_uint64, c_int64]
+        return np.array([self._lib.tba_cancel(self._h, int(k), int(i))
+                         for k, i in zip(np.asarray(keys).tolist(), np.asarray(ids).tolist())], dtype=np.uint8)
 
     def queue_of(self, key: int):
         cap = max(1, self.queue_limit) + self.zero_slots

@@ -488,6 +488,26 @@ uint32_t tbrq_queue_of(const tbrq_table *q, uint64_t key, int64_t *ids, int32_t 
 
 tbr_table *tbrq_bucket_table(tbrq_table *q) { return q->tb; }
 
+/* CancelQueueState.TrySetCanceled (Q:480-506), as oracle/semantics.py
+ * QueueingTokenBucketTable.cancel: 1 iff `id` was queued on `key`; _queueCount drops by its
+ * permits (Q:499) and the registration leaves the deque at once, the entries behind it
+ * closing up in order. */
+int tbrq_cancel(tbrq_table *q, uint64_t key, int64_t id) {
+    uint32_t cap = q->ring_cap, c = q->count[key], h = q->head[key];
+    uint64_t base = key * cap;
+    for (uint32_t j = 0; j < c; ++j) {
+        if (q->ring_id[base + (h + j) % cap] != id) continue;
+        q->qsum[key] -= q->ring_p[base + (h + j) % cap];
+        for (uint32_t m = j; m + 1 < c; ++m) {
+            q->ring_id[base + (h + m) % cap] = q->ring_id[base + (h + m + 1) % cap];
+            q->ring_p[base + (h + m) % cap] = q->ring_p[base + (h + m + 1) % cap];
+        }
+        q->count[key] = c - 1;
+        return 1;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------ approximate limiter
  * C restatement of one client of ApproximateTokenBucket/RedisApproximateTokenBucketRateLimiter.cs
  * ("A"), for every key, plus that client's replica of the global tier (the Redis hash
@@ -792,6 +812,26 @@ void tba_export(const tba_table *a, int32_t *local, int32_t *global_score, doubl
 }
 
 /* Queue of one key, oldest first: returns the entry count. */
+/* CancelQueueState.TrySetCanceled (A:545-556), as oracle/semantics.py ApproxClient.cancel:
+ * 1 iff `id` was queued on `key`; _queueCount drops by its permits; removed at once. */
+int tba_cancel(tba_table *a, uint64_t key, int64_t id) {
+    uint32_t rc = a->ring_cap, c = a->count[key], h = a->head[key];
+    uint64_t base = key * rc;
+    for (uint32_t j = 0; j < c; ++j) {
+        if (a->ring_id[base + (h + j) % rc] != id) continue;
+        const int32_t p = a->ring_p[base + (h + j) % rc];
+        a->qsum[key] -= p;
+        if (p == 0) a->zc[key]--;
+        for (uint32_t m = j; m + 1 < c; ++m) {
+            a->ring_id[base + (h + m) % rc] = a->ring_id[base + (h + m + 1) % rc];
+            a->ring_p[base + (h + m) % rc] = a->ring_p[base + (h + m + 1) % rc];
+        }
+        a->count[key] = c - 1;
+        return 1;
+    }
+    return 0;
+}
+
 uint32_t tba_queue_of(const tba_table *a, uint64_t key, int64_t *ids, int32_t *permits, uint32_t max) {
     uint32_t c = a->count[key], rc = a->ring_cap;
     for (uint32_t j = 0; j < c && j < max; ++j) {

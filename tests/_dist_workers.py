@@ -38,20 +38,32 @@ def tb_batch(rank: int, step: int):
     return keys, permits, ts.astype(np.int64)
 
 
-def tb_route_worker(rank: int, world: int, port: int, out_dir: str):
+def tb_owner_map(world: int, kind: str):
+    """None (hash partition) or the balanced owner map of the test's whole stream (every
+    rank computes the same one from the same loads)."""
+    from distributedratelimiting.redis_amd import cluster
+    if kind != "balanced":
+        return None
+    keys = np.concatenate([tb_batch(r, s)[0] for r in range(world) for s in range(TB_STEPS)])
+    return cluster.balanced_owner_map(np.bincount(cluster.key_vnode(keys), minlength=cluster.OWNER_MAP_SIZE), world)
+
+
+def tb_route_worker(rank: int, world: int, port: int, out_dir: str, map_kind: str = "hash"):
     dist = _init(rank, world, port)
     from oracle import cref
     from oracle.semantics import fill_rate_per_second
     from distributedratelimiting.redis_amd import cluster
 
     rate = fill_rate_per_second(TB["tokens_per_period"], TB["period_ticks"])
-    cap = cluster.keys_per_rank(TB["n_keys"], world)
+    omap = tb_owner_map(world, map_kind)
+    cap = cluster.keys_per_rank(TB["n_keys"], world, owner_map=omap)
     directory = cluster.HostDirectory(cap)
     ref = cref.CTokenBucket(cap, TB["token_limit"], rate)
-    out = {}
+    out = {} if omap is None else {"owner_map": omap}
     for s in range(TB_STEPS):
         k, p, t = tb_batch(rank, s)
-        g, r = cluster.route_batch(lambda lk, lp, lt: ref.acquire_batch(lk, lp, lt), k, p, t, directory)
+        g, r = cluster.route_batch(lambda lk, lp, lt: ref.acquire_batch(lk, lp, lt), k, p, t, directory,
+                                   owner_map=omap)
         out[f"g{s}"], out[f"r{s}"] = g, r
     v, tt = ref.export_state()
     out["v"], out["t"] = v, tt
@@ -212,11 +224,11 @@ def _hip_setup():
     return torch, dev, stream
 
 
-def _owned_keys(batch_fn, steps: int, rank: int, world: int) -> np.ndarray:
+def _owned_keys(batch_fn, steps: int, rank: int, world: int, owner_map=None) -> np.ndarray:
     """Every key this rank owns among all ranks' batches (each rank can compute them)."""
     from distributedratelimiting.redis_amd import cluster
     keys = np.unique(np.concatenate([batch_fn(r, s)[0] for r in range(world) for s in range(steps)]))
-    return keys[cluster.key_owner(keys, world) == rank].astype(np.uint64)
+    return keys[cluster.key_owner(keys, world, owner_map) == rank].astype(np.uint64)
 
 
 def _dir_ids(directory, keys: np.ndarray, torch, dev) -> np.ndarray:
@@ -226,14 +238,15 @@ def _dir_ids(directory, keys: np.ndarray, torch, dev) -> np.ndarray:
     return directory.lookup(keys)
 
 
-def tb_route_worker_hip(rank: int, world: int, port: int, out_dir: str, path: str):
+def tb_route_worker_hip(rank: int, world: int, port: int, out_dir: str, path: str, map_kind: str = "hash"):
     dist = _init(rank, world, port)
     torch, dev, stream = _hip_setup()
     from distributedratelimiting.redis_amd import TokenBucketEngine, cluster
 
-    cap = cluster.keys_per_rank(TB["n_keys"], world)
+    omap = tb_owner_map(world, map_kind)
+    cap = cluster.keys_per_rank(TB["n_keys"], world, owner_map=omap)
     eng = TokenBucketEngine(cap, TB["token_limit"], TB["tokens_per_period"], TB["period_ticks"], device=0)
-    out = {}
+    out = {} if omap is None else {"owner_map": omap}
     if path == "device":
         directory = cluster.DeviceDirectory(cap, device=0)
 
@@ -245,18 +258,19 @@ def tb_route_worker_hip(rank: int, world: int, port: int, out_dir: str, path: st
         for s in range(TB_STEPS):
             k, p, t = (torch.from_numpy(np.asarray(x).view(np.int64) if x.dtype == np.uint64 else x).to(dev)
                        for x in tb_batch(rank, s))
-            g, r = cluster.route_batch(decide, k, p, t, directory)
+            g, r = cluster.route_batch(decide, k, p, t, directory, owner_map=omap)
             out[f"g{s}"], out[f"r{s}"] = g.cpu().numpy(), r.cpu().numpy()
     else:
         directory = cluster.HostDirectory(cap)
         for s in range(TB_STEPS):
             k, p, t = tb_batch(rank, s)
-            g, r = cluster.route_batch(lambda lk, lp, lt: eng.acquire_batch(lk, lp, lt), k, p, t, directory)
+            g, r = cluster.route_batch(lambda lk, lp, lt: eng.acquire_batch(lk, lp, lt), k, p, t, directory,
+                                       owner_map=omap)
             out[f"g{s}"], out[f"r{s}"] = g, r
     eng.synchronize()
     v, tt = eng.export_state()
     out["v"], out["t"] = v, tt
-    owned = _owned_keys(tb_batch, TB_STEPS, rank, world)
+    owned = _owned_keys(tb_batch, TB_STEPS, rank, world, omap)
     out["dir_keys"], out["dir_ids"] = owned, _dir_ids(directory, owned, torch, dev)
     np.savez(os.path.join(out_dir, f"tb_{rank}.npz"), **out)
     eng.close()

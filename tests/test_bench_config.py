@@ -84,7 +84,8 @@ def test_gpus_n_spawns_n_ranks():
     if torch.cuda.is_available():
         pytest.skip("GPU visible: the spawned ranks would run the benchmark")
     p = _bench(["--gpus", "2", "--share-device", "--steps", "1", "--warmup", "0"])
-    assert p.returncode != 0 and not p.stdout.strip()
+    # (gloo's own connection messages may reach stdout; no JSON line may)
+    assert p.returncode != 0 and not [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert "bench.py: rank 0 of 2" in p.stderr and "bench.py: rank 1 of 2" in p.stderr
 
 

@@ -57,9 +57,44 @@ def test_key_owner_and_directory():
     assert small.overflow and out[2] == cluster.NO_ID
 
 
-def test_route_batch_matches_serial_reference(oracle_lib, tmp_path):
-    _spawn(W.tb_route_worker, str(tmp_path))
+@pytest.mark.parametrize("map_kind", ["hash", "balanced"])
+def test_route_batch_matches_serial_reference(oracle_lib, tmp_path, map_kind):
+    _spawn(W.tb_route_worker, str(tmp_path), map_kind)
     check_tb_route([np.load(tmp_path / f"tb_{r}.npz") for r in range(WORLD)])
+
+
+def test_owner_maps():
+    """Table-driven ownership (include/tbe_cluster.h owner maps): the hash map reproduces
+    the hash partition; the balanced map evens out a Zipf stream's owner loads that the
+    hash partition leaves ~1.7x uneven (SURVEY.md §7 hard part iii), keeps the owners'
+    shares of the key space level, is deterministic, and the host vnode function equals
+    the engine's (tbe_key_vnode)."""
+    from distributedratelimiting.redis_amd import _capi, cluster
+    keys = np.arange(300_000, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    for world in (1, 2, 4, 8, 64):
+        assert np.array_equal(cluster.key_owner(keys, world),
+                              cluster.key_owner(keys, world, cluster.hash_owner_map(world)))
+    lib = _capi.load()
+    assert [lib.tbe_key_vnode(int(k)) for k in keys[:2000]] == cluster.key_vnode(keys[:2000]).tolist()
+    # Zipf(1.1)-like loads: one key ~10% of the stream
+    rng = np.random.default_rng(3)
+    ranks = np.minimum(rng.zipf(1.1, 2_000_000), 10**9).astype(np.uint64)
+    zkeys = cluster._mix64(ranks)                  # rank -> key
+    loads = np.bincount(cluster.key_vnode(zkeys), minlength=cluster.OWNER_MAP_SIZE)
+    for world in (4, 8):
+        per_hash = np.bincount(cluster.key_owner(zkeys, world), minlength=world)
+        m = cluster.balanced_owner_map(loads, world)
+        assert np.array_equal(m, cluster.balanced_owner_map(loads.copy(), world))
+        per_bal = np.bincount(cluster.key_owner(zkeys, world, m), minlength=world)
+        assert per_hash.max() / per_hash.mean() > 1.3
+        assert per_bal.max() / per_bal.mean() < 1.01
+        nv = np.bincount(m, minlength=world)
+        assert nv.sum() == cluster.OWNER_MAP_SIZE and nv.min() > 0
+        cap = cluster.keys_per_rank(10**9, world, owner_map=m)
+        assert cap >= 10**9 * nv.max() // cluster.OWNER_MAP_SIZE
+    # no load at all: the shares of the key space stay level
+    m = cluster.balanced_owner_map(np.zeros(cluster.OWNER_MAP_SIZE, np.int64), 8)
+    assert np.bincount(m, minlength=8).tolist() == [512] * 8
 
 
 def check_tb_route(res):
@@ -81,9 +116,10 @@ def check_tb_route(res):
     from distributedratelimiting.redis_amd import cluster
     v, t = ref.export_state()
     seen = 0
+    omap = res[0]["owner_map"] if "owner_map" in res[0] else None
     for r in range(WORLD):
         keys, ids = res[r]["dir_keys"].astype(np.int64), res[r]["dir_ids"].astype(np.int64)
-        assert np.all(cluster.key_owner(keys.astype(np.uint64), WORLD) == r)   # the owner's keys only
+        assert np.all(cluster.key_owner(keys.astype(np.uint64), WORLD, omap) == r)   # the owner's keys only
         assert np.array_equal(res[r]["t"][ids], t[keys])
         assert np.array_equal(res[r]["v"][ids].view(np.int64), v[keys].view(np.int64))
         seen += keys.size

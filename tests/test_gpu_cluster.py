@@ -58,6 +58,40 @@ def test_route_plan_matches_host(engine_lib, gpu, n_owners, n):
     assert np.array_equal(b[:, 0].view(np.uint64), k) and np.array_equal(b[:, 1], np.arange(n) * 3)
 
 
+@pytest.mark.parametrize("n_owners", [2, 8, 256])
+@pytest.mark.parametrize("n", [4095, 300_000])
+def test_route_plan_owner_map_matches_host(engine_lib, gpu, n_owners, n):
+    """tbe_route_plan_map_device (owner = map[vnode(key)]) against the host mirror, for a
+    balanced map of the batch's own loads and a random map; tbe_vnode_count_device against
+    numpy's vnode histogram."""
+    import torch
+    from distributedratelimiting.redis_amd import _capi, cluster
+    lib = _capi.load()
+    k = _keys(n, n_owners * 11 + n, hot=0.3)
+    dk = torch.from_numpy(k.view(np.int64)).to(gpu)
+    loads = np.bincount(cluster.key_vnode(k), minlength=cluster.OWNER_MAP_SIZE)
+    side = torch.cuda.Stream(gpu)
+    with torch.cuda.stream(side):
+        got_loads = cluster.vnode_loads(dk).cpu().numpy()
+    assert np.array_equal(got_loads, loads)
+    rng = np.random.default_rng(n)
+    for omap in (cluster.balanced_owner_map(loads, n_owners),
+                 rng.integers(0, n_owners, cluster.OWNER_MAP_SIZE).astype(np.uint8)):
+        dmap = torch.from_numpy(omap).to(gpu)
+        pos = torch.empty(n, dtype=torch.int32, device=gpu)
+        counts = torch.empty(n_owners, dtype=torch.int64, device=gpu)
+        work = torch.empty(lib.tbe_route_workspace_bytes(n, n_owners), dtype=torch.uint8, device=gpu)
+        assert lib.tbe_route_plan_map_device(dk.data_ptr(), n, n_owners, dmap.data_ptr(), work.data_ptr(),
+                                             pos.data_ptr(), counts.data_ptr(), None) == 0
+        owner = cluster.key_owner(k, n_owners, omap)
+        order = np.argsort(owner, kind="stable")
+        want = np.empty(n, dtype=np.int64)
+        want[order] = np.arange(n)
+        torch.cuda.synchronize()
+        assert np.array_equal(pos.cpu().numpy().astype(np.int64), want)
+        assert np.array_equal(counts.cpu().numpy(), np.bincount(owner, minlength=n_owners))
+
+
 def test_directory_matches_host(engine_lib, gpu):
     import torch
     with torch.cuda.stream(torch.cuda.Stream(gpu)):   # the device path needs a real stream

@@ -39,13 +39,13 @@ def _port() -> int:
     return p
 
 
-def _run_ranks(worker: str, out_dir, arg: str, timeout: int = 150):
+def _run_ranks(worker: str, out_dir, *args: str, timeout: int = 150):
     """Both ranks as child processes (never exec'd from this GPU-initialised process)."""
     port = _port()
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_dist_workers.py"), worker, str(r),
-                               str(WORLD), str(port), str(out_dir), arg],
+                               str(WORLD), str(port), str(out_dir), *args],
                               cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(WORLD)]
     outs = []
@@ -62,9 +62,9 @@ def _run_ranks(worker: str, out_dir, arg: str, timeout: int = 150):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["host", "device"])
-def test_route_batch_two_hip_ranks(gpu, oracle_lib, tmp_path, path):
-    _run_ranks("tb_route_worker_hip", tmp_path, path)
+@pytest.mark.parametrize("path,map_kind", [("host", "hash"), ("device", "hash"), ("device", "balanced")])
+def test_route_batch_two_hip_ranks(gpu, oracle_lib, tmp_path, path, map_kind):
+    _run_ranks("tb_route_worker_hip", tmp_path, path, map_kind)
     G.check_tb_route([np.load(tmp_path / f"tb_{r}.npz") for r in range(WORLD)])
 
 

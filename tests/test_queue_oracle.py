@@ -145,3 +145,56 @@ def test_c_queue_multithreaded_matches_serial(oracle_lib, order):
         assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
     for key in range(0, n_keys, 97):
         assert a.queue_of(key) == b.queue_of(key)
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+def test_c_cancel_matches_python(oracle_lib, order):
+    """tbrq_cancel (the C restatement the large sharded GPU tests use as their reference)
+    against QueueingTokenBucketTable.cancel: queued, finished, unknown and repeated ids,
+    between wait batches and ticks; queues and drain logs stay identical."""
+    n_keys, qlimit = 40, 6
+    cfg = TokenBucketConfig.from_options(5, 2, 10_000_000)
+    py = QueueingTokenBucketTable(cfg, qlimit, order)
+    c = cref.CQueueingTokenBucket(n_keys, cfg.token_limit, cfg.fill_rate, qlimit, order)
+    rng = np.random.default_rng(5 + order)
+    rid = 0
+    for keys, permits, ts, t_refresh in random_ops(11 + order, n_keys, 6, 1500):
+        for i, (k, p, s) in enumerate(zip(keys, permits, ts)):
+            py.acquire(int(k), int(p), int(s), rid + i)
+        c.acquire_batch(keys, permits, ts, rid)
+        pick = rng.integers(0, len(keys), 300)
+        ck, cid = keys[pick], rid + pick.astype(np.int64)
+        cid[::7] = -5                                       # unknown ids
+        want = [int(py.cancel(int(k), int(i))) for k, i in zip(ck, cid)]
+        assert c.cancel(ck, cid).tolist() == want
+        assert sum(want) > 0
+        rid += len(keys)
+        lk, lid, lrem = c.refresh(t_refresh)
+        assert list(zip(lk.tolist(), lid.tolist(), lrem.tolist())) == py.refresh(t_refresh)
+    for k in range(n_keys):
+        assert c.queue_of(k) == py.queue_of(k)
+
+
+@pytest.mark.parametrize("order", [OLDEST_FIRST, NEWEST_FIRST])
+def test_c_approx_cancel_matches_python(oracle_lib, order):
+    """tba_cancel against ApproxClient.cancel, zero-permit entries included."""
+    from oracle.semantics import ApproxClient
+    n_keys, qlimit = 30, 5
+    py = ApproxClient(6, 3, 10_000_000, qlimit, order, zero_slots=2)
+    c = cref.CApprox(n_keys, 6, 3, 10_000_000, qlimit, order, zero_slots=2)
+    rng = np.random.default_rng(17 + order)
+    rid = 0
+    for _ in range(4):
+        keys = rng.integers(0, n_keys, 800).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 2, 3], 800).astype(np.int32)
+        for i, (k, p) in enumerate(zip(keys.tolist(), permits.tolist())):
+            py.wait(k, p, rid + i)
+        c.acquire_batch(keys, permits, wait=True, id_base=rid)
+        pick = rng.integers(0, 800, 200)
+        want = [int(py.cancel(int(keys[j]), rid + int(j))) for j in pick]
+        assert c.cancel(keys[pick], rid + pick.astype(np.int64)).tolist() == want
+        assert sum(want) > 0
+        rid += 800
+        for k in range(n_keys):
+            s = py.st(k)
+            assert c.queue_of(k) == [(e.request_id, e.permits) for e in s.queue]
