@@ -604,6 +604,85 @@ __device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restri
     ts = ((rec >> (F.kb + F.pb)) & 1) ? ts_orig[pay] : (int64_t)((uint64_t)tbase + pay);
 }
 
+// Fold records (token-bucket kind, packed, >= 2 partition passes).  The last pass writes,
+// instead of a PackFmt record and its permutation, what the fold and the hot runs need:
+//
+//   bits [0, rb)              row within the bucket (the key field's low r_bits)
+//   bits [rb, rb+pb)          permit code (as PackFmt)
+//   bit  rb+pb                escape
+//   bits [rb+pb+1, +pw)       the request's position in the last pass's INPUT (the previous
+//                             pass's output): its reply goes there, so the last pass needs
+//                             no permutation and no un-partition pass of its own
+//   bits [rb+pb+1+pw, 64)     ts - base1 (tw bits, base1 = ts[0] - 2^(tw-1)); with the
+//                             escape bit: unused, and the fold takes the request's time from
+//                             the previous pass's record at that position
+//
+// pw = ceil_log2(batch), tw = 64 - rb - pb - 1 - pw (config B: 22 bits, +-2.1 s around the
+// batch's first request; the batch spans 10 ms).  Used when tw >= 8.
+struct FoldFmt {
+    int32_t on;
+    int32_t rb, pb, pw, tw;
+    uint32_t nb;            // ordinary buckets
+    uint32_t region_bits;   // 8 * (passes - 1): buckets with equal low region_bits share a reply region
+    uint32_t n_hi;          // ceil(nb / 2^region_bits)
+};
+__device__ __forceinline__ int64_t fold_base(const int64_t *__restrict__ ts, const FoldFmt &G) {
+    return ts[0] - ((int64_t)1 << (G.tw - 1));
+}
+__device__ __forceinline__ uint64_t fold_rec(uint64_t rec0, uint32_t pos, int64_t tbase0, int64_t tbase1,
+                                             const PackFmt &F, const FoldFmt &G) {
+    const uint64_t row = rec0 & ((1ull << G.rb) - 1);
+    const uint64_t pc = (rec0 >> F.kb) & ((1ull << F.pb) - 1);
+    const bool esc0 = (rec0 >> (F.kb + F.pb)) & 1;
+    const int64_t ts = (int64_t)((uint64_t)tbase0 + (rec0 >> (F.kb + F.pb + 1)));
+    const uint64_t d = (uint64_t)ts - (uint64_t)tbase1;
+    const bool fits = !esc0 && ts >= tbase1 && (d >> G.tw) == 0;
+    return row | (pc << G.rb) | ((uint64_t)!fits << (G.rb + G.pb)) | ((uint64_t)pos << (G.rb + G.pb + 1)) |
+           ((fits ? d : 0ull) << (G.rb + G.pb + 1 + G.pw));
+}
+// Decode a fold record: row, permit code, time (escaped: through the previous pass's
+// record `rec0[pos]`, itself possibly escaped to the caller's ts array) and reply position.
+__device__ __forceinline__ void unfold_rec(uint64_t rec, const FoldFmt &G, int64_t tbase1,
+                                           const uint64_t *__restrict__ rec0, const int64_t *__restrict__ ts_orig,
+                                           int64_t tbase0, const PackFmt &F, uint32_t &row, int32_t &p,
+                                           int64_t &ts, uint32_t &pos) {
+    row = (uint32_t)(rec & ((1ull << G.rb) - 1));
+    p = (int32_t)((rec >> G.rb) & ((1ull << G.pb) - 1));
+    pos = (uint32_t)((rec >> (G.rb + G.pb + 1)) & ((1ull << G.pw) - 1));
+    if ((rec >> (G.rb + G.pb)) & 1) {
+        uint32_t k;
+        int32_t p0;
+        unpack_rec(rec0[pos], ts_orig, tbase0, F, k, p0, ts);
+    } else {
+        ts = (int64_t)((uint64_t)tbase1 + (rec >> (G.rb + G.pb + 1 + G.pw)));
+    }
+}
+// The fold's bucket for this workgroup.  With fold records the replies of all buckets
+// that share their low region_bits land in one region of the previous pass's output (256
+// KB of one-byte replies at config B); the buckets of a region are dealt to one XCD
+// (workgroups b and b + 8 share one) and run there together, so that XCD's L2 merges their
+// scattered one-byte reply stores into whole lines.  Workgroups past the last bucket exit.
+__device__ __forceinline__ uint32_t fold_bucket(const FoldFmt &G) {
+    if (!G.on) return blockIdx.x;
+    const uint32_t x = blockIdx.x & 7u, s = blockIdx.x >> 3;
+    const uint32_t j = s / G.n_hi, hi = s - j * G.n_hi;
+    return (hi << G.region_bits) | (x + 8u * j);
+}
+// Any record of the fold's input: (row, permit code, time, reply position).
+__device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldFmt &G, int64_t tbase1,
+                                           const uint64_t *__restrict__ rec0, const int64_t *__restrict__ ts_orig,
+                                           int64_t tbase0, const PackFmt &F, uint32_t rmask, uint32_t &row,
+                                           int32_t &p, int64_t &ts, uint32_t &pos) {
+    if (G.on) {
+        unfold_rec(rec, G, tbase1, rec0, ts_orig, tbase0, F, row, p, ts, pos);
+    } else {
+        uint32_t k;
+        unpack_rec(rec, ts_orig, tbase0, F, k, p, ts);
+        row = k & rmask;
+        pos = q;
+    }
+}
+
 // Stable partition pass over packed records (see k_scatter; one 8-byte LDS staging
 // round instead of two).  FIRST: read the caller's arrays, validate permits and
 // timestamps, and pack; otherwise read the previous pass's records.
@@ -613,7 +692,10 @@ __device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restri
 // 4-byte staging round); pass 0 generates it.
 // NOTS (approximate kind, FIRST): no timestamps -- every record takes the escape form,
 // so its payload field carries the arrival index.
-template <bool FIRST, bool HOT = false, bool IDX = false, bool NOTS = false>
+// LAST (token-bucket kind, the last of >= 2 passes): write fold records (FoldFmt) -- each
+// element's position in this pass's input rides along -- and no permutation; `tin` is
+// then the caller's timestamps (for the record bases).
+template <bool FIRST, bool HOT = false, bool IDX = false, bool NOTS = false, bool LAST = false>
 __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
@@ -621,10 +703,12 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
     uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
     uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
-    uint32_t *__restrict__ iout = nullptr) {
+    uint32_t *__restrict__ iout = nullptr, FoldFmt G = FoldFmt{}) {
+    static_assert(!(FIRST && LAST), "fold records come from a pass after the first");
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
+    __shared__ uint16_t stage_e[LAST ? kTile : 1];   // LAST: each staged record's input element
     __shared__ uint64_t hs[HOT ? kHotLds : 1];
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
@@ -683,10 +767,18 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
         if (e < nvalid) {
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
             stage[lpos[it]] = rec[it];
-            ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
+            if (LAST)
+                stage_e[lpos[it]] = (uint16_t)e;
+            else
+                ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
         }
     }
     __syncthreads();
+    int64_t tbase0 = 0, tbase1 = 0;
+    if (LAST) {
+        tbase0 = pack_base(tin, F);
+        tbase1 = fold_base(tin, G);
+    }
     uint32_t gpos[kPartItems];
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
@@ -695,7 +787,8 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
             const uint64_t s = stage[j];
             const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
-            rout[gpos[it]] = s;   // runs merge in L2: keep cached
+            // runs merge in L2: keep cached
+            rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
         }
     }
     if (IDX) {
@@ -863,18 +956,19 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow, uint32_t wide_min) {
+    uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
     // A pending entry is 16 bytes (row | local id << 16, permits, timestamp); its request
     // times are recomputed per round rather than stored, so 512 entries fit in 8 KB.
-    __shared__ uint64_t aux[kWideTail * 2];
+    __shared__ uint64_t aux[kWideTail * 2 + kWideTail / 2];
     __shared__ uint32_t wsum[kWideBlock / 64];
     uint32_t *hcnt = reinterpret_cast<uint32_t *>(aux);
     uint32_t *t_kl_lid = reinterpret_cast<uint32_t *>(aux);
     int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kWideTail;
     int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kWideTail;
+    uint32_t *t_pos = reinterpret_cast<uint32_t *>(aux + kWideTail * 2);   // reply positions
     static_assert(kWideTail * 2 * 8 >= kMaxRows * 4, "hcnt fits in aux");
 #if TBE_WIDE_FT
     __shared__ double ft[kMaxRows];
@@ -889,7 +983,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 
     if (*err) return;
     const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = fold_bucket(G);
+    if (G.on && b >= G.nb) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     if (s == e) return;
     const uint32_t R = 1u << r_bits;
@@ -902,12 +997,14 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     if (e - s < wide_min) return;
     const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
 
     uint32_t kl[kWidePer];
     int32_t pm[kWidePer];
     int64_t tsv[kWidePer];
+    uint32_t pos[kWidePer];   // where each request's reply goes (FoldFmt), or its sorted position
     uint32_t pend = 0;
     auto load_chunk = [&](uint32_t c) {
         pend = 0;
@@ -917,11 +1014,11 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             kl[r] = 0;
             pm[r] = 0;
             tsv[r] = 0;
+            pos[r] = q;
             if (q < e) {
                 if (PACKED) {
-                    uint32_t k;
-                    unpack_rec(LD_F(srec + q), ts_orig, tbase, F, k, pm[r], tsv[r]);
-                    kl[r] = k & rmask;
+                    fold_input(LD_F(srec + q), q, G, tbase1, rec0, ts_orig, tbase, F, rmask, kl[r], pm[r],
+                               tsv[r], pos[r]);
                 } else {
                     kl[r] = skeys[q] & rmask;
                     pm[r] = sperm[q];
@@ -956,7 +1053,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         if (c != s) load_chunk(c);
 #pragma unroll
         for (int r = 0; r < kWidePer; ++r)
-            if (pend & (1u << r)) put_reply(res, c + r * kWideBlock + tid, kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
+            if (pend & (1u << r)) put_reply(res, pos[r], kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
     }
     for (uint32_t j = tid; j < nrows; j += kWideBlock) ST_S(rows + j, row[j]);
     return;
@@ -1076,6 +1173,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     t_kl_lid[at] = kl[r] | ((uint32_t)(r * kWideBlock + tid) << 16);
                     t_pm[at] = pm[r];
                     t_ts[at] = tsv[r];
+                    t_pos[at] = pos[r];
                     ++at;
                 }
             }
@@ -1142,7 +1240,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                             bool m;
                             const uint32_t rp = tb_step_ft(st, WIDE_FT_GET(rw, st), t_pm[en], rq1, P, m);
                             mod |= m;
-                            put_reply(res, c + (t_kl_lid[en] >> 16), rp, narrow);
+                            put_reply(res, t_pos[en], rp, narrow);
                         }
                         if (mod) {
                             row[rw] = st;
@@ -1157,7 +1255,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 n_tail = 0;    // block-uniform: skip the rounds below
             }
 #endif
-            uint32_t tkl = 0, tlid = 0, trep = 0;
+            uint32_t tkl = 0, tlid = 0, trep = 0, tpos = 0;
             int32_t tpm = 0;
             int64_t tts = 0;
             ReqTime trq{0.0, 0, 0};
@@ -1166,6 +1264,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 tlid = t_kl_lid[at] >> 16;
                 tpm = t_pm[at];
                 tts = t_ts[at];
+                tpos = t_pos[at];
                 trq = PACKED ? req_time_rel(tts, TB, P.ttl_ms) : req_time(tts, P.ttl_ms);
             };
             if (tp) take(tid);
@@ -1194,7 +1293,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                         atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
                         tp = false;
                     }
-                    if (!tp) put_reply(res, c + tlid, trep, narrow);
+                    if (!tp) put_reply(res, tpos, trep, narrow);
                 }
                 const uint64_t bal = __ballot(tp);
                 if ((tid & 63) == 0) wsum[tid >> 6] = (uint32_t)__popcll(bal);
@@ -1213,6 +1312,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                         t_kl_lid[at] = tkl | (tlid << 16);
                         t_pm[at] = tpm;
                         t_ts[at] = tts;
+                        t_pos[at] = tpos;
                     }
                     __syncthreads();
                     tp = (uint32_t)tid < left;
@@ -1265,7 +1365,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 #pragma unroll
         for (int r = 0; r < kWidePer; ++r) {
             const uint32_t q = c + r * kWideBlock + tid;
-            if (q < e && (keep & (1u << r))) put_reply(res, q, rep[r], narrow);
+            if (q < e && (keep & (1u << r))) put_reply(res, pos[r], rep[r], narrow);
         }
     }
     __syncthreads();
@@ -1312,7 +1412,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow, uint32_t wide_min) {
+    uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -1322,7 +1422,8 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     uint32_t *t_kl_lid = aux;
     int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kTbTail;
     int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kTbTail;
-    static_assert(kTbTail * 16 <= kMaxRows * 4, "tail list fits in aux");
+    uint32_t *t_pos = aux + 4 * kTbTail;                       // reply positions
+    static_assert(kTbTail * 20 <= kMaxRows * 4, "tail list fits in aux");
     static_assert(kTbChunk <= 4096, "election tags hold 12-bit local ids");
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t loaded[kMaxRows / 32];
@@ -1330,7 +1431,8 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
 
     if (*err) return;
     const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = fold_bucket(G);
+    if (G.on && b >= G.nb) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     if (s == e) return;
     const uint32_t R = 1u << r_bits;
@@ -1342,6 +1444,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     // Whole slice (dense) or touched rows only (sparse), decided below.
     bool dense = false;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     // one time base for request times and row field times: kRowWindow below the packed
     // base, so rows granted up to ~35 minutes before the batch also take the fast path
     const TimeBase TB = time_base(PACKED ? tbase - kRowWindow : -1, P.ttl_ms);
@@ -1350,6 +1453,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     uint32_t kl[kTbPer];
     int32_t pm[kTbPer];
     int64_t tsv[kTbPer];
+    uint32_t pos[kTbPer];   // where each request's reply goes (FoldFmt), or its sorted position
     uint32_t pend = 0;
     auto load_chunk = [&](uint32_t c) {
         pend = 0;
@@ -1359,11 +1463,11 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
             kl[r] = 0;
             pm[r] = 0;
             tsv[r] = 0;
+            pos[r] = q;
             if (q < e) {
                 if (PACKED) {
-                    uint32_t k;
-                    unpack_rec(LD_F(srec + q), ts_orig, tbase, F, k, pm[r], tsv[r]);
-                    kl[r] = k & rmask;
+                    fold_input(LD_F(srec + q), q, G, tbase1, rec0, ts_orig, tbase, F, rmask, kl[r], pm[r],
+                               tsv[r], pos[r]);
                 } else {
                     kl[r] = skeys[q] & rmask;
                     pm[r] = sperm[q];
@@ -1507,6 +1611,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
                     t_kl_lid[at] = kl[r] | ((uint32_t)(r * kTbBlock + tid) << 16);
                     t_pm[at] = pm[r];
                     t_ts[at] = tsv[r];
+                    t_pos[at] = pos[r];
                     ++at;
                 }
             }
@@ -1557,7 +1662,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
                         atomicOr(&dirty[tkl[i] >> 5], 1u << (tkl[i] & 31));
                         tp[i] = false;
                     }
-                    if (!tp[i]) put_reply(res, c + tlid[i], trep[i], narrow);
+                    if (!tp[i]) put_reply(res, t_pos[tid + i * kTbBlock], trep[i], narrow);
                     any |= tp[i];
                 }
                 if (!__syncthreads_or(any)) break;
@@ -1574,7 +1679,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
 #pragma unroll
         for (int r = 0; r < kTbPer; ++r) {
             const uint32_t q = c + r * kTbBlock + tid;
-            if (q < e && (keep & (1u << r))) put_reply(res, q, rep[r], narrow);
+            if (q < e && (keep & (1u << r))) put_reply(res, pos[r], rep[r], narrow);
         }
     }
     __syncthreads();
@@ -1753,13 +1858,14 @@ __device__ __forceinline__ uint32_t seg_run(const uint32_t *__restrict__ segbase
 __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
-    SegSummary *__restrict__ summ, const uint32_t *__restrict__ err) {
+    SegSummary *__restrict__ summ, const uint32_t *__restrict__ err, FoldFmt G, const uint64_t *__restrict__ rec0) {
     __shared__ int64_t wts[kSegBlock / 64];
     __shared__ int32_t wp[kSegBlock / 64];
     if (*err) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const uint32_t h = seg_run(segbase, j);
         const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
@@ -1776,10 +1882,10 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
         for (int it = 0; it < kSegItems; ++it) {
             const uint32_t q = a + it * kSegBlock + tid;
             if (q >= b) continue;
-            uint32_t k;
+            uint32_t k, pos;
             int32_t p;
             int64_t ts;
-            unpack_rec(rv[it], ts_orig, tbase, F, k, p, ts);
+            fold_input(rv[it], q, G, tbase1, rec0, ts_orig, tbase, F, 0u, k, p, ts, pos);
             mx = max(mx, ts);
             mn = min(mn, p);
         }
@@ -1810,7 +1916,8 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     const uint32_t *__restrict__ bstart, uint32_t nb, const HotSet *__restrict__ hot,
     HotSet *__restrict__ hot_next, const uint32_t *__restrict__ segbase,
     const SegSummary *__restrict__ summ, SegState *__restrict__ sst, Slot *__restrict__ table,
-    TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow) {
+    TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow, FoldFmt G,
+    const uint64_t *__restrict__ rec0) {
     __shared__ Slot S;
     __shared__ double ftS;
     __shared__ uint32_t first, own;
@@ -1823,6 +1930,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     if (s0 == e0) return;
     const uint32_t j0 = segbase[h], nseg = segbase[h + 1] - j0;
     const int64_t tbase = pack_base(ts_orig, F);
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);
     if (tid == 0) {
         S = table[key];
@@ -1860,16 +1968,17 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
         for (uint32_t c = a; c < b; c += kFoldChunk) {
             int32_t pm[kFoldPer];
             ReqTime rq[kFoldPer];
-            uint32_t rep[kFoldPer], pend = 0;
+            uint32_t rep[kFoldPer], pos[kFoldPer], pend = 0;
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
                 const uint32_t q = c + r * kSegBlock + tid;
                 int64_t ts = 0;
                 pm[r] = 0;
                 rep[r] = 0;
+                pos[r] = q;
                 if (q < b) {
                     uint32_t k;
-                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts);
+                    fold_input(srec[q], q, G, tbase1, rec0, ts_orig, tbase, F, 0u, k, pm[r], ts, pos[r]);
                     pend |= 1u << r;
                 }
                 rq[r] = req_time_rel(ts, TB, P.ttl_ms);
@@ -1908,7 +2017,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
 #pragma unroll
             for (int r = 0; r < kFoldPer; ++r) {
                 const uint32_t q = c + r * kSegBlock + tid;
-                if (q < b) put_reply(res, q, rep[r], narrow);
+                if (q < b) put_reply(res, pos[r], rep[r], narrow);
             }
         }
         __syncthreads();
@@ -1928,11 +2037,12 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
     const SegState *__restrict__ sst, TbParams P, uint32_t *__restrict__ res,
-    const uint32_t *__restrict__ err, uint32_t narrow) {
+    const uint32_t *__restrict__ err, uint32_t narrow, FoldFmt G, const uint64_t *__restrict__ rec0) {
     if (*err) return;
     const int tid = threadIdx.x;
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const SegState st = sst[j];
@@ -1950,13 +2060,13 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
         for (int it = 0; it < kSegItems; ++it) {
             const uint32_t q = a + it * kSegBlock + tid;
             if (q >= b) continue;
-            uint32_t k;
+            uint32_t k, pos;
             int32_t p;
             int64_t ts;
-            unpack_rec(rv[it], ts_orig, tbase, F, k, p, ts);
+            fold_input(rv[it], q, G, tbase1, rec0, ts_orig, tbase, F, 0u, k, p, ts, pos);
             Slot c = st.s;
             bool m;
-            put_reply(res, q, tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m), narrow);
+            put_reply(res, pos, tb_step_ft(c, st.ft, p, req_time_rel(ts, TB, P.ttl_ms), P, m), narrow);
         }
     }
 }
@@ -3157,6 +3267,10 @@ struct tbe_engine {
     // reply width code of the wait kinds' folds (put_wait): 1, 2 or 4 (as 0) bytes
     uint32_t wait_rw() const { return narrow ? 1u : (medium ? 2u : 0u); }
     PackFmt pf{};
+    // fold records (FoldFmt): the last of >= 2 passes writes them, the fold and the hot runs
+    // put each reply straight into the previous pass's order, and that pass's un-partition
+    // and permutation disappear (token bucket, packed; TBE_FLAG_UNSCATTER_ALL turns it off)
+    bool foldrec = false;
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
     // batch b+1 is partitioned by was complete before batch b's fold began.
@@ -3433,6 +3547,25 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
+    // fold records for this batch: the reply position takes ceil_log2(n) bits, the time
+    // offset what is left (>= 8 bits, else the plain records)
+    FoldFmt G{};
+    if (e->foldrec && !approx && !wait) {
+        const int pw = std::max(1, ceil_log2(n));
+        const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
+        if (tw >= 8) {
+            G.on = 1;
+            G.rb = e->r_bits;
+            G.pb = e->pf.pb;
+            G.pw = pw;
+            G.tw = tw;
+            G.nb = e->nbuckets;
+            G.region_bits = (uint32_t)(kDigitBits * (e->passes - 1));
+            G.n_hi = (uint32_t)(((uint64_t)e->nbuckets + (1ull << G.region_bits) - 1) >> G.region_bits);
+        }
+    }
+    const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
+    const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
     HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
@@ -3494,6 +3627,11 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, out.perm, w.err);
+        else if (e->packed && G.on && p == e->passes - 1)
+            k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0, nullptr,
+                nullptr, G);
         else if (e->packed)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3573,22 +3711,22 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     } else if (e->packed) {
         // dense buckets in k_fold_wide, the others in k_fold (each skips the other's)
         const uint32_t wmin = fold_wide_min(e, n);
-        k_fold_wide<true><<<e->nbuckets, kWideBlock, 0, sf>>>(
+        k_fold_wide<true><<<fold_grid, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin);
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
         if (wmin > 1u)   // else k_fold_wide takes every bucket
-            k_fold<true><<<e->nbuckets, kTbBlock, 0, sf>>>(
+            k_fold<true><<<fold_grid, kTbBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin);
+                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
     } else {
         const uint32_t wmin = fold_wide_min(e, n);
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin);
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin, G, rec0);
         if (wmin > 1u)
             k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart,
-                e->r_bits, e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin);
+                e->r_bits, e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin, G, rec0);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {
@@ -3598,12 +3736,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
         k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
         k_hot_summary<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                   w.segbase, w.summ, w.err);
+                                                   w.segbase, w.summ, w.err, G, rec0);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
                                                       hot_next, w.segbase, w.summ, w.sst, e->table,
-                                                      e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
+                                                      e->params, w.res[0], w.err, e->narrow ? 1u : 0u, G, rec0);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                   w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u);
+                                                   w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u,
+                                                   G, rec0);
         if (pipe) {
             // The next-but-one batch's hot set, on a stream of its own beside this batch's
             // un-partition; batch b+2 (same workspace) waits for it before its partition.
@@ -3620,7 +3759,8 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     stage_begin(e, ST_UNSCATTER, sf);
     const unsigned untiles = (unsigned)((n + kUnTile - 1) / kUnTile);
     int cur = 0;
-    for (int p = e->passes - 1; p >= 1; --p) {
+    // with fold records the replies are already in pass passes-2's output order
+    for (int p = e->passes - (G.on ? 2 : 1); p >= 1; --p) {
         if (e->narrow && !approx)
             k_unscatter<false, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[p].perm, w.res[cur],
                                                                    w.res[cur ^ 1], nullptr, nullptr);
@@ -3768,6 +3908,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
+        e->foldrec = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && e->passes >= 2 &&
+                     (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
@@ -4802,7 +4944,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *passes = (uint32_t)e->passes;
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
-              (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u);
+              (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u);
     return TBE_OK;
 }
 

@@ -90,6 +90,12 @@ typedef struct tbe_config {
                                              1-byte (TokenLimit <= 62) and 2-byte (<= 16382)
                                              replies; approximate kind 2-byte replies
                                              (TokenLimit <= 16382) */
+#define TBE_FLAG_UNSCATTER_ALL 0x20u      /* token bucket (A/B checks): the last partition pass
+                                             writes plain records and its permutation, and its
+                                             own un-partition pass runs.  By default (>= 2
+                                             passes, packed records) it writes fold records that
+                                             carry each request's position in its input, and the
+                                             fold puts every reply straight there */
 
 typedef struct tbe_engine tbe_engine;
 
@@ -328,7 +334,10 @@ tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t 
  * bucket kind) rather than the wide {key, permits, ts} records, bit 1 set
  * when hot keys get runs of their own (TBE_FLAG_NO_HOT clears it), bit 2 set when
  * consecutive device batches overlap (TBE_FLAG_NO_PIPELINE clears it), bit 3 set when
- * replies travel as one byte (TBE_FLAG_NO_NARROW clears it). */
+ * replies travel as one byte (TBE_FLAG_NO_NARROW clears it), bit 4 set when the queueing
+ * or approximate kind's replies travel as two bytes, bit 5 set when the last partition
+ * pass writes fold records (TBE_FLAG_UNSCATTER_ALL clears it; used by batches whose
+ * reply position and time offset fit). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* Per-stage device time (ms) accumulated since the last call, when
