@@ -217,7 +217,8 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
                                                   uint64_t kmask, const HotSet *__restrict__ hot = nullptr,
                                                   uint32_t nb = 0, int r_bits = 0,
                                                   uint32_t *__restrict__ bcount = nullptr,
-                                                  int lowbits = 0, uint32_t nbt = 0) {
+                                                  int lowbits = 0, uint32_t nbt = 0,
+                                                  uint8_t *__restrict__ dig_out = nullptr) {
     __shared__ uint32_t h8[kDigits * 8];
     __shared__ uint32_t tile_lo[2];
     static_assert(kHBlock == 2 * kDigits && kDigits * 8 == 4 * kHBlock, "two threads per digit; 4 counters each");
@@ -284,6 +285,7 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
                 // hit different words instead of serialising on one
                 if (valid) atomicAdd(&h8[d * 8 + (tid & 7)], 1u);
             }
+            if (dig_out && valid) dig_out[i] = (uint8_t)d;   // pass 0: k_unrank re-ranks from it
             if (valid) {
                 bad |= validate && ((uint64_t)kv[it] >= n_keys);
                 if (bcount && (i == base || i == last)) {
@@ -769,7 +771,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
             stage[lpos[it]] = rec[it];
             if (LAST)
                 stage_e[lpos[it]] = (uint16_t)e;
-            else
+            else if (perm)   // (null: k_unrank recomputes the positions)
                 ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
         }
     }
@@ -1785,6 +1787,57 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
             ST_U(reinterpret_cast<uint16_t *>(res_out) + i, (uint16_t)r[it]);
         } else {
             ST_U(res_out + i, r[it]);
+        }
+    }
+}
+
+// Final un-partition of the token-bucket kind without a stored permutation.  Pass 0 put
+// request i of tile t at goff_t[d] + (its stable rank among the tile's digit-d requests),
+// d = its pass-0 digit.  That position is recomputed here per partition tile -- the same
+// tile, the same wave-blocked ranking (rank_tile_wb) of the same digits, which k_hist's
+// first pass stored as one byte per request, and the same tile offsets -- so pass 0 writes
+// no 4-byte permutation and this pass reads one byte per request instead of four:
+// granted[i], remaining[i] = reply at that position.  W: reply width (1 or 4 bytes).
+template <int W>
+__global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t *__restrict__ digit,
+                                                       const uint32_t *__restrict__ tileprefix,
+                                                       const uint32_t *__restrict__ blockprefix,
+                                                       const uint32_t *__restrict__ digit_total,
+                                                       uint32_t tiles_per_blk, const uint32_t *__restrict__ res_in,
+                                                       uint8_t *__restrict__ granted,
+                                                       int32_t *__restrict__ remaining) {
+    __shared__ RankLds<kPartBlock> L;
+    __shared__ uint32_t goff[kDigits];
+    __shared__ uint32_t wcnt[(kPartBlock / 64) * kDigits];
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kTile;
+    const int nvalid = (int)min<uint64_t>(kTile, n - base);
+    uint32_t dg[kPartItems], lpos[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = wb_elem<kPartBlock, kPartItems>(it);
+        dg[it] = e < nvalid ? (uint32_t)LD_U(digit + base + e) : 0u;
+    }
+    tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
+    rank_tile_wb<kPartBlock, kPartItems>(dg, 0, nvalid, L, wcnt, lpos);
+    uint32_t r[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = wb_elem<kPartBlock, kPartItems>(it);
+        const uint32_t q = goff[dg[it]] + lpos[it] - L.lstart[dg[it]];
+        r[it] = e < nvalid ? (W == 1 ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[q] : res_in[q]) : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int e = wb_elem<kPartBlock, kPartItems>(it);
+        if (e >= nvalid) continue;
+        const uint64_t i = base + e;
+        if (W == 1) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 7));
+            ST_U(remaining + i, (int32_t)(r[it] & 0x7Fu));
+        } else {
+            ST_U(granted + i, (uint8_t)(r[it] >> 31));
+            ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
         }
     }
 }
@@ -3233,6 +3286,7 @@ struct Workspace {
     uint32_t *res[2] = {nullptr, nullptr};
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
+    uint8_t *dig0 = nullptr;      // each request's pass-0 digit (k_unrank re-ranks from it)
     uint32_t *err = nullptr;      // the batch's invalid-request flag
     hipEvent_t hot_done = nullptr;   // pipelined: k_hot_update of the last batch on this workspace
     bool hot_pending = false;
@@ -3271,6 +3325,9 @@ struct tbe_engine {
     // put each reply straight into the previous pass's order, and that pass's un-partition
     // and permutation disappear (token bucket, packed; TBE_FLAG_UNSCATTER_ALL turns it off)
     bool foldrec = false;
+    // k_unrank: the final un-partition recomputes pass 0's positions from one-byte digits,
+    // so pass 0 writes no permutation (token bucket, packed; TBE_FLAG_UNSCATTER_ALL: off)
+    bool unrank = false;
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
     // batch b+1 is partitioned by was complete before batch b's fold began.
@@ -3393,6 +3450,7 @@ void free_workspace(Workspace &w) {
     dfree(w.res[1]);
     dfree(w.bstart);
     dfree(w.bcount);
+    dfree(w.dig0);
     dfree(w.err);
     w.cap_n = 0;
     w.used = false;
@@ -3446,6 +3504,7 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.res[1], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bcount, (uint64_t)e->nb_total * sizeof(uint32_t)));
+    if (e->unrank) HIP_TRY(e, hipMalloc(&w.dig0, cap));
     HIP_TRY(e, hipMalloc(&w.err, sizeof(uint32_t)));
     w.cap_n = cap;
     return TBE_OK;
@@ -3565,6 +3624,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         }
     }
     const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
+    const bool unrank = e->unrank && !approx && !wait;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
@@ -3577,16 +3637,17 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         // the last pass also counts requests per bucket (k_bscan turns them into bstart)
         uint32_t *bc = (p == e->passes - 1) ? w.bcount : nullptr;
         const int lowbits = kDigitBits * p;
+        uint8_t *dig = (p == 0 && unrank) ? w.dig0 : nullptr;
         if (p == 0 && hot)
             k_hist<uint64_t, true><<<nblk, kHBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                              w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                              hot, e->nbuckets, e->r_bits, bc, lowbits,
-                                                             e->nb_total);
+                                                             e->nb_total, dig);
         else if (p == 0)
             k_hist<uint64_t><<<nblk, kHBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
-                                                       e->nb_total);
+                                                       e->nb_total, dig);
         else if (e->packed)
             k_hist<uint64_t><<<nblk, kHBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
                                                        out.tileprefix, w.blocksum, e->cfg.n_keys,
@@ -3622,11 +3683,11 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err, hot, e->nbuckets, e->r_bits);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, hot, e->nbuckets, e->r_bits);
         else if (e->packed && p == 0)
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err);
         else if (e->packed && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3772,7 +3833,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                                     w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
-    if (e->narrow && !wait && !approx)
+    if (unrank && e->narrow)
+        k_unrank<1><<<ntiles, kPartBlock, 0, sf>>>(n, w.dig0, w.pass[0].tileprefix, w.pass[0].blockprefix,
+                                                   w.pass[0].digit_total, tpb, w.res[cur], granted, remaining);
+    else if (unrank)
+        k_unrank<4><<<ntiles, kPartBlock, 0, sf>>>(n, w.dig0, w.pass[0].tileprefix, w.pass[0].blockprefix,
+                                                   w.pass[0].digit_total, tpb, w.res[cur], granted, remaining);
+    else if (e->narrow && !wait && !approx)
         k_unscatter<true, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                   nullptr, granted, remaining);
     else if (wait && e->narrow)
@@ -3910,6 +3977,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->nb_total = e->nbuckets + hot_cap;
         e->foldrec = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && e->passes >= 2 &&
                      (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->unrank = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
