@@ -1798,7 +1798,7 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
 // first pass stored as one byte per request, and the same tile offsets -- so pass 0 writes
 // no 4-byte permutation and this pass reads one byte per request instead of four:
 // granted[i], remaining[i] = reply at that position.  W: reply width (1 or 4 bytes).
-template <int W>
+template <int W, bool WAIT = false>
 __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t *__restrict__ digit,
                                                        const uint32_t *__restrict__ tileprefix,
                                                        const uint32_t *__restrict__ blockprefix,
@@ -1825,14 +1825,29 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
     for (int it = 0; it < kPartItems; ++it) {
         const int e = wb_elem<kPartBlock, kPartItems>(it);
         const uint32_t q = goff[dg[it]] + lpos[it] - L.lstart[dg[it]];
-        r[it] = e < nvalid ? (W == 1 ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[q] : res_in[q]) : 0u;
+        r[it] = e < nvalid ? (W == 1   ? (uint32_t)reinterpret_cast<const uint8_t *>(res_in)[q]
+                              : W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(res_in)[q]
+                                       : res_in[q])
+                           : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int e = wb_elem<kPartBlock, kPartItems>(it);
         if (e >= nvalid) continue;
         const uint64_t i = base + e;
-        if (W == 1) {
+        if (WAIT && W == 1) {            // status, remaining (put_wait forms)
+            ST_U(granted + i, (uint8_t)(r[it] >> 6));
+            const uint32_t rem = r[it] & 63u;
+            ST_U(remaining + i, (rem == kRemNone8) ? -1 : (int32_t)rem);
+        } else if (WAIT && W == 2) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 14));
+            const uint32_t rem = r[it] & kRemNone16;
+            ST_U(remaining + i, (rem == kRemNone16) ? -1 : (int32_t)rem);
+        } else if (WAIT) {
+            ST_U(granted + i, (uint8_t)(r[it] >> 30));
+            const uint32_t rem = r[it] & kRemNone;
+            ST_U(remaining + i, (rem == kRemNone) ? -1 : (int32_t)rem);
+        } else if (W == 1) {             // granted, remaining (put_reply forms)
             ST_U(granted + i, (uint8_t)(r[it] >> 7));
             ST_U(remaining + i, (int32_t)(r[it] & 0x7Fu));
         } else {
@@ -2388,7 +2403,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow,
-    QTick T) {
+    QTick T, FoldFmt G, const uint64_t *__restrict__ rec0) {
     __shared__ __attribute__((aligned(16))) Slot slot[1 << kMaxRBits];   // LDS-DMA destinations
     __shared__ __attribute__((aligned(16))) uint64_t qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
@@ -2400,6 +2415,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     __shared__ int32_t tw_pm[kQTail];
     __shared__ int64_t tw_ts[kQTail];
     __shared__ uint32_t tw_ai[kQTail];
+    __shared__ uint32_t tw_pos[kQTail];           // reply positions
     __shared__ uint16_t tw_sorted[kQTail];        // tail entries by row
     __shared__ uint32_t tw_sum[kQBlock / 64];
     __shared__ uint32_t tw_max;
@@ -2412,7 +2428,8 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
 
     if (*err) return;
     const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = fold_bucket(G);
+    if (G.on && b >= G.nb) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     const bool tick = T.ts >= 0;
     if (s == e && !tick) return;
@@ -2428,6 +2445,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     // back whole; a sparse one gathers and writes back only the rows it touches.
     const bool dense = tick || (e - s) >= (R >> 3);   // a tick drains every row
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
         // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held for
@@ -2463,18 +2481,17 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     __syncthreads();
 
     for (uint32_t c = s; c < e; c += kQChunk) {
-        uint32_t kl[kQItems], ai[kQItems];
+        uint32_t kl[kQItems], ai[kQItems], pos[kQItems];
         int32_t pm[kQItems];
         int64_t ts[kQItems];
         uint32_t pend = 0;
 #pragma unroll
         for (int r = 0; r < kQItems; ++r) {
             const uint32_t q = c + r * kQBlock + tid;
+            pos[r] = q;
             if (q < e) {
                 if (PACKED) {
-                    uint32_t k;
-                    unpack_rec(srec[q], ts_orig, tbase, F, k, pm[r], ts[r]);
-                    kl[r] = k & rmask;
+                    fold_input(srec[q], q, G, tbase1, rec0, ts_orig, tbase, F, rmask, kl[r], pm[r], ts[r], pos[r]);
                 } else {
                     kl[r] = skeys[q] & rmask;
                     pm[r] = sperm[q];
@@ -2571,9 +2588,10 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                     const uint32_t q = c + wsorted[x];
                     int32_t p;
                     int64_t t;
+                    uint32_t qp = q;
                     if (PACKED) {
                         uint32_t k;
-                        unpack_rec(srec[q], ts_orig, tbase, F, k, p, t);
+                        fold_input(srec[q], q, G, tbase1, rec0, ts_orig, tbase, F, rmask, k, p, t, qp);
                     } else {
                         p = sperm[q];
                         t = sts[q];
@@ -2583,7 +2601,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                     const ReqTime rq1 = req_time_rel(t, TB, P.ttl_ms);
                     q_step(st, h, smod, hmod, p, rq1, TB, sidx[q], kr, P, Q, ev_cause, ev_id, ev_count, ev_cap, status,
                            rem, evaluated);
-                    put_wait(res, q, status, evaluated, rem, narrow);
+                    put_wait(res, qp, status, evaluated, rem, narrow);
                 }
                 if (smod) slot[j] = st;
                 if (hmod) qh[j] = h;
@@ -2620,7 +2638,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 const ReqTime rqr = req_time_rel(ts[r], TB, P.ttl_ms);
                 q_step(st, h, smod, hmod, pm[r], rqr, TB, ai[r], ring + (row0 + kl[r]) * (uint64_t)Q.cap, P, Q,
                        ev_cause, ev_id, ev_count, ev_cap, status, rem, evaluated);
-                put_wait(res, c + r * kQBlock + tid, status, evaluated, rem, narrow);
+                put_wait(res, pos[r], status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
                 if (hmod) qh[kl[r]] = h;
                 if (smod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
@@ -2645,6 +2663,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                             tw_pm[at] = pm[r];
                             tw_ts[at] = ts[r];
                             tw_ai[at] = ai[r];
+                            tw_pos[at] = pos[r];
                             ++at;
                         }
                     }
@@ -2713,7 +2732,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                                     const ReqTime rq1 = req_time_rel(tw_ts[en], TB, P.ttl_ms);
                                     q_step(st, h, smod, hmod, tw_pm[en], rq1, TB, tw_ai[en], kr, P, Q, ev_cause, ev_id,
                                            ev_count, ev_cap, status, rem, evaluated);
-                                    put_wait(res, c + (tw_e[en] >> 16), status, evaluated, rem, narrow);
+                                    put_wait(res, tw_pos[en], status, evaluated, rem, narrow);
                                 }
                                 if (smod) {
                                     slot[row] = st;
@@ -2740,6 +2759,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                                 pm[r] = tw_pm[at1];
                                 ts[r] = tw_ts[at1];
                                 ai[r] = tw_ai[at1];
+                                pos[r] = tw_pos[at1];
                                 ++at1;
                             }
                         }
@@ -3609,7 +3629,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // fold records for this batch: the reply position takes ceil_log2(n) bits, the time
     // offset what is left (>= 8 bits, else the plain records)
     FoldFmt G{};
-    if (e->foldrec && !approx && !wait) {
+    if (e->foldrec && !approx) {
         const int pw = std::max(1, ceil_log2(n));
         const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
         if (tw >= 8) {
@@ -3624,7 +3644,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         }
     }
     const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
-    const bool unrank = e->unrank && !approx && !wait;
+    const bool unrank = e->unrank && !approx;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
@@ -3674,7 +3694,12 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         else if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
+        else if (e->packed && wait && G.on && p == e->passes - 1)
+            k_scatter_rec<false, false, true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0,
+                w.pass[p - 1].idx, out.idx, G);
         else if (e->packed && wait)
             k_scatter_rec<false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3758,17 +3783,17 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         q.wait = e->wait_mode;
         q.ai_base = ai_base;
         if (e->packed)
-            k_fold_q<true><<<e->nbuckets, kQBlock, 0, sf>>>(
+            k_fold_q<true><<<fold_grid, kQBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
                 e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
                 e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(),
-                e->qtick);
+                e->qtick, G, rec0);
         else
             k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
                 e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
                 e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
-                e->wait_rw(), e->qtick);
+                e->wait_rw(), e->qtick, G, rec0);
     } else if (e->packed) {
         // dense buckets in k_fold_wide, the others in k_fold (each skips the other's)
         const uint32_t wmin = fold_wide_min(e, n);
@@ -3833,12 +3858,20 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                                     w.res[cur ^ 1], nullptr, nullptr);
         cur ^= 1;
     }
-    if (unrank && e->narrow)
-        k_unrank<1><<<ntiles, kPartBlock, 0, sf>>>(n, w.dig0, w.pass[0].tileprefix, w.pass[0].blockprefix,
-                                                   w.pass[0].digit_total, tpb, w.res[cur], granted, remaining);
+#define TBE_UNRANK(...)                                                                             \
+    __VA_ARGS__<<<ntiles, kPartBlock, 0, sf>>>(n, w.dig0, w.pass[0].tileprefix, w.pass[0].blockprefix, \
+                                               w.pass[0].digit_total, tpb, w.res[cur], granted, remaining)
+    if (unrank && !wait && e->narrow)
+        TBE_UNRANK(k_unrank<1>);
+    else if (unrank && !wait)
+        TBE_UNRANK(k_unrank<4>);
+    else if (unrank && e->narrow)
+        TBE_UNRANK(k_unrank<1, true>);
+    else if (unrank && e->medium)
+        TBE_UNRANK(k_unrank<2, true>);
     else if (unrank)
-        k_unrank<4><<<ntiles, kPartBlock, 0, sf>>>(n, w.dig0, w.pass[0].tileprefix, w.pass[0].blockprefix,
-                                                   w.pass[0].digit_total, tpb, w.res[cur], granted, remaining);
+        TBE_UNRANK(k_unrank<4, true>);
+#undef TBE_UNRANK
     else if (e->narrow && !wait && !approx)
         k_unscatter<true, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                   nullptr, granted, remaining);
@@ -3975,9 +4008,9 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
-        e->foldrec = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && e->passes >= 2 &&
-                     (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
-        e->unrank = e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        const bool tbq = c.kind == TBE_KIND_TOKEN_BUCKET || c.kind == TBE_KIND_QUEUEING;
+        e->foldrec = e->packed && tbq && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->unrank = e->packed && tbq && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
