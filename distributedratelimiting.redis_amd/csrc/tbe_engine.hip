@@ -777,7 +777,7 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
     }
     __syncthreads();
     int64_t tbase0 = 0, tbase1 = 0;
-    if (LAST) {
+    if (LAST && tin) {   // (the approximate kind has no timestamps: its records all escape)
         tbase0 = pack_base(tin, F);
         tbase1 = fold_base(tin, G);
     }
@@ -2935,7 +2935,8 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
     const uint32_t *__restrict__ bstart, int r_bits,
     uint64_t n_keys, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring, AParams A,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
-    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t rw) {
+    uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t rw, FoldFmt G,
+    const uint64_t *__restrict__ rec0) {
     __shared__ ALocal sl[kMaxRows];
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t rbuf[kAChunk];
@@ -2944,7 +2945,8 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
 
     if (*err) return;
     const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = fold_bucket(G);
+    if (G.on && b >= G.nb) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     if (s == e) return;
     const uint32_t R = 1u << r_bits;
@@ -2985,10 +2987,11 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
             const uint32_t q = c + r * kFoldBlock + tid;
             kl[r] = 0; pm[r] = 0;
             if (q < e) {
-                if (PACKED) {   // key | permit code | escape | arrival index (k_scatter_rec NOTS)
+                if (PACKED) {   // key | permit code | escape | arrival index (k_scatter_rec NOTS),
+                                // or a fold record: row | permit code | escape | reply position
                     const uint64_t rec = srec[q];
                     kl[r] = (uint32_t)rec & rmask;
-                    pm[r] = (int32_t)((rec >> F.kb) & ((1ull << F.pb) - 1));
+                    pm[r] = (int32_t)((rec >> (G.on ? G.rb : F.kb)) & ((1ull << F.pb) - 1));
                 } else {
                     kl[r] = skeys[q] & rmask;
                     pm[r] = sperm[q];
@@ -2997,10 +3000,15 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
             }
         }
         // a request's arrival index is read again where it queues or evicts (rare): not
-        // held across the rounds (registers)
+        // held across the rounds (registers).  With fold records it is the payload of the
+        // previous pass's record at the reply position.
+        auto reply_pos = [&](uint32_t q) -> uint32_t {
+            return G.on ? (uint32_t)((srec[q] >> (G.rb + G.pb + 1)) & ((1ull << G.pw) - 1)) : q;
+        };
         auto arrival = [&](int r) -> uint32_t {
             const uint32_t q = c + r * kFoldBlock + tid;
-            return PACKED ? (uint32_t)(srec[q] >> (F.kb + F.pb + 1)) : sidx[q];
+            if (!PACKED) return sidx[q];
+            return (uint32_t)((G.on ? rec0[reply_pos(q)] : srec[q]) >> (F.kb + F.pb + 1));
         };
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();
@@ -3121,8 +3129,9 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         for (int r = 0; r < kAPer; ++r) {
             const uint32_t q = c + r * kFoldBlock + tid;
             if (q < e) {
-                if (rw == 2) reinterpret_cast<uint16_t *>(res)[q] = wait16(rbuf[r * kFoldBlock + tid]);
-                else res[q] = rbuf[r * kFoldBlock + tid];
+                const uint32_t at = PACKED ? reply_pos(q) : q;
+                if (rw == 2) reinterpret_cast<uint16_t *>(res)[at] = wait16(rbuf[r * kFoldBlock + tid]);
+                else res[at] = rbuf[r * kFoldBlock + tid];
             }
         }
     }
@@ -3629,10 +3638,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // fold records for this batch: the reply position takes ceil_log2(n) bits, the time
     // offset what is left (>= 8 bits, else the plain records)
     FoldFmt G{};
-    if (e->foldrec && !approx) {
+    if (e->foldrec) {
         const int pw = std::max(1, ceil_log2(n));
         const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
-        if (tw >= 8) {
+        if (tw >= (approx ? 1 : 8)) {   // (the approximate kind's records carry no time)
             G.on = 1;
             G.rb = e->r_bits;
             G.pb = e->pf.pb;
@@ -3644,7 +3653,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         }
     }
     const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
-    const bool unrank = e->unrank && !approx;
+    const bool unrank = e->unrank;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
@@ -3686,7 +3695,12 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         if (e->packed && approx && p == 0)
             k_scatter_rec<true, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, nullptr, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, out.perm, w.err);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err);
+        else if (e->packed && approx && G.on && p == e->passes - 1)
+            k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
+                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0, nullptr,
+                nullptr, G);
         else if (e->packed && approx)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3768,15 +3782,15 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         a.wait = e->wait_mode;
         a.ai_base = ai_base;
         if (e->packed)
-            k_fold_a<true><<<e->nbuckets, kFoldBlock, 0, sf>>>(
+            k_fold_a<true><<<fold_grid, kFoldBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, e->pf, w.bstart, e->r_bits, e->cfg.n_keys, e->alocal,
                 e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
-                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw());
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(), G, rec0);
         else
             k_fold_a<false><<<e->nbuckets, kFoldBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.idx, nullptr, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
                 e->alocal, e->ring, a, w.res[0], e->ev_cause, e->ev_id, e->counters,
-                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw());
+                (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(), G, rec0);
     } else if (wait) {
         QParams q = e->qp;
         q.id_base = id_base;
@@ -4008,9 +4022,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         }
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
-        const bool tbq = c.kind == TBE_KIND_TOKEN_BUCKET || c.kind == TBE_KIND_QUEUEING;
-        e->foldrec = e->packed && tbq && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
-        e->unrank = e->packed && tbq && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->foldrec = e->packed && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->unrank = e->packed && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
