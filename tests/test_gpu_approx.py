@@ -24,16 +24,21 @@ S_US = 1_760_572_800 * 1_000_000
     # AvailableTokens fit the two-byte replies (14 bits, 16383 = "no script call"); 16383
     # and above take four-byte replies
     (2, OLDEST_FIRST, 8, True, True, 16382), (2, NEWEST_FIRST, 8, True, True, 16383),
-    (2, OLDEST_FIRST, 0, False, True, 16382)])
+    (2, OLDEST_FIRST, 0, False, True, 16382),
+    # 50k keys: two partition passes, so fold records and k_unrank (marked by a negative limit)
+    (2, NEWEST_FIRST, 4, True, True, -20), (2, OLDEST_FIRST, 0, False, True, -20)])
 def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, limit):
     import torch
     from distributedratelimiting.redis_amd import ApproximateEngine
-    n_keys, n, tokens, ticks = 300, 4000, 10, 10_000_000
+    n_keys, n, tokens, ticks = (300 if limit > 0 else 50_000), 4000, 10, 10_000_000
+    limit = abs(limit)
     rng = np.random.default_rng(n_clients * 100 + order * 10 + qlimit + limit)
     engines = [ApproximateEngine(n_keys, limit, tokens, ticks, qlimit, order, device=0, pack=pack)
                for _ in range(n_clients)]
     assert engines[0].layout()["packed"] == pack
     assert engines[0].layout()["medium"] == (limit <= 16382)
+    assert engines[0].layout()["passes"] == (1 if n_keys == 300 else 2)
+    assert engines[0].layout()["fold_records"] == (pack and n_keys != 300)
     choices = [0, 1, 1, 2, 3, 25] + ([limit // 3, limit // 2, limit, limit + 1] if limit > 100 else [])
     clients = [ApproxClient(limit, tokens, ticks, qlimit, order) for _ in range(n_clients)]
     table = ApproxGlobalTable(clients[0].decay_rate)
@@ -70,7 +75,7 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, l
             k, i, _ = logs[r]
             assert list(zip(k.tolist(), i.tolist())) == exp_logs[r]
         for r in range(n_clients):
-            for key in range(0, n_keys, 7):
+            for key in range(0, n_keys, 7 if n_keys == 300 else 613):
                 lo, gl, est, av, q = engines[r].local_state(key)
                 s = clients[r].st(key)
                 assert (lo, gl, est, av, q) == (s.local, s.global_, s.est, clients[r].available(s), len(s.queue))

@@ -17,9 +17,9 @@ S_US = 1_760_572_800 * 1_000_000
 ABSENT = np.iinfo(np.int64).min
 
 
-def make_pair(n_keys, token_limit, tokens_per_period, period_ticks, pack=True):
+def make_pair(n_keys, token_limit, tokens_per_period, period_ticks, pack=True, **kw):
     from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
-    eng = TokenBucketEngine(n_keys, token_limit, tokens_per_period, period_ticks, device=0, pack=pack)
+    eng = TokenBucketEngine(n_keys, token_limit, tokens_per_period, period_ticks, device=0, pack=pack, **kw)
     ref = cref.CTokenBucket(n_keys, token_limit, fill_rate(tokens_per_period, period_ticks))
     return eng, ref
 
@@ -438,3 +438,44 @@ def test_two_pass_partition_shapes(engine_lib, gpu, n_keys, n, batches):
     assert np.array_equal(v[touched].view(np.uint64), v_ref[touched].view(np.uint64))
     eng.close()
     ref.close()
+
+
+@pytest.mark.parametrize("case", ["two_pass", "two_pass_escape", "two_pass_hot", "three_pass", "sparse"])
+@pytest.mark.parametrize("fold", [True, False], ids=["fold_records", "unscatter_all"])
+def test_fold_records_layouts(engine_lib, gpu, case, fold):
+    """Fold records (the last partition pass carries each request's position in its input;
+    the fold, the sparse fold and the hot runs reply straight there) and the recomputed
+    final un-partition (k_unrank), against TBE_FLAG_UNSCATTER_ALL and the C restatement:
+    two passes; timestamps spread over hours (fold records escape to the previous pass's
+    record, itself escaping to the caller's array); hot-key runs; three passes (> 2^27
+    keys: 65536 reply regions); a sparse batch (the density gate sends its buckets to
+    k_fold)."""
+    rng = np.random.default_rng(hash(case) % 1000)
+    n_keys = {"three_pass": 140_000_000, "sparse": 100_000_000}.get(case, 3_000_000)
+    n = {"sparse": 1 << 16, "three_pass": 300_000}.get(case, 400_000)
+    eng, ref = make_pair(n_keys, 10, 3, 10_000_000, fold_records=fold)
+    lay = eng.layout()
+    assert lay["fold_records"] == fold and lay["passes"] == (3 if case == "three_pass" else 2)
+    hot = rng.integers(0, n_keys, 20).astype(np.uint64)
+    t = S_US
+    for b in range(4 if case == "two_pass_hot" else 2):
+        k = rng.integers(0, n_keys, n).astype(np.uint64)
+        if case == "two_pass_hot":
+            sel = rng.random(n) < 0.8
+            k[sel] = hot[rng.integers(0, 20, int(sel.sum()))]
+        p = rng.integers(0, 4, n).astype(np.int32)
+        span = 3 * 3_600_000_000 if case == "two_pass_escape" else 10_000
+        ts = (t + np.sort(rng.integers(0, span, n))).astype(np.int64)
+        if case == "two_pass_escape":
+            rng.shuffle(ts[: n // 2])       # out of order too
+        t = int(ts.max()) + 1
+        run_and_compare(eng, ref, k, p, ts)
+    if case != "three_pass":
+        assert_same_state(eng, ref)
+    else:   # 2.2 GB tables: the rows the batches touched
+        touched = np.unique(k)
+        v, tt = eng.export_state()
+        v_ref, t_ref = ref.export_state()
+        assert np.array_equal(tt[touched], t_ref[touched])
+        assert np.array_equal(v[touched].view(np.uint64), v_ref[touched].view(np.uint64))
+        assert np.array_equal(tt != ABSENT, t_ref != ABSENT)
