@@ -106,6 +106,9 @@ def parse():
                     help="skip the sparse-batch leg (2^20-request batches over config B's keys)")
     ap.add_argument("--no-strdir", action="store_true",
                     help="skip the string-key directory leg (config B batches as key text)")
+    ap.add_argument("--unscatter-all", action="store_true",
+                    help="plain last-pass records, every pass's permutation and un-partition "
+                         "(TBE_FLAG_UNSCATTER_ALL; A/B of the fold records and k_unrank)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     args = ap.parse_args()
@@ -275,7 +278,7 @@ def main():
                             args.period_ticks, device=dev.index,
                             stage_timing=not args.no_stage_timing, max_batch=m_max,
                             pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
-                            pipeline=not args.no_pipeline)
+                            pipeline=not args.no_pipeline, fold_records=not args.unscatter_all)
     layout = eng.layout()
     if rank == 0:
         write_fingerprint(run_fingerprint(args, world, keys_local, layout))
@@ -353,7 +356,7 @@ def main():
         ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                                 args.period_ticks, device=dev.index, stage_timing=True,
                                 max_batch=n, pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
-                                pipeline=False)
+                                pipeline=False, fold_records=not args.unscatter_all)
         g2 = torch.empty_like(granted)
         r2 = torch.empty_like(remaining)
         for s in range(args.warmup):

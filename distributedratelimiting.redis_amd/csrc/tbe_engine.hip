@@ -697,8 +697,13 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 // LAST (token-bucket kind, the last of >= 2 passes): write fold records (FoldFmt) -- each
 // element's position in this pass's input rides along -- and no permutation; `tin` is
 // then the caller's timestamps (for the record bases).
+// TBE_SCATTER0_WAVES (A/B): minimum waves per SIMD of the first pass (which holds the
+// caller's three columns of its 8 requests per thread in registers: 108 VGPRs, 4 waves)
+#ifndef TBE_SCATTER0_WAVES
+#define TBE_SCATTER0_WAVES 1
+#endif
 template <bool FIRST, bool HOT = false, bool IDX = false, bool NOTS = false, bool LAST = false>
-__global__ __launch_bounds__(kPartBlock) void k_scatter_rec(
+__global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_scatter_rec(
     const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
     const uint64_t *__restrict__ rin, uint64_t n, int shift, PackFmt F,
     const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,

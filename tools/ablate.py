@@ -102,6 +102,18 @@ VARIANT_SETS = {
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
     },
+    "r04": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
+        "s0w6_u": (["TBE_SCATTER0_WAVES=6"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "unall_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--unscatter-all"]),
+        "s0w6_z": (["TBE_SCATTER0_WAVES=6"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "unall_q": ([], ["--workload", "queue", "--no-drain-variant", "--unscatter-all"]),
+        "base_a": ([], ["--workload", "approx"]),
+        "unall_a": ([], ["--workload", "approx", "--unscatter-all"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),

@@ -25,3 +25,10 @@ if [ "$PART" = bench ]; then
     timeout -k 10 300 python -u bench.py --workload zipf --emulate-world 4 --steps 20 --warmup 5 > $OUT/${TAG}_emul4.log 2>&1 || { echo "emul4 failed"; tail -20 $OUT/${TAG}_emul4.log; exit 1; }
     tail -c 600 $OUT/${TAG}_emul4.log
 fi
+if [ "$PART" = ablate ]; then
+    # variants prebuilt here: ABLATE_SET=r04 python tools/ablate.py --build
+    ABLATE_SET=${ABLATE_SET:-r04} timeout -k 10 ${ABLATE_TIMEOUT:-900} python -u tools/ablate.py --run --rounds ${ROUNDS:-2} --steps ${STEPS:-5} > $OUT/${TAG}_ablate.log 2>&1
+    rc=$?
+    cut -c 1-400 $OUT/${TAG}_ablate.log | tail -40
+    exit $rc
+fi
