@@ -125,6 +125,21 @@ struct HotSet {
 
 __device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - TBE_HOT_SLOT_BITS); }
 constexpr uint64_t kHotSlotEmpty = 0xFFFFFFFFFFFFFFFFull;
+// TBE_HOT_CUCKOO (default on): the table is two halves of kHotSlots/2 slots and a key lives
+// at hot_h1 in the first half or hot_h2 in the second, so a probe is two independent LDS
+// reads and never a chain.  With linear probing at load 1/4, ~10% of a Zipf batch's
+// lookups continued a chain, so nearly every wave of every tile ran the chain loop
+// (profiles/r03_ablate_hot_probe.log: the probes cost 0.13 + 0.15 ms over uniform).
+#ifndef TBE_HOT_CUCKOO
+#define TBE_HOT_CUCKOO 1
+#endif
+constexpr uint32_t kHotHalf = kHotSlots / 2;
+__device__ __forceinline__ uint32_t hot_h1(uint32_t key) { return (key * 0x9E3779B1u) >> (33 - TBE_HOT_SLOT_BITS); }
+__device__ __forceinline__ uint32_t hot_h2(uint32_t key) {
+    uint32_t x = (key ^ (key >> 16)) * 0x85EBCA6Bu;
+    x ^= x >> 13;
+    return kHotHalf + ((x * 0xC2B2AE35u) >> (33 - TBE_HOT_SLOT_BITS));
+}
 
 // Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns
 // whether any key is hot.
@@ -151,6 +166,12 @@ __device__ __forceinline__ const uint64_t *hot_table(const HotSet *__restrict__ 
 // Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
 __device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *slots, uint32_t nb,
                                                 int r_bits) {
+#if TBE_HOT_CUCKOO
+    const uint64_t v1 = slots[hot_h1(key)], v2 = slots[hot_h2(key)];
+    if ((uint32_t)v1 == key) return (nb + (uint32_t)(v1 >> 32)) << r_bits;
+    if ((uint32_t)v2 == key) return (nb + (uint32_t)(v2 >> 32)) << r_bits;
+    return key;
+#endif
     uint32_t h = hot_hash(key);
     for (;;) {
         const uint64_t v = slots[h];
@@ -170,6 +191,28 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
     // A/B timing only (wrong partition): the cost of the hot-set probes
 #pragma unroll
     for (int it = 0; it < N; ++it) sk[it] = (uint32_t)kv[it] ^ ((uint32_t)slots[it & 7] & 1u);
+    return;
+#endif
+#if TBE_HOT_CUCKOO
+    // both probes of 4 requests in flight at a time (8 would spill in the hot histogram)
+    constexpr int G = N < 4 ? N : 4;
+    static_assert(N % G == 0, "groups of G requests");
+#pragma unroll
+    for (int g = 0; g < N; g += G) {
+        uint64_t v1[G], v2[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            v1[u] = slots[hot_h1((uint32_t)kv[g + u])];
+            v2[u] = slots[hot_h2((uint32_t)kv[g + u])];
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const uint32_t key = (uint32_t)kv[g + u];
+            const bool in1 = (uint32_t)v1[u] == key;
+            const uint64_t v = in1 ? v1[u] : v2[u];
+            sk[g + u] = (in1 || (uint32_t)v2[u] == key) ? (nb + (uint32_t)(v >> 32)) << r_bits : key;
+        }
+    }
     return;
 #endif
     uint64_t v[N];
@@ -2173,6 +2216,53 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
         }
     }
     const uint32_t nh = min(nc, cap);
+#if TBE_HOT_CUCKOO
+    // Two-choice placement in LDS (c is reused as the table once every thread holds its
+    // key): a CAS into the key's first-half slot, else its second-half slot; the few keys
+    // that lose both (~1% at load 1/4) are placed by thread 0 with cuckoo kicks.  A key
+    // that still finds no slot after kCuckooKicks moves stays out of the table: its requests
+    // take their ordinary buckets and its run is empty (speed only, never a decision).
+    __shared__ uint64_t left[64];
+    __shared__ uint32_t n_left;
+    const uint32_t key = t < nh ? (uint32_t)c[t] : 0u;
+    __syncthreads();
+    for (uint32_t j = t; j < kHotSlots; j += 1024) c[j] = kHotSlotEmpty;
+    if (t == 0) n_left = 0;
+    __syncthreads();
+    if (t < nh) {
+        next->key[t] = key;
+        const unsigned long long mine = ((unsigned long long)t << 32) | key;
+        unsigned long long *tab = reinterpret_cast<unsigned long long *>(c);
+        const unsigned long long o1 = atomicCAS(&tab[hot_h1(key)], kHotSlotEmpty, mine);
+        if (o1 != kHotSlotEmpty && (uint32_t)o1 != key) {
+            const unsigned long long o2 = atomicCAS(&tab[hot_h2(key)], kHotSlotEmpty, mine);
+            if (o2 != kHotSlotEmpty && (uint32_t)o2 != key) {
+                const uint32_t at = atomicAdd(&n_left, 1u);
+                if (at < 64) left[at] = mine;
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        constexpr int kCuckooKicks = 64;
+        for (uint32_t l = 0; l < min(n_left, 64u); ++l) {
+            uint64_t cur = left[l];
+            const uint32_t k0 = (uint32_t)cur;
+            if ((uint32_t)c[hot_h1(k0)] == k0 || (uint32_t)c[hot_h2(k0)] == k0) continue;   // a duplicate placed since
+            uint32_t at = hot_h1(k0);
+            for (int m = 0; m < kCuckooKicks && cur != kHotSlotEmpty; ++m) {
+                const uint64_t old = c[at];
+                c[at] = cur;
+                cur = old;
+                if (cur == kHotSlotEmpty) break;
+                const uint32_t k = (uint32_t)cur;
+                at = (at == hot_h1(k)) ? hot_h2(k) : hot_h1(k);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot[j] = c[j];
+#else
     if (t < nh) {
         const uint32_t key = (uint32_t)c[t];
         next->key[t] = key;
@@ -2186,6 +2276,7 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
             h = (h + 1) & (kHotSlots - 1);
         }
     }
+#endif
     if (t == 0) next->count = nh;
 }
 

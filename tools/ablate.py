@@ -109,6 +109,7 @@ VARIANT_SETS = {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "unall_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--unscatter-all"]),
         "s0w6_z": (["TBE_SCATTER0_WAVES=6"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "linprobe_z": (["TBE_HOT_CUCKOO=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
         "unall_q": ([], ["--workload", "queue", "--no-drain-variant", "--unscatter-all"]),
         "base_a": ([], ["--workload", "approx"]),
