@@ -24,6 +24,7 @@ TBE_FLAG_NO_HOT = 0x4
 TBE_FLAG_NO_PIPELINE = 0x8
 TBE_FLAG_NO_NARROW = 0x10
 TBE_FLAG_UNSCATTER_ALL = 0x20
+TBE_FLAG_HIST_RECORDS = 0x40
 STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter", "hot")
 
 # Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).

@@ -402,6 +402,139 @@ __global__ __launch_bounds__(kHBlock, HOT ? TBE_HIST_HOT_WAVES : TBE_HIST_WAVES)
     if (__any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
+// Pass 1's histogram (of 2) from the digit stream: pass 0's scatter wrote each request's
+// pass-1 digit as one byte in pass 0's output order (dig), so this reads 1 byte per request
+// where k_hist reads the 8-byte record.  Same outputs as k_hist's last pass: tileprefix,
+// blocksum and the per-bucket counts.  A request's bucket is (pass-1 digit << 8) | its
+// pass-0 digit, and the pass-0 digit follows from its position: pass 0's output is sorted
+// by it, with digit d starting at the exclusive scan of pass 0's digit totals (dtot0).
+// 512 threads x 8 consecutive bytes (one 8-byte load) per 4096-request tile.
+__global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
+    const uint8_t *__restrict__ dig, uint64_t n, uint32_t tiles_per_blk, uint32_t ntiles,
+    uint32_t *__restrict__ tileprefix, uint32_t *__restrict__ blocksum,
+    const uint32_t *__restrict__ dtot0, uint32_t *__restrict__ bcount, uint32_t nbt) {
+    __shared__ uint32_t h8[kDigits * 8];
+    __shared__ uint32_t dstart[kDigits + 1];
+    __shared__ uint32_t wsum[kHBlock / 64];
+    __shared__ uint32_t tile_lo[2];
+    static_assert(kHBlock == 2 * kDigits && kDigits * 8 == 4 * kHBlock, "two threads per digit; 4 counters each");
+    static_assert(kHItems == 8, "one 8-byte load per thread per tile");
+    const int tid = threadIdx.x;
+    const bool own = tid < kDigits;                  // this thread owns digit `tid`'s totals
+    {
+        uint32_t all;
+        const uint32_t pre = block_excl_scan<kHBlock>(own ? dtot0[tid] : 0u, wsum, &all);
+        if (own) dstart[tid] = pre;
+        if (tid == 0) dstart[kDigits] = 0xFFFFFFFFu;
+    }
+    // pass-0 digit of output position i: the last digit whose start is <= i
+    auto d0_of = [&](uint32_t i) {
+        uint32_t lo = 0, hi = kDigits;               // dstart[lo] <= i < dstart[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (dstart[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t t0 = blockIdx.x * tiles_per_blk;
+    const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
+    uint32_t run = 0, acc = 0, acc_lo = 0;
+    auto load = [&](uint32_t t) -> uint64_t {
+        const uint64_t i = (uint64_t)t * kTile + (uint64_t)tid * kHItems;
+        if (t >= t1 || i >= n) return 0ull;
+        if (i + kHItems <= n) return LD_P(reinterpret_cast<const uint64_t *>(dig + i));
+        uint64_t v = 0;
+        for (int u = 0; i + u < n; ++u) v |= (uint64_t)dig[i + u] << (8 * u);
+        return v;
+    };
+    uint64_t vn = load(t0);
+    __syncthreads();                                 // dstart
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint64_t v = vn;
+        vn = load(t + 1);                            // in flight while this tile is counted
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
+        const uint64_t base = (uint64_t)t * kTile;
+        const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
+        if (tid == 0) {
+            tile_lo[0] = d0_of((uint32_t)base);
+            tile_lo[1] = d0_of((uint32_t)last);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kHItems; ++u) {
+            const uint64_t i = base + (uint64_t)tid * kHItems + u;
+            const bool valid = i < n;
+            const uint32_t d = (uint32_t)(v >> (8 * u)) & (kDigits - 1);
+            const uint64_t vmask = __ballot(valid);
+            const uint32_t dw = __shfl(d, vmask ? __ffsll((long long)vmask) - 1 : 0, 64);
+            if (__all(!valid || d == dw)) {
+                if (vmask && (vmask & lanemask_lt()) == 0 && valid) atomicAdd(&h8[dw * 8], (uint32_t)__popcll(vmask));
+            } else if (valid) {
+                atomicAdd(&h8[d * 8 + (tid & 7)], 1u);
+            }
+        }
+        __syncthreads();
+        uint32_t c = 0;
+        if (own) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) c += h8[tid * 8 + ((u + tid) & 7)];
+            tileprefix[(uint64_t)t * kDigits + tid] = run;
+            run += c;
+        }
+        // per-bucket counts, as k_hist's last pass
+        const uint32_t lo0 = tile_lo[0], lo1 = tile_lo[1];
+        if (lo0 == lo1) {
+            if (own) {
+                if (lo0 != acc_lo) {
+                    const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
+                    if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+                    acc = 0;
+                    acc_lo = lo0;
+                }
+                acc += c;
+            }
+        } else if (lo1 - lo0 < 8) {
+            __syncthreads();                         // everyone has read its digit count
+#pragma unroll
+            for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kHItems; ++u) {
+                const uint64_t i = base + (uint64_t)tid * kHItems + u;
+                if (i >= n) continue;
+                uint32_t lo = 0;
+                for (uint32_t x = 1; x <= lo1 - lo0; ++x) lo += dstart[lo0 + x] <= (uint32_t)i;
+                const uint32_t d = (uint32_t)(v >> (8 * u)) & (kDigits - 1);
+                atomicAdd(&h8[lo * kDigits + d], 1u);
+            }
+            __syncthreads();
+            if (own) {
+                for (uint32_t u = 0; u <= lo1 - lo0; ++u) {
+                    const uint32_t cnt = h8[u * kDigits + tid];
+                    const uint32_t bk = ((uint32_t)tid << kDigitBits) | (lo0 + u);
+                    if (cnt && bk < nbt) atomicAdd(&bcount[bk], cnt);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kHItems; ++u) {
+                const uint64_t i = base + (uint64_t)tid * kHItems + u;
+                if (i >= n) continue;
+                const uint32_t bk = (((uint32_t)(v >> (8 * u)) & (kDigits - 1)) << kDigitBits) | d0_of((uint32_t)i);
+                if (bk < nbt) atomicAdd(&bcount[bk], 1u);
+            }
+        }
+        __syncthreads();
+    }
+    if (own) {
+        const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
+        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+        blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
+    }
+}
+
 // Digit-column scan, one workgroup per digit d: blockprefix[j][d] = number of digit-d
 // elements in blocks < j; digit_total[d] = all of them.  The digit bases (exclusive scan
 // of digit_total) are formed by each consumer workgroup itself.
@@ -753,7 +886,7 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
     uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
     uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
-    uint32_t *__restrict__ iout = nullptr, FoldFmt G = FoldFmt{}) {
+    uint32_t *__restrict__ iout = nullptr, FoldFmt G = FoldFmt{}, uint8_t *__restrict__ dig_next = nullptr) {
     static_assert(!(FIRST && LAST), "fold records come from a pass after the first");
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
@@ -839,6 +972,9 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             // runs merge in L2: keep cached
             rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
+            // the next pass's digit, one byte beside the record (k_hist_dig reads these)
+            if (!LAST && dig_next)
+                dig_next[gpos[it]] = (uint8_t)(((uint32_t)(s & F.kmask) >> (shift + kDigitBits)) & (kDigits - 1));
         }
     }
     if (IDX) {
@@ -3412,6 +3548,7 @@ struct Workspace {
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
     uint8_t *dig0 = nullptr;      // each request's pass-0 digit (k_unrank re-ranks from it)
+    uint8_t *dig1 = nullptr;      // pass 1's digit of pass 0's output, in that order (k_hist_dig)
     uint32_t *err = nullptr;      // the batch's invalid-request flag
     hipEvent_t hot_done = nullptr;   // pipelined: k_hot_update of the last batch on this workspace
     bool hot_pending = false;
@@ -3453,6 +3590,10 @@ struct tbe_engine {
     // k_unrank: the final un-partition recomputes pass 0's positions from one-byte digits,
     // so pass 0 writes no permutation (token bucket, packed; TBE_FLAG_UNSCATTER_ALL: off)
     bool unrank = false;
+    // digit stream (packed, 2 passes): pass 0 also writes each request's pass-1 digit as a
+    // byte in its output order, and pass 1's histogram (k_hist_dig) reads 1 byte per
+    // request instead of 8 (TBE_FLAG_HIST_RECORDS: off)
+    bool dig1 = false;
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
     // batch b+1 is partitioned by was complete before batch b's fold began.
@@ -3576,6 +3717,7 @@ void free_workspace(Workspace &w) {
     dfree(w.bstart);
     dfree(w.bcount);
     dfree(w.dig0);
+    dfree(w.dig1);
     dfree(w.err);
     w.cap_n = 0;
     w.used = false;
@@ -3630,6 +3772,7 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bcount, (uint64_t)e->nb_total * sizeof(uint32_t)));
     if (e->unrank) HIP_TRY(e, hipMalloc(&w.dig0, cap));
+    if (e->dig1) HIP_TRY(e, hipMalloc(&w.dig1, cap));
     HIP_TRY(e, hipMalloc(&w.err, sizeof(uint32_t)));
     w.cap_n = cap;
     return TBE_OK;
@@ -3763,6 +3906,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         uint32_t *bc = (p == e->passes - 1) ? w.bcount : nullptr;
         const int lowbits = kDigitBits * p;
         uint8_t *dig = (p == 0 && unrank) ? w.dig0 : nullptr;
+        uint8_t *dnext = (p == 0 && e->dig1) ? w.dig1 : nullptr;   // pass 1's digits (k_hist_dig)
         if (p == 0 && hot)
             k_hist<uint64_t, true><<<nblk, kHBlock, 0, sp>>>(keys, n, shift, tpb, ntiles, out.tileprefix,
                                                              w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
@@ -3773,6 +3917,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total, dig);
+        else if (e->dig1 && p == 1)
+            k_hist_dig<<<nblk, kHBlock, 0, sp>>>(w.dig1, n, tpb, ntiles, out.tileprefix, w.blocksum,
+                                                 w.pass[0].digit_total, bc, e->nb_total);
         else if (e->packed)
             k_hist<uint64_t><<<nblk, kHBlock, 0, sp>>>(w.pass[p - 1].rec, n, shift, tpb, ntiles,
                                                        out.tileprefix, w.blocksum, e->cfg.n_keys,
@@ -3791,7 +3938,8 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         if (e->packed && approx && p == 0)
             k_scatter_rec<true, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, nullptr, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
+                nullptr, FoldFmt{}, dnext);
         else if (e->packed && approx && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3804,7 +3952,8 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         else if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr, out.idx);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr, out.idx,
+                FoldFmt{}, dnext);
         else if (e->packed && wait && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -3818,11 +3967,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, hot, e->nbuckets, e->r_bits);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, hot, e->nbuckets, e->r_bits,
+                nullptr, nullptr, FoldFmt{}, dnext);
         else if (e->packed && p == 0)
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
                 keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
-                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err);
+                out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
+                nullptr, FoldFmt{}, dnext);
         else if (e->packed && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -4120,6 +4271,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->nb_total = e->nbuckets + hot_cap;
         e->foldrec = e->packed && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->unrank = e->packed && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->dig1 = e->packed && e->passes == 2 && (c.flags & TBE_FLAG_HIST_RECORDS) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
@@ -5154,7 +5306,8 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *passes = (uint32_t)e->passes;
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
-              (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u);
+              (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
+              (e->dig1 ? 64u : 0u);
     return TBE_OK;
 }
 

@@ -96,6 +96,11 @@ typedef struct tbe_config {
                                              passes, packed records) it writes fold records that
                                              carry each request's position in its input, and the
                                              fold puts every reply straight there */
+#define TBE_FLAG_HIST_RECORDS 0x40u       /* packed records, 2 passes (A/B checks): the second
+                                             pass's histogram reads the first pass's 8-byte
+                                             records.  By default the first pass also writes each
+                                             request's second digit as one byte beside its record,
+                                             and that histogram reads those */
 
 typedef struct tbe_engine tbe_engine;
 

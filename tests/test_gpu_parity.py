@@ -5,6 +5,8 @@ oracle (oracle/tb_ref.c), then compares granted/remaining per request and the fu
 bucket table (v bits and last-grant timestamps)."""
 import ctypes
 
+import zlib
+
 import numpy as np
 import pytest
 
@@ -441,21 +443,25 @@ def test_two_pass_partition_shapes(engine_lib, gpu, n_keys, n, batches):
 
 
 @pytest.mark.parametrize("case", ["two_pass", "two_pass_escape", "two_pass_hot", "three_pass", "sparse"])
-@pytest.mark.parametrize("fold", [True, False], ids=["fold_records", "unscatter_all"])
-def test_fold_records_layouts(engine_lib, gpu, case, fold):
+@pytest.mark.parametrize("fold,digits", [(True, True), (False, True), (True, False)],
+                         ids=["fold_records", "unscatter_all", "hist_records"])
+def test_fold_records_layouts(engine_lib, gpu, case, fold, digits):
     """Fold records (the last partition pass carries each request's position in its input;
     the fold, the sparse fold and the hot runs reply straight there) and the recomputed
     final un-partition (k_unrank), against TBE_FLAG_UNSCATTER_ALL and the C restatement:
     two passes; timestamps spread over hours (fold records escape to the previous pass's
     record, itself escaping to the caller's array); hot-key runs; three passes (> 2^27
     keys: 65536 reply regions); a sparse batch (the density gate sends its buckets to
-    k_fold)."""
-    rng = np.random.default_rng(hash(case) % 1000)
+    k_fold).  hist_records: the second pass's histogram reads the first pass's records
+    instead of the digit stream (k_hist_dig), whose tiles here lie inside one pass-0 digit,
+    straddle a few or (sparse) span many."""
+    rng = np.random.default_rng(zlib.crc32(case.encode()) % 1000)
     n_keys = {"three_pass": 140_000_000, "sparse": 100_000_000}.get(case, 3_000_000)
     n = {"sparse": 1 << 16, "three_pass": 300_000}.get(case, 400_000)
-    eng, ref = make_pair(n_keys, 10, 3, 10_000_000, fold_records=fold)
+    eng, ref = make_pair(n_keys, 10, 3, 10_000_000, fold_records=fold, digit_stream=digits)
     lay = eng.layout()
     assert lay["fold_records"] == fold and lay["passes"] == (3 if case == "three_pass" else 2)
+    assert lay["digit_stream"] == (digits and case != "three_pass")
     hot = rng.integers(0, n_keys, 20).astype(np.uint64)
     t = S_US
     for b in range(4 if case == "two_pass_hot" else 2):

@@ -105,10 +105,12 @@ VARIANT_SETS = {
     "r04": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
+        "histrec_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--hist-records"]),
         "s0w6_u": (["TBE_SCATTER0_WAVES=6"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "unall_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--unscatter-all"]),
         "s0w6_z": (["TBE_SCATTER0_WAVES=6"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "histrec_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--hist-records"]),
         "linprobe_z": (["TBE_HOT_CUCKOO=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
         "unall_q": ([], ["--workload", "queue", "--no-drain-variant", "--unscatter-all"]),

@@ -167,7 +167,7 @@ def summarise(workload, rmodel, wmodel):
             "step_hbm_bytes": step["read"] + step["write"]}
 
 
-STAGES = {"k_hist": "hist", "k_colscan": "colscan", "k_scatter": "scatter", "k_scatter_rec": "scatter",
+STAGES = {"k_hist": "hist", "k_hist_dig": "hist", "k_unrank": "unscatter", "k_bscan": "bounds", "k_colscan": "colscan", "k_scatter": "scatter", "k_scatter_rec": "scatter",
           "k_bounds": "bounds", "k_fold": "fold", "k_fold_wide": "fold", "k_fold_q": "fold", "k_fold_a": "fold",
           "k_unscatter": "unscatter", "k_drain": "drain", "k_hot_plan": "hot", "k_hot_summary": "hot",
           "k_hot_chain": "hot", "k_hot_replies": "hot", "k_hot_update": "hot"}
