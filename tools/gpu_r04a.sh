@@ -25,6 +25,15 @@ if [ "$PART" = bench ]; then
     timeout -k 10 300 python -u bench.py --workload zipf --emulate-world 4 --steps 20 --warmup 5 > $OUT/${TAG}_emul4.log 2>&1 || { echo "emul4 failed"; tail -20 $OUT/${TAG}_emul4.log; exit 1; }
     tail -c 600 $OUT/${TAG}_emul4.log
 fi
+if [ "$PART" = qab ]; then
+    # config D on one box: round 2's final tree (tools/r02tree, git worktree of d10368e, built
+    # here) and this tree, on the driver's schedule, twice each, alternating
+    for r in 1 2; do
+        (cd tools/r02tree && timeout -k 10 240 python -u bench.py --workload queue --steps 20 --warmup 5 --cpu-seconds 0) > $OUT/${TAG}_qab_r02_$r.log 2>&1 || { echo "r02 queue failed"; tail -20 $OUT/${TAG}_qab_r02_$r.log; exit 1; }
+        timeout -k 10 240 python -u bench.py --workload queue --steps 20 --warmup 5 --cpu-seconds 0 > $OUT/${TAG}_qab_now_$r.log 2>&1 || { echo "queue failed"; tail -20 $OUT/${TAG}_qab_now_$r.log; exit 1; }
+        for f in r02 now; do echo "$f $r: $(grep -o '"ms_per_step": [0-9.]*' $OUT/${TAG}_qab_${f}_$r.log | head -1) $(grep -o '"fold": [0-9.]*' $OUT/${TAG}_qab_${f}_$r.log | head -1)"; done
+    done
+fi
 if [ "$PART" = ablate ]; then
     # variants prebuilt here: ABLATE_SET=r04 python tools/ablate.py --build
     ABLATE_SET=${ABLATE_SET:-r04} timeout -k 10 ${ABLATE_TIMEOUT:-900} python -u tools/ablate.py --run --rounds ${ROUNDS:-2} --steps ${STEPS:-5} > $OUT/${TAG}_ablate.log 2>&1
