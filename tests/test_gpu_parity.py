@@ -458,7 +458,9 @@ def test_fold_records_layouts(engine_lib, gpu, case, fold, digits):
     rng = np.random.default_rng(zlib.crc32(case.encode()) % 1000)
     n_keys = {"three_pass": 140_000_000, "sparse": 100_000_000}.get(case, 3_000_000)
     n = {"sparse": 1 << 16, "three_pass": 300_000}.get(case, 400_000)
-    eng, ref = make_pair(n_keys, 10, 3, 10_000_000, fold_records=fold, digit_stream=digits)
+    # three passes (> 2^27 keys: a 28-bit key field) pack only with a 3-bit permit code
+    eng, ref = make_pair(n_keys, 6 if case == "three_pass" else 10, 3, 10_000_000, fold_records=fold,
+                         digit_stream=digits)
     lay = eng.layout()
     assert lay["fold_records"] == fold and lay["passes"] == (3 if case == "three_pass" else 2)
     assert lay["digit_stream"] == (digits and case != "three_pass")
