@@ -257,7 +257,7 @@ def main():
     if routed and args.owner_map == "balanced":
         loads = cluster.vnode_loads(gen_batch(0)[0])
         cluster._all_reduce_sum(loads)
-        omap = cluster.balanced_owner_map(loads.cpu().numpy(), world)
+        omap = cluster.balanced_owner_map(loads.cpu().numpy(), world, n_keys=keys_total)
     keys_local = cluster.keys_per_rank(keys_total, world, owner_map=omap)
     # --route timed: the directory's overflow check must not synchronise inside a step
     directory = cluster.DeviceDirectory(keys_local, device=dev.index, strict=args.route != "timed") \

@@ -75,7 +75,8 @@ def owner_stream(lib, args, W, rank, omap, keys_total, total, dev, stream, direc
 
 def time_owner(args, keys_local, bufs, dev):
     """The driver's schedule on one owner's batches: warm-up, then the timed steps between
-    synchronisations; the engine as bench.py builds it (pipelined, hot runs)."""
+    synchronisations; the engine as bench.py builds it (pipelined, hot runs).  The stage
+    times are the pipelined engine's event intervals, so the two streams' stages overlap."""
     from distributedratelimiting.redis_amd import TokenBucketEngine
     m_max = max(b[0].numel() for b in bufs)
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period, args.period_ticks,
@@ -97,8 +98,9 @@ def time_owner(args, keys_local, bufs, dev):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     st = eng.stage_times()
+    lay = eng.layout()
     eng.close()
-    return elapsed / args.steps * 1e3, {k: round(v / args.steps, 4) for k, v in st.items()}
+    return elapsed / args.steps * 1e3, {k: round(v / args.steps, 4) for k, v in st.items()}, lay
 
 
 def run(args, lib, dev):
@@ -120,7 +122,7 @@ def run(args, lib, dev):
                      keys_only=True)
             acc += cluster.vnode_loads(k)
         vn[s_] = acc.cpu().numpy()
-    maps = {"hash": cluster.hash_owner_map(W), "balanced": cluster.balanced_owner_map(vn[0], W)}
+    maps = {"hash": cluster.hash_owner_map(W), "balanced": cluster.balanced_owner_map(vn[0], W, n_keys=keys_total)}
     hot_vnode = int(np.argmax(vn[0]))
     res = {}
     for name, m in maps.items():
@@ -136,11 +138,12 @@ def run(args, lib, dev):
         for rk in pick:
             d = cluster.DeviceDirectory(keys_local, device=dev.index)
             bufs = owner_stream(lib, args, W, rk, m, keys_total, total, dev, stream, d)
-            ms, st = time_owner(args, keys_local, bufs, dev)
+            ms, st, lay = time_owner(args, keys_local, bufs, dev)
             ranks[str(rk)] = {"role": ",".join(x for x, y in (("max_load", worst), ("mean_load", typical),
                                                               ("hot_key_owner", hot_owner)) if y == rk),
                               "requests_per_step": round(float(mean[rk]), 1), "ms_per_step": round(ms, 4),
-                              "stage_ms_per_step": st, "directory_ids": d.size()}
+                              "stage_ms_per_step_overlapped": st, "directory_ids": d.size(),
+                              "layout": lay}
             del bufs
             d.close()
             torch.cuda.empty_cache()

@@ -92,14 +92,38 @@ def hash_owner_map(world: int) -> np.ndarray:
     return ((np.arange(OWNER_MAP_SIZE, dtype=np.int64) * world) >> OWNER_MAP_BITS).astype(np.uint8)
 
 
-def balanced_owner_map(loads, world: int) -> np.ndarray:
+# Keys one engine holds in its fastest layout: two 8-bit LSD passes over the bucket ids
+# (2^11 keys per bucket) with room for the 1024 hot-key buckets, and packed 8-byte records.
+# Past it the engine takes a third partition pass, and past 2^27 keys its records no longer
+# pack (a 28-bit key field leaves under 32 bits for the time offset), which also turns off
+# hot-key runs: on Zipf traffic that is a cliff, not a slope (DESIGN.md §7 "owner maps").
+PACKED_KEYS_MAX = (65536 - 1024) << 11
+
+
+def max_vnodes_per_owner(n_keys: int, world: int, slack: float = 0.01, limit: int = PACKED_KEYS_MAX) -> int:
+    """The most virtual nodes one owner may take while its table (keys_per_rank) stays
+    within `limit` keys; never fewer than the even share ceil(4096 / world)."""
+    fair = -(-OWNER_MAP_SIZE // world)
+    best = fair
+    for m in range(fair + 1, OWNER_MAP_SIZE + 1):
+        share = -(-n_keys * m // OWNER_MAP_SIZE)
+        if min(n_keys, int(share * (1.0 + slack)) + 1024) > limit:
+            break
+        best = m
+    return best
+
+
+def balanced_owner_map(loads, world: int, n_keys: int | None = None) -> np.ndarray:
     """An owner map that evens out the owners' request loads (DESIGN.md §7 "owner maps").
     loads[v] = requests observed on virtual node v (e.g. all ranks' vnode counts of a
     batch, all-reduced so that every rank builds the same map).  Longest processing time
     first: virtual nodes by descending load (ties by index), each to the owner with the
     least load so far (ties to the lowest rank), virtual nodes without load spread so that
     every owner ends with about the same number of them (its share of the key space).
-    Deterministic: the same loads give the same map on every rank."""
+    n_keys (the global key space): no owner takes more than max_vnodes_per_owner virtual
+    nodes, so every owner's table stays in the packed two-pass layout -- the owner of a
+    very hot key then keeps more of the load than the others instead of pushing their
+    tables over that limit.  Deterministic: the same loads give the same map on every rank."""
     loads = np.asarray(loads, dtype=np.int64).reshape(-1)
     if loads.size != OWNER_MAP_SIZE or world < 1 or world > 256:
         raise ValueError("loads must have 4096 entries and 1 <= world <= 256")
@@ -108,9 +132,11 @@ def balanced_owner_map(loads, world: int) -> np.ndarray:
     acc = np.zeros(world, dtype=np.int64)
     nv = np.zeros(world, dtype=np.int64)
     cap_v = -(-OWNER_MAP_SIZE // world)
+    cap = OWNER_MAP_SIZE if n_keys is None else max_vnodes_per_owner(n_keys, world)
+    big = np.iinfo(np.int64).max
     for v in order.tolist():
         if loads[v] > 0:
-            r = int(np.argmin(acc))
+            r = int(np.argmin(np.where(nv < cap, acc, big)))
         else:   # no load seen: keep the owners' shares of the key space level
             r = int(np.argmin(np.where(nv < cap_v, nv, OWNER_MAP_SIZE + 1)))
         out[v] = r

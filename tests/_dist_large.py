@@ -77,7 +77,7 @@ def tb_large_worker(rank: int, world: int, port: int, out_dir: str, keyspace: st
         # the owner map every rank builds from the all-reduced virtual-node loads of step 0
         loads = cluster.vnode_loads(gen(0, rank)[0])
         cluster._all_reduce_sum(loads)
-        omap = cluster.balanced_owner_map(loads.cpu().numpy(), world)
+        omap = cluster.balanced_owner_map(loads.cpu().numpy(), world, n_keys=K)
     cap = cluster.keys_per_rank(K, world, owner_map=omap)
     eng = TokenBucketEngine(cap, C["token_limit"], C["tokens_per_period"], C["period_ticks"], device=0,
                             stage_timing=True, max_batch=2 * N)

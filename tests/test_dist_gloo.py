@@ -95,6 +95,25 @@ def test_owner_maps():
     # no load at all: the shares of the key space stay level
     m = cluster.balanced_owner_map(np.zeros(cluster.OWNER_MAP_SIZE, np.int64), 8)
     assert np.bincount(m, minlength=8).tolist() == [512] * 8
+    # config C at 8 GPUs (1e9 keys): the uncapped map gives the hot key's owner few virtual
+    # nodes and every other owner more than 2^27 keys (a third pass, unpacked records, no
+    # hot runs); with n_keys no table leaves the packed two-pass layout, and the load is
+    # still more even than the hash partition's
+    for world in (4, 8):
+        per_hash = np.bincount(cluster.key_owner(zkeys, world), minlength=world)
+        free = cluster.balanced_owner_map(loads, world)
+        m = cluster.balanced_owner_map(loads, world, n_keys=10**9)
+        cap_v = cluster.max_vnodes_per_owner(10**9, world)
+        assert np.bincount(m, minlength=world).max() <= cap_v
+        if world == 8:   # (at 4 GPUs the even share, 2.5e8 keys, is past the limit anyway)
+            assert cluster.keys_per_rank(10**9, world, owner_map=m) <= cluster.PACKED_KEYS_MAX
+            assert cluster.keys_per_rank(10**9, world, owner_map=free) > cluster.PACKED_KEYS_MAX
+        per_bal = np.bincount(cluster.key_owner(zkeys, world, m), minlength=world)
+        assert per_bal.max() / per_bal.mean() < per_hash.max() / per_hash.mean()
+    # the cap never goes below the even share, and is the limit when the share is small
+    assert cluster.max_vnodes_per_owner(10**9, 8) >= 512
+    assert cluster.max_vnodes_per_owner(4 * 10**9, 8) == 512
+    assert cluster.max_vnodes_per_owner(10**6, 8) == cluster.OWNER_MAP_SIZE
 
 
 def check_tb_route(res):
