@@ -4270,7 +4270,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
         e->foldrec = e->packed && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
-        e->unrank = e->packed && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
+        e->unrank = e->packed && (c.flags & (TBE_FLAG_UNSCATTER_ALL | TBE_FLAG_PERM0)) == 0;
         e->dig1 = e->packed && e->passes == 2 && (c.flags & TBE_FLAG_HIST_RECORDS) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
@@ -5307,7 +5307,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
               (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
-              (e->dig1 ? 64u : 0u);
+              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u);
     return TBE_OK;
 }
 

@@ -59,7 +59,7 @@ class TokenBucketEngine:
                  device: int = -1, stage_timing: bool = False, max_batch: int = 0,
                  queue_limit: int = 0, queue_order: int = 0, pack: bool = True, hot: bool = True,
                  pipeline: bool = True, narrow: bool = True, zero_wait_slots: int = 0,
-                 fold_records: bool = True, digit_stream: bool = True):
+                 fold_records: bool = True, digit_stream: bool = True, rerank: bool = True):
         self._lib = _capi.load()
         flags = _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0
         if not pack:
@@ -74,6 +74,8 @@ class TokenBucketEngine:
             flags |= _capi.TBE_FLAG_UNSCATTER_ALL
         if not digit_stream:
             flags |= _capi.TBE_FLAG_HIST_RECORDS
+        if not rerank:
+            flags |= _capi.TBE_FLAG_PERM0
         self.config = _capi.make_config(n_keys, token_limit, tokens_per_period, period_ticks,
                                         kind=self.KIND, queue_limit=queue_limit,
                                         queue_order=queue_order, device=device, flags=flags,
@@ -174,14 +176,14 @@ class TokenBucketEngine:
                                                t_us.ctypes.data))
 
     def layout(self) -> dict:
-        """{passes, r_bits, packed, hot, pipeline, narrow, medium, fold_records, digit_stream} of this engine's
+        """{passes, r_bits, packed, hot, pipeline, narrow, medium, fold_records, digit_stream, rerank} of this engine's
         batch pipeline (tbe_layout)."""
         a, b, c = c_uint32(), c_uint32(), c_uint32()
         self._check(self._lib.tbe_layout(self.handle, byref(a), byref(b), byref(c)))
         return {"passes": a.value, "r_bits": b.value, "packed": bool(c.value & 1),
                 "hot": bool(c.value & 2), "pipeline": bool(c.value & 4), "narrow": bool(c.value & 8),
                 "medium": bool(c.value & 16), "fold_records": bool(c.value & 32),
-                "digit_stream": bool(c.value & 64)}
+                "digit_stream": bool(c.value & 64), "rerank": bool(c.value & 128)}
 
     def stage_times(self) -> dict:
         out = (c_double * len(_capi.STAGES))()

@@ -443,9 +443,10 @@ def test_two_pass_partition_shapes(engine_lib, gpu, n_keys, n, batches):
 
 
 @pytest.mark.parametrize("case", ["two_pass", "two_pass_escape", "two_pass_hot", "three_pass", "sparse"])
-@pytest.mark.parametrize("fold,digits", [(True, True), (False, True), (True, False)],
-                         ids=["fold_records", "unscatter_all", "hist_records"])
-def test_fold_records_layouts(engine_lib, gpu, case, fold, digits):
+@pytest.mark.parametrize("fold,digits,rerank", [(True, True, True), (False, True, True), (True, False, True),
+                                                (True, True, False)],
+                         ids=["fold_records", "unscatter_all", "hist_records", "perm0"])
+def test_fold_records_layouts(engine_lib, gpu, case, fold, digits, rerank):
     """Fold records (the last partition pass carries each request's position in its input;
     the fold, the sparse fold and the hot runs reply straight there) and the recomputed
     final un-partition (k_unrank), against TBE_FLAG_UNSCATTER_ALL and the C restatement:
@@ -460,10 +461,11 @@ def test_fold_records_layouts(engine_lib, gpu, case, fold, digits):
     n = {"sparse": 1 << 16, "three_pass": 300_000}.get(case, 400_000)
     # three passes (> 2^27 keys: a 28-bit key field) pack only with a 3-bit permit code
     eng, ref = make_pair(n_keys, 6 if case == "three_pass" else 10, 3, 10_000_000, fold_records=fold,
-                         digit_stream=digits)
+                         digit_stream=digits, rerank=rerank)
     lay = eng.layout()
     assert lay["fold_records"] == fold and lay["passes"] == (3 if case == "three_pass" else 2)
     assert lay["digit_stream"] == (digits and case != "three_pass")
+    assert lay["rerank"] == (fold and rerank)
     hot = rng.integers(0, n_keys, 20).astype(np.uint64)
     t = S_US
     for b in range(4 if case == "two_pass_hot" else 2):

@@ -117,6 +117,17 @@ VARIANT_SETS = {
         "base_a": ([], ["--workload", "approx"]),
         "unall_a": ([], ["--workload", "approx", "--unscatter-all"]),
     },
+    "r04b": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "perm0_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--perm0"]),
+        "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "perm0_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--perm0"]),
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "perm0_q": ([], ["--workload", "queue", "--no-drain-variant", "--perm0"]),
+        "base_a": ([], ["--workload", "approx"]),
+        "perm0_a": ([], ["--workload", "approx", "--perm0"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
