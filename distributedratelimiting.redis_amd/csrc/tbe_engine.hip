@@ -840,12 +840,13 @@ __device__ __forceinline__ void unfold_rec(uint64_t rec, const FoldFmt &G, int64
 // KB of one-byte replies at config B); the buckets of a region are dealt to one XCD
 // (workgroups b and b + 8 share one) and run there together, so that XCD's L2 merges their
 // scattered one-byte reply stores into whole lines.  Workgroups past the last bucket exit.
-__device__ __forceinline__ uint32_t fold_bucket(const FoldFmt &G) {
-    if (!G.on) return blockIdx.x;
-    const uint32_t x = blockIdx.x & 7u, s = blockIdx.x >> 3;
+__device__ __forceinline__ uint32_t fold_bucket_at(const FoldFmt &G, uint32_t blk) {
+    if (!G.on) return blk;
+    const uint32_t x = blk & 7u, s = blk >> 3;
     const uint32_t j = s / G.n_hi, hi = s - j * G.n_hi;
     return (hi << G.region_bits) | (x + 8u * j);
 }
+__device__ __forceinline__ uint32_t fold_bucket(const FoldFmt &G) { return fold_bucket_at(G, blockIdx.x); }
 // Any record of the fold's input: (row, permit code, time, reply position).
 __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldFmt &G, int64_t tbase1,
                                            const uint64_t *__restrict__ rec0, const int64_t *__restrict__ ts_orig,
@@ -1093,6 +1094,9 @@ constexpr int kWideBlock = TBE_WIDE_BLOCK;
 constexpr int kWidePer = TBE_WIDE_PER;
 constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
+#ifndef TBE_FOLD_PREFETCH
+#define TBE_FOLD_PREFETCH 0                  // A/B: blocks ahead whose slice k_fold_wide touches
+#endif
 #ifndef TBE_WIDE_MIN_SHIFT
 #define TBE_WIDE_MIN_SHIFT 11
 #endif
@@ -1215,6 +1219,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         }
     };
 
+#if TBE_FOLD_PREFETCH
+    uint32_t pf_sink = 0;
+#endif
     load_chunk(s);   // in flight together with the dense slice
     if (dense) {
         // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held
@@ -1252,6 +1259,28 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (uint32_t j = tid; j < R; j += kWideBlock) hcnt[j] = 0;
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
+#if TBE_FOLD_PREFETCH
+        // A/B: touch one word per 128-B line of the slice and of the records of the
+        // workgroup TBE_FOLD_PREFETCH blocks later (the same XCD), so that its loads find
+        // them in L2 or the Infinity Cache; issued after this slice landed, and not waited
+        // for until this workgroup ends
+        if (c == s) {
+            const uint32_t fblk = blockIdx.x + TBE_FOLD_PREFETCH;
+            const uint32_t fb = fold_bucket_at(G, fblk);
+            if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
+                const uint32_t fs = bstart[fb], fe = bstart[fb + 1];
+                if (fe - fs >= wide_min && fe > fs) {
+                    if (tid < (int)(kMaxRows / 8)) {
+                        const uint64_t fr = ((uint64_t)fb << r_bits) + (uint64_t)tid * 8u;
+                        if (fr < n_keys) pf_sink = reinterpret_cast<const uint32_t *>(table + fr)[0];
+                    } else if (PACKED) {
+                        const uint32_t q = fs + (uint32_t)(tid - kMaxRows / 8) * 16u;
+                        if (q < fe) pf_sink = (uint32_t)srec[q];
+                    }
+                }
+            }
+        }
+#endif
         if (count_hot) {
 #pragma unroll
             for (int r = 0; r < kWidePer; ++r)
@@ -1567,6 +1596,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             }
         }
     }
+#if TBE_FOLD_PREFETCH
+    if (wide_min == 0xFFFFFFFFu) res[s] = pf_sink;   // never (this kernel returned above): keeps the touches
+#endif
 }
 
 // k_fold's shape: 256-thread workgroups, 4 requests per thread per chunk, 48.5 KB of

@@ -121,6 +121,9 @@ VARIANT_SETS = {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "perm0_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--perm0"]),
         "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
+        "pf768_u": (["TBE_FOLD_PREFETCH=768"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf1536_u": (["TBE_FOLD_PREFETCH=1536"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf384_u": (["TBE_FOLD_PREFETCH=384"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "perm0_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--perm0"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
