@@ -112,9 +112,9 @@ def parse():
     ap.add_argument("--hist-records", action="store_true",
                     help="the second pass's histogram reads the first pass's records, not the "
                          "one-byte digit stream (TBE_FLAG_HIST_RECORDS; A/B)")
-    ap.add_argument("--perm0", action="store_true",
-                    help="pass 0 writes its permutation and the final un-partition gathers through "
-                         "it instead of re-ranking (TBE_FLAG_PERM0; A/B of k_unrank)")
+    ap.add_argument("--rerank", action="store_true",
+                    help="the final un-partition re-ranks pass 0's tiles from one-byte digits instead "
+                         "of gathering through pass 0's permutation (TBE_FLAG_RERANK; A/B of k_unrank)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream per batch: no overlap of batch b+1's partition with batch b's fold (A/B)")
     args = ap.parse_args()
@@ -285,7 +285,7 @@ def main():
                             stage_timing=not args.no_stage_timing, max_batch=m_max,
                             pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                             pipeline=not args.no_pipeline, fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=not args.perm0)
+                            digit_stream=not args.hist_records, rerank=args.rerank)
     layout = eng.layout()
     if rank == 0:
         write_fingerprint(run_fingerprint(args, world, keys_local, layout))
@@ -364,7 +364,7 @@ def main():
                                 args.period_ticks, device=dev.index, stage_timing=True,
                                 max_batch=n, pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                                 pipeline=False, fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=not args.perm0)
+                            digit_stream=not args.hist_records, rerank=args.rerank)
         g2 = torch.empty_like(granted)
         r2 = torch.empty_like(remaining)
         for s in range(args.warmup):

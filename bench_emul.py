@@ -81,7 +81,7 @@ def time_owner(args, keys_local, bufs, dev):
     m_max = max(b[0].numel() for b in bufs)
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period, args.period_ticks,
                             device=dev.index, stage_timing=True, max_batch=m_max, fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=not args.perm0)
+                            digit_stream=not args.hist_records, rerank=args.rerank)
     g = torch.empty(m_max, dtype=torch.uint8, device=dev)
     r = torch.empty(m_max, dtype=torch.int32, device=dev)
     for s_ in range(args.warmup):

@@ -226,7 +226,7 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
                                     args.queue_limit, 0, device=dev.index,
                                     stage_timing=not args.no_stage_timing, max_batch=n, pack=not args.no_pack,
                                     fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=not args.perm0)
+                            digit_stream=not args.hist_records, rerank=args.rerank)
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int32, device=dev)
@@ -420,7 +420,7 @@ def run_approx(args, lib, dev, world, rank, dist):
     eng = ApproximateEngine(kshared, args.token_limit, args.tokens_per_period, args.period_ticks,
                             0, 0, device=dev.index, stage_timing=not args.no_stage_timing, max_batch=n,
                             pack=not args.no_pack, fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=not args.perm0)
+                            digit_stream=not args.hist_records, rerank=args.rerank)
     seed = SEED_E + 7919 * rank
     bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)

@@ -25,7 +25,7 @@ TBE_FLAG_NO_PIPELINE = 0x8
 TBE_FLAG_NO_NARROW = 0x10
 TBE_FLAG_UNSCATTER_ALL = 0x20
 TBE_FLAG_HIST_RECORDS = 0x40
-TBE_FLAG_PERM0 = 0x80
+TBE_FLAG_RERANK = 0x80
 STAGES = ("hist", "colscan", "scatter", "bounds", "fold", "unscatter", "hot")
 
 # Every symbol include/tbe.h declares (tests/test_capi_symbols.py checks the header too).

@@ -1095,7 +1095,7 @@ constexpr int kWidePer = TBE_WIDE_PER;
 constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_FOLD_PREFETCH
-#define TBE_FOLD_PREFETCH 0                  // A/B: blocks ahead whose slice k_fold_wide touches
+#define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
 #endif
 #ifndef TBE_WIDE_MIN_SHIFT
 #define TBE_WIDE_MIN_SHIFT 11
@@ -1260,10 +1260,12 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
 #if TBE_FOLD_PREFETCH
-        // A/B: touch one word per 128-B line of the slice and of the records of the
-        // workgroup TBE_FOLD_PREFETCH blocks later (the same XCD), so that its loads find
-        // them in L2 or the Infinity Cache; issued after this slice landed, and not waited
-        // for until this workgroup ends
+        // Touch one word per 128-B line of the slice and of the records of the workgroup
+        // TBE_FOLD_PREFETCH blocks later (the same XCD), so that its loads find them in L2 or
+        // the Infinity Cache; issued after this slice landed, and waited for only at the
+        // barrier before this workgroup's write-back.  384 blocks = half of the 768
+        // workgroups in flight: config B fold 0.93 -> 0.85 ms; 768 -> 0.90, 1536 -> 0.93
+        // (profiles/r04d_ablate_perm0_prefetch.log)
         if (c == s) {
             const uint32_t fblk = blockIdx.x + TBE_FOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
@@ -3619,8 +3621,8 @@ struct tbe_engine {
     // put each reply straight into the previous pass's order, and that pass's un-partition
     // and permutation disappear (token bucket, packed; TBE_FLAG_UNSCATTER_ALL turns it off)
     bool foldrec = false;
-    // k_unrank: the final un-partition recomputes pass 0's positions from one-byte digits,
-    // so pass 0 writes no permutation (token bucket, packed; TBE_FLAG_UNSCATTER_ALL: off)
+    // k_unrank (TBE_FLAG_RERANK, A/B): the final un-partition recomputes pass 0's positions
+    // from one-byte digits, so pass 0 writes no permutation (packed records)
     bool unrank = false;
     // digit stream (packed, 2 passes): pass 0 also writes each request's pass-1 digit as a
     // byte in its output order, and pass 1's histogram (k_hist_dig) reads 1 byte per
@@ -4302,7 +4304,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->hot_cap = hot_cap;
         e->nb_total = e->nbuckets + hot_cap;
         e->foldrec = e->packed && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
-        e->unrank = e->packed && (c.flags & (TBE_FLAG_UNSCATTER_ALL | TBE_FLAG_PERM0)) == 0;
+        e->unrank = e->packed && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0 && (c.flags & TBE_FLAG_RERANK) != 0;
         e->dig1 = e->packed && e->passes == 2 && (c.flags & TBE_FLAG_HIST_RECORDS) == 0;
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||

@@ -59,7 +59,7 @@ class TokenBucketEngine:
                  device: int = -1, stage_timing: bool = False, max_batch: int = 0,
                  queue_limit: int = 0, queue_order: int = 0, pack: bool = True, hot: bool = True,
                  pipeline: bool = True, narrow: bool = True, zero_wait_slots: int = 0,
-                 fold_records: bool = True, digit_stream: bool = True, rerank: bool = True):
+                 fold_records: bool = True, digit_stream: bool = True, rerank: bool = False):
         self._lib = _capi.load()
         flags = _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0
         if not pack:
@@ -74,8 +74,8 @@ class TokenBucketEngine:
             flags |= _capi.TBE_FLAG_UNSCATTER_ALL
         if not digit_stream:
             flags |= _capi.TBE_FLAG_HIST_RECORDS
-        if not rerank:
-            flags |= _capi.TBE_FLAG_PERM0
+        if rerank:
+            flags |= _capi.TBE_FLAG_RERANK
         self.config = _capi.make_config(n_keys, token_limit, tokens_per_period, period_ticks,
                                         kind=self.KIND, queue_limit=queue_limit,
                                         queue_order=queue_order, device=device, flags=flags,

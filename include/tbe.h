@@ -96,10 +96,12 @@ typedef struct tbe_config {
                                              passes, packed records) it writes fold records that
                                              carry each request's position in its input, and the
                                              fold puts every reply straight there */
-#define TBE_FLAG_PERM0 0x80u              /* packed records (A/B checks): pass 0 writes its
-                                             permutation and the final un-partition gathers
-                                             through it, instead of re-ranking pass 0's tiles
-                                             from one-byte digits (k_unrank) */
+#define TBE_FLAG_RERANK 0x80u             /* packed records (A/B checks): the final
+                                             un-partition re-ranks pass 0's tiles from one-byte
+                                             digits the first histogram wrote (k_unrank) instead
+                                             of gathering through pass 0's stored permutation:
+                                             0.4 GB less traffic per config-B batch, 0.06 ms
+                                             slower */
 #define TBE_FLAG_HIST_RECORDS 0x40u       /* packed records, 2 passes (A/B checks): the second
                                              pass's histogram reads the first pass's 8-byte
                                              records.  By default the first pass also writes each
@@ -348,7 +350,7 @@ tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t 
  * pass writes fold records (TBE_FLAG_UNSCATTER_ALL clears it; used by batches whose
  * reply position and time offset fit), bit 6 set when the second
  * pass's histogram reads the one-byte digit stream (TBE_FLAG_HIST_RECORDS clears it),
- * bit 7 set when the final un-partition re-ranks pass 0's tiles (TBE_FLAG_PERM0 clears
+ * bit 7 set when the final un-partition re-ranks pass 0's tiles (TBE_FLAG_RERANK sets
  * it). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 

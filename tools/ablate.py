@@ -119,17 +119,28 @@ VARIANT_SETS = {
     },
     "r04b": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "perm0_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--perm0"]),
+        "rerank_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--rerank"]),
         "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
         "pf768_u": (["TBE_FOLD_PREFETCH=768"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "pf1536_u": (["TBE_FOLD_PREFETCH=1536"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "pf384_u": (["TBE_FOLD_PREFETCH=384"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "perm0_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--perm0"]),
+        "rerank_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--rerank"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
-        "perm0_q": ([], ["--workload", "queue", "--no-drain-variant", "--perm0"]),
+        "rerank_q": ([], ["--workload", "queue", "--no-drain-variant", "--rerank"]),
         "base_a": ([], ["--workload", "approx"]),
-        "perm0_a": ([], ["--workload", "approx", "--perm0"]),
+        "rerank_a": ([], ["--workload", "approx", "--rerank"]),
+    },
+    "r04c": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf0_u": (["TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf192_u": (["TBE_FOLD_PREFETCH=192"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf256_u": (["TBE_FOLD_PREFETCH=256"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf512_u": (["TBE_FOLD_PREFETCH=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "unall_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--unscatter-all"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "pf0_z": (["TBE_FOLD_PREFETCH=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "pf256_z": (["TBE_FOLD_PREFETCH=256"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
