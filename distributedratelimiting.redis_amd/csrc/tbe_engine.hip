@@ -1097,6 +1097,9 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_FOLD_PREFETCH
 #define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
 #endif
+#ifndef TBE_FOLD_PREFETCH_MIN
+#define TBE_FOLD_PREFETCH_MIN 1024           // ... by workgroups whose bucket has this many requests
+#endif
 #ifndef TBE_WIDE_MIN_SHIFT
 #define TBE_WIDE_MIN_SHIFT 11
 #endif
@@ -1266,7 +1269,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         // barrier before this workgroup's write-back.  384 blocks = half of the 768
         // workgroups in flight: config B fold 0.93 -> 0.85 ms; 768 -> 0.90, 1536 -> 0.93
         // (profiles/r04d_ablate_perm0_prefetch.log)
-        if (c == s) {
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
             const uint32_t fblk = blockIdx.x + TBE_FOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {

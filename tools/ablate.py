@@ -142,6 +142,16 @@ VARIANT_SETS = {
         "pf0_z": (["TBE_FOLD_PREFETCH=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "pf256_z": (["TBE_FOLD_PREFETCH=256"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "r04d": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pfmin0_u": (["TBE_FOLD_PREFETCH_MIN=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pfmin768_u": (["TBE_FOLD_PREFETCH_MIN=768"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf0_u": (["TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "pfmin0_z": (["TBE_FOLD_PREFETCH_MIN=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "pfmin768_z": (["TBE_FOLD_PREFETCH_MIN=768"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "pf0_z": (["TBE_FOLD_PREFETCH=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
