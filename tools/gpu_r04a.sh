@@ -34,6 +34,18 @@ if [ "$PART" = qab ]; then
         for f in r02 now; do echo "$f $r: $(grep -o '"ms_per_step": [0-9.]*' $OUT/${TAG}_qab_${f}_$r.log | head -1) $(grep -o '"fold": [0-9.]*' $OUT/${TAG}_qab_${f}_$r.log | head -1)"; done
     done
 fi
+if [ "$PART" = treeab ]; then
+    # the same box: round 3's final tree (tools/r03tree, git worktree of 3227af5, built here)
+    # against this one, alternating, on the driver's schedule (bench lines without the
+    # host-buffer and string-directory legs)
+    for r in $(seq 1 ${ROUNDS:-2}); do
+        for W in ${WLS:-uniform zipf}; do
+            (cd tools/r03tree && timeout -k 10 240 python -u bench.py --workload $W --steps 20 --warmup 5 --cpu-seconds 0 --no-host-buffer --no-strdir) > $OUT/${TAG}_tab_r03_${W}_$r.log 2>&1 || { echo "r03 $W failed"; tail -20 $OUT/${TAG}_tab_r03_${W}_$r.log; exit 1; }
+            timeout -k 10 240 python -u bench.py --workload $W --steps 20 --warmup 5 --cpu-seconds 0 --no-host-buffer --no-strdir --no-sparse > $OUT/${TAG}_tab_now_${W}_$r.log 2>&1 || { echo "now $W failed"; tail -20 $OUT/${TAG}_tab_now_${W}_$r.log; exit 1; }
+            for f in r03 now; do echo "$W $f $r: $(grep -o '"ms_per_step": [0-9.]*' $OUT/${TAG}_tab_${f}_${W}_$r.log | head -1)"; done
+        done
+    done
+fi
 if [ "$PART" = ablate ]; then
     # variants prebuilt here: ABLATE_SET=r04 python tools/ablate.py --build
     ABLATE_SET=${ABLATE_SET:-r04} timeout -k 10 ${ABLATE_TIMEOUT:-900} python -u tools/ablate.py --run --rounds ${ROUNDS:-2} --steps ${STEPS:-5} > $OUT/${TAG}_ablate.log 2>&1
