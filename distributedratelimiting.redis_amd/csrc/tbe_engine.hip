@@ -1097,6 +1097,12 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_FOLD_PREFETCH
 #define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
 #endif
+#ifndef TBE_QFOLD_PREFETCH
+#define TBE_QFOLD_PREFETCH 0                 // A/B: the same for k_fold_q
+#endif
+#ifndef TBE_AFOLD_PREFETCH
+#define TBE_AFOLD_PREFETCH 0                 // A/B: the same for k_fold_a
+#endif
 #ifndef TBE_FOLD_PREFETCH_MIN
 #define TBE_FOLD_PREFETCH_MIN 1024           // ... by workgroups whose bucket has this many requests
 #endif
@@ -2748,6 +2754,32 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     }
     lds_dma_wait();    // this wave's slice and header DMA landed
     __syncthreads();
+#if TBE_QFOLD_PREFETCH
+    // as k_fold_wide: touch the rows, queue headers and records of the workgroup
+    // TBE_QFOLD_PREFETCH blocks later (same XCD); waited for at the write-back barrier
+    uint32_t pf_sink = 0;
+    if (e - s >= TBE_FOLD_PREFETCH_MIN) {
+        const uint32_t fblk = blockIdx.x + TBE_QFOLD_PREFETCH;
+        const uint32_t fb = fold_bucket_at(G, fblk);
+        if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
+            const uint32_t fs = bstart[fb], fe = bstart[fb + 1];
+            const uint64_t frow = (uint64_t)fb << r_bits;
+            if (fe > fs && frow < n_keys) {
+                const uint32_t fn = (uint32_t)min<uint64_t>(R, n_keys - frow);
+                const uint32_t t = (uint32_t)tid;
+                if (t < kMaxRows / 8) {
+                    if (t * 8u < fn) pf_sink = reinterpret_cast<const uint32_t *>(table + frow + t * 8u)[0];
+                } else if (t < kMaxRows / 8 + kMaxRows / 16) {
+                    const uint32_t h = (t - kMaxRows / 8) * 16u;
+                    if (h < fn) pf_sink = reinterpret_cast<const uint32_t *>(qhdr + frow + h)[0];
+                } else if (PACKED) {
+                    const uint32_t q = fs + (t - kMaxRows / 8 - kMaxRows / 16) * 16u;
+                    if (q < fe) pf_sink = (uint32_t)srec[q];
+                }
+            }
+        }
+    }
+#endif
 
     for (uint32_t c = s; c < e; c += kQChunk) {
         uint32_t kl[kQItems], ai[kQItems], pos[kQItems];
@@ -3092,6 +3124,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
         if (dense ? ((hdirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(hdirty, j)) ST_U(hrows + j, qh[j]);
     }
+#if TBE_QFOLD_PREFETCH
+    if (n_keys == 0) res[s] = pf_sink;   // never (no engine has 0 keys): keeps the touches
+#endif
 }
 
 // One replenish tick (Q:237-271) over every key: drain the head (OldestFirst) or tail
@@ -3246,6 +3281,9 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         loaded[j] = dense ? ~0u : 0u;
         dirty[j] = 0;
     }
+#if TBE_AFOLD_PREFETCH
+    uint32_t pf_sink = 0;
+#endif
     for (uint32_t c = s; c < e; c += kAChunk) {
         for (uint32_t j = tid; j < R; j += kFoldBlock) own[j] = 0;
         uint32_t kl[kAPer];
@@ -3281,6 +3319,28 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
         };
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();
+#if TBE_AFOLD_PREFETCH
+        // as k_fold_wide: touch the local-tier slice and records of the workgroup
+        // TBE_AFOLD_PREFETCH blocks later (same XCD); waited for at the write-back barrier
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
+            const uint32_t fblk = blockIdx.x + TBE_AFOLD_PREFETCH;
+            const uint32_t fb = fold_bucket_at(G, fblk);
+            if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
+                const uint32_t fs = bstart[fb], fe = bstart[fb + 1];
+                const uint64_t frow = (uint64_t)fb << r_bits;
+                if (fe > fs && frow < n_keys) {
+                    const uint32_t fn = (uint32_t)min<uint64_t>(R, n_keys - frow);
+                    const uint32_t t = (uint32_t)tid;
+                    if (t < kMaxRows / 8) {
+                        if (t * 8u < fn) pf_sink = reinterpret_cast<const uint32_t *>(alocal + frow + t * 8u)[0];
+                    } else if (PACKED) {
+                        const uint32_t q = fs + (t - kMaxRows / 8) * 16u;
+                        if (q < fe) pf_sink = (uint32_t)srec[q];
+                    }
+                }
+            }
+        }
+#endif
         uint32_t mine = 0;
 #pragma unroll
         for (int r = 0; r < kAPer; ++r) {
@@ -3414,6 +3474,9 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
             rows[j] = sl[j];
         }
     }
+#if TBE_AFOLD_PREFETCH
+    if (n_keys == 0) res[s] = pf_sink;   // never (no engine has 0 keys): keeps the touches
+#endif
 }
 
 // A:430-435: count = _localThrottleScore; _localThrottleScore = 0, for every key.

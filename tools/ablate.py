@@ -152,6 +152,13 @@ VARIANT_SETS = {
         "pfmin768_z": (["TBE_FOLD_PREFETCH_MIN=768"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "pf0_z": (["TBE_FOLD_PREFETCH=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "r04e": {
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "qpf384_q": (["TBE_QFOLD_PREFETCH=384"], ["--workload", "queue", "--no-drain-variant"]),
+        "qpf768_q": (["TBE_QFOLD_PREFETCH=768"], ["--workload", "queue", "--no-drain-variant"]),
+        "base_a": ([], ["--workload", "approx"]),
+        "apf384_a": (["TBE_AFOLD_PREFETCH=384"], ["--workload", "approx"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
