@@ -2105,6 +2105,9 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
 //   k_hot_replies  (parallel)  decides every request of a pass-through segment against
 //                              the S it saw.
 // Which keys are hot only changes speed, never a decision.
+#ifndef TBE_HOT_SPEC
+#define TBE_HOT_SPEC 1
+#endif
 constexpr int kSegBlock = kFoldBlock;
 constexpr int kSegItems = 16;
 constexpr uint32_t kSeg = kSegBlock * kSegItems;  // 8192 requests per run segment
@@ -2117,7 +2120,8 @@ struct SegSummary {
 struct SegState {
     Slot s;          // the run's row when the segment starts
     double ft;       // its field t
-    uint32_t pass;   // 1: no request of the segment modifies s (k_hot_replies decides it)
+    uint32_t pass;   // 0: k_hot_chain decided the segment; 1: no request of it modifies s and
+                     // k_hot_replies decides it; 2: the same, already decided by k_hot_summary<true>
     uint32_t pad;
 };
 
@@ -2150,17 +2154,27 @@ __device__ __forceinline__ uint32_t seg_run(const uint32_t *__restrict__ segbase
     return lo;
 }
 
+// SPEC (TBE_HOT_SPEC, the default): also decide the segment here when it passes the run's
+// row as it stands before the batch (S0, table[key]) through -- the test k_hot_chain makes
+// first, on the same summary -- so in the steady state, where a run's segments all pass
+// (a hot key is mostly denied), k_hot_replies reads the run a second time only behind a
+// segment that modified the row.
+template <bool SPEC>
 __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
-    SegSummary *__restrict__ summ, const uint32_t *__restrict__ err, FoldFmt G, const uint64_t *__restrict__ rec0) {
+    SegSummary *__restrict__ summ, const uint32_t *__restrict__ err, FoldFmt G, const uint64_t *__restrict__ rec0,
+    const HotSet *__restrict__ hot = nullptr, const Slot *__restrict__ table = nullptr, TbParams P = TbParams{},
+    uint32_t *__restrict__ res = nullptr, uint32_t narrow = 0) {
     __shared__ int64_t wts[kSegBlock / 64];
     __shared__ int32_t wp[kSegBlock / 64];
+    __shared__ uint32_t pass_s0;
     if (*err) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
+    const TimeBase TB = time_base(tbase, P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const uint32_t h = seg_run(segbase, j);
         const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
@@ -2201,6 +2215,31 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
             }
             summ[j] = SegSummary{mx, mn, 0u};
         }
+        if (SPEC) {
+            const Slot s0 = table[hot->key[h]];
+            const double ft0 = new_t_of(s0.t_us == kAbsent ? 0 : s0.t_us);
+            if (tid == 0) {
+                Slot c = s0;
+                bool m;
+                (void)tb_step_ft(c, ft0, mn, req_time(mx, P.ttl_ms), P, m);
+                pass_s0 = m ? 0u : 1u;
+            }
+            __syncthreads();
+            if (pass_s0) {
+#pragma unroll
+                for (int it = 0; it < kSegItems; ++it) {
+                    const uint32_t q = a + it * kSegBlock + tid;
+                    if (q >= b) continue;
+                    uint32_t k, pos;
+                    int32_t p;
+                    int64_t ts;
+                    fold_input(rv[it], q, G, tbase1, rec0, ts_orig, tbase, F, 0u, k, p, ts, pos);
+                    Slot c = s0;
+                    bool m;
+                    put_reply(res, pos, tb_step_ft(c, ft0, p, req_time_rel(ts, TB, P.ttl_ms), P, m), narrow);
+                }
+            }
+        }
         __syncthreads();
     }
 }
@@ -2212,7 +2251,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     HotSet *__restrict__ hot_next, const uint32_t *__restrict__ segbase,
     const SegSummary *__restrict__ summ, SegState *__restrict__ sst, Slot *__restrict__ table,
     TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow, FoldFmt G,
-    const uint64_t *__restrict__ rec0) {
+    const uint64_t *__restrict__ rec0, uint32_t spec) {
     __shared__ Slot S;
     __shared__ double ftS;
     __shared__ uint32_t first, own;
@@ -2254,7 +2293,11 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
         atomicMin(&first, f);
         __syncthreads();
         f = first;
-        for (uint32_t u = cur + tid; u < f; u += kSegBlock) sst[j0 + u] = SegState{s, ft, 1u, 0u};
+        // pass = 1: k_hot_replies decides the segment; 2: k_hot_summary<true> already did
+        // (it passes the run's initial row through, which only the segments before the
+        // first modifying one see)
+        const uint32_t pv = (spec && !touched) ? 2u : 1u;
+        for (uint32_t u = cur + tid; u < f; u += kSegBlock) sst[j0 + u] = SegState{s, ft, pv, 0u};
         if (f == nseg) break;
         if (tid == 0) sst[j0 + f].pass = 0u;
         touched = true;
@@ -2341,7 +2384,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     const TimeBase TB = time_base(tbase, P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const SegState st = sst[j];
-        if (!st.pass) continue;
+        if (st.pass != 1u) continue;
         const uint32_t h = seg_run(segbase, j);
         const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
         const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
@@ -4182,11 +4225,17 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         stage_begin(e, ST_HOT, sf);
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
         k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
-        k_hot_summary<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                   w.segbase, w.summ, w.err, G, rec0);
+        if (TBE_HOT_SPEC)
+            k_hot_summary<true><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
+                                                             w.segbase, w.summ, w.err, G, rec0, hot, e->table,
+                                                             e->params, w.res[0], e->narrow ? 1u : 0u);
+        else
+            k_hot_summary<false><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
+                                                              w.segbase, w.summ, w.err, G, rec0);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
                                                       hot_next, w.segbase, w.summ, w.sst, e->table,
-                                                      e->params, w.res[0], w.err, e->narrow ? 1u : 0u, G, rec0);
+                                                      e->params, w.res[0], w.err, e->narrow ? 1u : 0u, G, rec0,
+                                                      TBE_HOT_SPEC ? 1u : 0u);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                    w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u,
                                                    G, rec0);

@@ -158,6 +158,8 @@ VARIANT_SETS = {
         "qpf768_q": (["TBE_QFOLD_PREFETCH=768"], ["--workload", "queue", "--no-drain-variant"]),
         "base_a": ([], ["--workload", "approx"]),
         "apf384_a": (["TBE_AFOLD_PREFETCH=384"], ["--workload", "approx"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "nospec_z": (["TBE_HOT_SPEC=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
