@@ -160,6 +160,9 @@ VARIANT_SETS = {
         "apf384_a": (["TBE_AFOLD_PREFETCH=384"], ["--workload", "approx"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "nospec_z": (["TBE_HOT_SPEC=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "hotw8_z": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "hotw8_u": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
