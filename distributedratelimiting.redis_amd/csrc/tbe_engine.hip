@@ -1097,6 +1097,9 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_FOLD_PREFETCH
 #define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
 #endif
+#ifndef TBE_WIDE_EARLY_DMA
+#define TBE_WIDE_EARLY_DMA 0
+#endif
 #ifndef TBE_QFOLD_PREFETCH
 #define TBE_QFOLD_PREFETCH 0                 // A/B: the same for k_fold_q
 #endif
@@ -1180,17 +1183,42 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     __shared__ uint32_t tw_max;
 #endif
 
-    if (*err) return;
     const int tid = threadIdx.x;
     const uint32_t b = fold_bucket(G);
     if (G.on && b >= G.nb) return;
-    const uint32_t s = bstart[b], e = bstart[b + 1];
-    if (s == e) return;
     const uint32_t R = 1u << r_bits;
     const uint32_t rmask = R - 1;
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
+    constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
+    // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held for it,
+    // so none of the loop invariants spill at this peak.  Rows past nrows get a copy of the
+    // last row; no request reaches them and they are never written.
+    auto slice_dma = [&]() {
+#pragma unroll
+        for (int u = 0; u < kRowsPerThread; ++u) {
+            const uint32_t j = tid + u * kWideBlock;
+            lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
+        }
+    };
+#if TBE_WIDE_EARLY_DMA
+    // A/B: in a dense batch (every bucket here) issue the slice before the error flag and
+    // the bucket bounds are read, so its latency overlaps theirs; an early return waits for
+    // the DMA first (its LDS must not be released under it)
+    const bool early = wide_min <= 1u;
+    if (early) slice_dma();
+    if (*err || bstart[b] == bstart[b + 1]) {
+        if (early) lds_dma_wait();
+        return;
+    }
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+#else
+    constexpr bool early = false;
+    if (*err) return;
+    const uint32_t s = bstart[b], e = bstart[b + 1];
+    if (s == e) return;
+#endif
     // Buckets with >= wide_min requests only (k_fold takes the others): the whole slice
     // is pulled in (LDS-DMA) and only its dirty lines are written back.
     if (e - s < wide_min) return;
@@ -1232,17 +1260,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     uint32_t pf_sink = 0;
 #endif
     load_chunk(s);   // in flight together with the dense slice
-    if (dense) {
-        // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held
-        // for it, so none of the loop invariants spill at this peak.  Rows past nrows get
-        // a copy of the last row; no request reaches them and they are never written.
-        constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
-#pragma unroll
-        for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kWideBlock;
-            lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
-        }
-    }
+    if (dense && !early) slice_dma();
     for (uint32_t j = tid; j < (R + 31) / 32; j += kWideBlock) {
         loaded[j] = 0;
         dirty[j] = 0;

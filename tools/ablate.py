@@ -163,6 +163,7 @@ VARIANT_SETS = {
         "hotw8_z": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "hotw8_u": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "edma_u": (["TBE_WIDE_EARLY_DMA=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
