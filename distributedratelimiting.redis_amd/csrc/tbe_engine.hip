@@ -876,6 +876,9 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 // then the caller's timestamps (for the record bases).
 // TBE_SCATTER0_WAVES (A/B): minimum waves per SIMD of the first pass (which holds the
 // caller's three columns of its 8 requests per thread in registers: 108 VGPRs, 4 waves)
+#ifndef TBE_LAST_PRESTAGE
+#define TBE_LAST_PRESTAGE 0                  // A/B: fold records formed before staging
+#endif
 #ifndef TBE_SCATTER0_WAVES
 #define TBE_SCATTER0_WAVES 1
 #endif
@@ -892,7 +895,11 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
+#if TBE_LAST_PRESTAGE
+    __shared__ uint8_t stage_d[LAST ? kTile : 1];    // LAST: each staged fold record's digit
+#else
     __shared__ uint16_t stage_e[LAST ? kTile : 1];   // LAST: each staged record's input element
+#endif
     __shared__ uint64_t hs[HOT ? kHotLds : 1];
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
@@ -944,35 +951,49 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
     rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
+    int64_t tbase0 = 0, tbase1 = 0;
+    if (LAST && tin) {   // (the approximate kind has no timestamps: its records all escape)
+        tbase0 = pack_base(tin, F);
+        tbase1 = fold_base(tin, G);
+    }
     __syncthreads();   // the counts in `stage` are dead from here on
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
         if (e < nvalid) {
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
+#if TBE_LAST_PRESTAGE
+            // LAST: the fold record is formed here, where the element's index is at hand,
+            // and its digit staged beside it (the record no longer carries it)
+            stage[lpos[it]] = LAST ? fold_rec(rec[it], (uint32_t)(base + e), tbase0, tbase1, F, G) : rec[it];
+            if (LAST)
+                stage_d[lpos[it]] = (uint8_t)d;
+#else
             stage[lpos[it]] = rec[it];
             if (LAST)
                 stage_e[lpos[it]] = (uint16_t)e;
+#endif
             else if (perm)   // (null: k_unrank recomputes the positions)
                 ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
         }
     }
     __syncthreads();
-    int64_t tbase0 = 0, tbase1 = 0;
-    if (LAST && tin) {   // (the approximate kind has no timestamps: its records all escape)
-        tbase0 = pack_base(tin, F);
-        tbase1 = fold_base(tin, G);
-    }
     uint32_t gpos[kPartItems];
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int j = it * kPartBlock + tid;
         if (j < nvalid) {
             const uint64_t s = stage[j];
+#if TBE_LAST_PRESTAGE
+            const uint32_t d = LAST ? (uint32_t)stage_d[j] : ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
+            gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
+            rout[gpos[it]] = s;   // runs merge in L2: keep cached
+#else
             const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             // runs merge in L2: keep cached
             rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
+#endif
             // the next pass's digit, one byte beside the record (k_hist_dig reads these)
             if (!LAST && dig_next)
                 dig_next[gpos[it]] = (uint8_t)(((uint32_t)(s & F.kmask) >> (shift + kDigitBits)) & (kDigits - 1));
@@ -1048,10 +1069,20 @@ __device__ __forceinline__ void lds_dma_wait() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#ifndef TBE_REPLY_NT
+#define TBE_REPLY_NT 0
+#endif
 // A token-bucket reply is {granted, trunc(new_v)} with 0 <= trunc(new_v) <= TokenLimit.
 // When TokenLimit <= 127 it travels as one byte (bit 7 granted, bits 0-6 remaining)
 // through the fold and the un-partition passes instead of four.
 __device__ __forceinline__ void put_reply(uint32_t *res, uint32_t q, uint32_t rep, uint32_t narrow) {
+#if TBE_REPLY_NT   // A/B: scattered one-byte replies with the streaming hint
+    if (narrow)
+        __builtin_nontemporal_store((uint8_t)(((rep >> 24) & 0x80u) | (rep & 0x7Fu)), reinterpret_cast<uint8_t *>(res) + q);
+    else
+        __builtin_nontemporal_store(rep, res + q);
+    return;
+#endif
     if (narrow)
         reinterpret_cast<uint8_t *>(res)[q] = (uint8_t)(((rep >> 24) & 0x80u) | (rep & 0x7Fu));
     else

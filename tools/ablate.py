@@ -165,6 +165,16 @@ VARIANT_SETS = {
         "hotw8_u": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "edma_u": (["TBE_WIDE_EARLY_DMA=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "r04f": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "prestage_u": (["TBE_LAST_PRESTAGE=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "replynt_u": (["TBE_REPLY_NT=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "prestage_z": (["TBE_LAST_PRESTAGE=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "replynt_z": (["TBE_REPLY_NT=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
+        "replynt_q": (["TBE_REPLY_NT=1"], ["--workload", "queue", "--no-drain-variant"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
