@@ -372,8 +372,10 @@ def main():
         ser.synchronize()
         ser.stage_times()
         g_all = [torch.empty(sizes[s], dtype=torch.uint8, device=dev) for s in range(args.warmup, total_steps)]
+        mark(lib, 3, dev)     # profiling marker: the replay's timed batches follow (tools/prof_window.py)
         for i, s in enumerate(range(args.warmup, total_steps)):
             ser.acquire_batch_device(*bufs[s], g_all[i], r2[:sizes[s]])
+        mark(lib, 4, dev)
         ser.synchronize()
         stages = ser.stage_times()
         replay_check = bool(torch.equal(g_all[-1][:m_last], granted[:m_last]) and
@@ -404,7 +406,7 @@ def main():
     if stages and sum(stages.values()) > 0:
         passes = layout["passes"]
         launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                    "unscatter": passes, "hot": 5}   # per step
+                    "unscatter": passes - (1 if layout.get("fold_records") else 0), "hot": 5}   # per step
         name = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
         # the dominant kernel's own algorithmic bytes per launch: the fold

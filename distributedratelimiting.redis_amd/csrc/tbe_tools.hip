@@ -199,6 +199,8 @@ extern "C" int tbe_mark_device(uint32_t tag, void *stream) {
     switch (tag) {
     case 1: k_mark<1><<<1, 64, 0, (hipStream_t)stream>>>(nullptr); break;
     case 2: k_mark<2><<<1, 64, 0, (hipStream_t)stream>>>(nullptr); break;
+    case 3: k_mark<3><<<1, 64, 0, (hipStream_t)stream>>>(nullptr); break;
+    case 4: k_mark<4><<<1, 64, 0, (hipStream_t)stream>>>(nullptr); break;
     default: return 1;
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;

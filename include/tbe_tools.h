@@ -45,9 +45,10 @@ int tbe_key_text_lengths_device(const uint64_t *d_keys, uint64_t n, uint32_t pre
 int tbe_key_text_device(const uint64_t *d_keys, uint64_t n, const char *prefix, uint32_t prefix_len,
                         const uint64_t *d_offs, uint8_t *d_bytes, void *stream);
 
-/* Profiling marker: enqueues one empty dispatch named k_mark<tag> (tag 1 or 2), so that a
- * rocprofv3 trace can keep exactly the dispatches enqueued between two markers (the
- * benchmark's timed batches).  Returns 0 on success. */
+/* Profiling marker: enqueues one empty dispatch named k_mark<tag> (tag 1 to 4), so that a
+ * rocprofv3 trace can keep exactly the dispatches enqueued between two markers: 1 and 2
+ * bracket the benchmark's timed batches, 3 and 4 the serial replay of them that the bench
+ * line's roofline times (tools/prof_window.py).  Returns 0 on success. */
 int tbe_mark_device(uint32_t tag, void *stream);
 
 /* HBM-counter calibration (k_calib<mode>): reads or writes a known byte count with one
