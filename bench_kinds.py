@@ -201,7 +201,8 @@ def mark(lib, tag: int, dev) -> None:
         lib.tbe_mark_device.restype = ctypes.c_int
         lib.tbe_mark_device.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
         _MARK_STREAM[dev] = torch.cuda.Stream(dev)
-    assert lib.tbe_mark_device(tag, _MARK_STREAM[dev].cuda_stream) == 0
+    # a profiling aid only: a library without this marker (an older A/B build) just skips it
+    lib.tbe_mark_device(tag, _MARK_STREAM[dev].cuda_stream)
 
 
 def _barrier_time(dist, dev, t0):
