@@ -69,6 +69,7 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, l
         for r in range(n_clients):
             engines[r].collect(counts[r])
         allc = torch.cat(counts)
+        torch.cuda.synchronize()   # the engines' sync replay reads allc on their own streams
         logs = [engines[r].sync(allc, n_clients, r, ts, stagger) for r in range(n_clients)]
         exp_logs = approx_refresh_all(clients, table, ts, stagger, range(n_keys))
         for r in range(n_clients):

@@ -278,6 +278,7 @@ def run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait
         for r in range(clients):
             engs[r].collect(counts[r])
         allc = torch.cat(counts)
+        torch.cuda.synchronize()   # the engines' sync replay reads allc on their own streams
         allc_h = np.concatenate([ref.collect() for ref in refs])
         assert np.array_equal(allc.cpu().numpy(), allc_h)
         ts = T0_US + (e + 1) * interval
