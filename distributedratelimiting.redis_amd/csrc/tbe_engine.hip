@@ -2157,6 +2157,9 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
 #ifndef TBE_HOT_SPEC
 #define TBE_HOT_SPEC 1
 #endif
+#ifndef TBE_HOT_SAMPLE
+#define TBE_HOT_SAMPLE 1
+#endif
 constexpr int kSegBlock = kFoldBlock;
 constexpr int kSegItems = 16;
 constexpr uint32_t kSeg = kSegBlock * kSegItems;  // 8192 requests per run segment
@@ -2549,6 +2552,55 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
     }
 #endif
     if (t == 0) next->count = nh;
+}
+
+// Cold start (TBE_HOT_SAMPLE): an engine's first two batches have no hot set yet (a key is
+// nominated by the fold of a batch and runs apart two batches later), so a key that
+// dominates them fills one ordinary bucket, whose workgroup walks its requests chunk by
+// chunk (config C's first two batches: ~27 ms folds).  Those batches are sampled instead:
+// kHotSampleN requests at a fixed stride are counted in a small hash table, every key
+// whose estimated requests reach kHotSampleMin is nominated into the batch's own hot set,
+// and k_hot_update builds it before the batch's first histogram.  Speed only: which keys
+// run apart never changes a decision.
+constexpr uint32_t kHotSampleN = 16384;
+constexpr uint32_t kHotSampleSlots = 32768;
+constexpr uint64_t kHotSampleMin = 65536;   // estimated requests of the batch
+__global__ __launch_bounds__(1024) void k_hot_sample_count(const uint64_t *__restrict__ keys, uint64_t n,
+                                                           uint64_t n_keys, uint32_t S,
+                                                           uint32_t *__restrict__ skey, uint32_t *__restrict__ scnt) {
+    const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+    if (i >= S) return;
+    const uint64_t key = keys[(uint64_t)i * n / S];
+    if (key >= n_keys || key >= 0xFFFFFFFFull) return;   // invalid keys fail the batch anyway
+    const uint32_t k = (uint32_t)key;
+    uint32_t h = (k * 0x9E3779B1u) >> (32 - 15);
+    static_assert(kHotSampleSlots == 1u << 15, "15-bit slots");
+    for (int probe = 0; probe < 64; ++probe) {
+        const uint32_t old = atomicCAS(&skey[h], 0xFFFFFFFFu, k);
+        if (old == 0xFFFFFFFFu || old == k) {
+            atomicAdd(&scnt[h], 1u);
+            return;
+        }
+        h = (h + 1) & (kHotSampleSlots - 1);
+    }
+}
+__global__ __launch_bounds__(1024) void k_hot_sample_pick(const uint32_t *__restrict__ skey,
+                                                          const uint32_t *__restrict__ scnt, uint64_t n,
+                                                          uint32_t S, HotSet *__restrict__ hot) {
+    __shared__ uint32_t nc;
+    if (threadIdx.x == 0) nc = 0;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kHotSampleSlots; j += 1024) {
+        const uint32_t c = scnt[j];
+        const uint64_t est = (uint64_t)c * n / S;
+        if (c != 0 && est >= kHotSampleMin) {
+            const uint32_t at = atomicAdd(&nc, 1u);
+            const uint64_t e32 = est < 0xFFFFFFFFull ? est : 0xFFFFFFFFull;
+            if (at < kHotCandMax) hot->cand[at] = (e32 << 32) | skey[j];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) hot->n_cand = nc;
 }
 
 // ----------------------------------------------------------------------------- queueing kind
@@ -3792,6 +3844,7 @@ struct tbe_engine {
     uint32_t hot_cap = 0;
     uint32_t nb_total = 0;
     HotSet *hot[3] = {nullptr, nullptr, nullptr};
+    uint32_t *hs_key = nullptr, *hs_cnt = nullptr;   // cold-start sampling (k_hot_sample_*)
     uint64_t nbatch = 0;
     Slot *table = nullptr;
     // queueing kind
@@ -4090,6 +4143,17 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // hot runs: see tbe_engine::hot
     HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
     HotSet *hot_next = e->hot_cap ? e->hot[(e->nbatch + 2) % 3] : nullptr;
+#if TBE_HOT_SAMPLE
+    if (hot && e->nbatch < 2 && e->hs_key && n >= kHotSampleMin) {
+        // cold start: nominate this batch's dominant keys into its own (still empty) hot set
+        const uint32_t S = (uint32_t)std::min<uint64_t>(n, kHotSampleN);
+        HIP_TRY(e, hipMemsetAsync(e->hs_key, 0xFF, kHotSampleSlots * sizeof(uint32_t), sp));
+        HIP_TRY(e, hipMemsetAsync(e->hs_cnt, 0, kHotSampleSlots * sizeof(uint32_t), sp));
+        k_hot_sample_count<<<(S + 1023) / 1024, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, S, e->hs_key, e->hs_cnt);
+        k_hot_sample_pick<<<1, 1024, 0, sp>>>(e->hs_key, e->hs_cnt, n, S, hot);
+        k_hot_update<<<1, 1024, 0, sp>>>(hot, e->hot_cap, w.err);
+    }
+#endif
     for (int p = 0; p < e->passes; ++p) {
         const int shift = e->r_bits + kDigitBits * p;
         PassBufs &out = w.pass[p];
@@ -4504,6 +4568,9 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
             if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
             if (hipMemsetAsync(hs, 0, sizeof(HotSet), e->stream) != hipSuccess) return bail(TBE_EDEVICE);
         }
+        if (hipMalloc(&e->hs_key, kHotSampleSlots * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&e->hs_cnt, kHotSampleSlots * sizeof(uint32_t)) != hipSuccess)
+            return bail(TBE_ENOMEM);
     }
     if (hipMalloc(&e->sticky, sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     if (hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), e->stream) != hipSuccess)
@@ -4575,6 +4642,8 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->log_rem);
     dfree(e->sticky);
     for (auto &hs : e->hot) dfree(hs);
+    dfree(e->hs_key);
+    dfree(e->hs_cnt);
     for (auto &ev : e->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ev_hot, e->ws[0].done, e->ws[1].done,

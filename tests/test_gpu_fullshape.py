@@ -106,7 +106,7 @@ def test_config_c_slice_full_shape(engine_lib, gpu):
     t = torch.empty(n, dtype=torch.int64, device=gpu)
     g = torch.empty(n, dtype=torch.uint8, device=gpu)
     r = torch.empty(n, dtype=torch.int32, device=gpu)
-    hot_ms = []
+    hot_ms, fold_ms = [], []
     for b in range(batches):
         assert lib.tbe_gen_zipf_keys_device(0x5EED000C, n_keys, 1.1, b * n, n, k.data_ptr(), None) == 0
         ts = workloads.batch_timestamps(b, n, 10_000, T0_US)
@@ -114,16 +114,21 @@ def test_config_c_slice_full_shape(engine_lib, gpu):
         torch.cuda.synchronize()
         eng.acquire_batch_device(k, p, t, g, r)
         eng.synchronize()
-        hot_ms.append(eng.stage_times().get("hot", 0.0))
+        st = eng.stage_times()
+        hot_ms.append(st.get("hot", 0.0))
+        fold_ms.append(st.get("fold", 0.0))
         hk = k.cpu().numpy().view(np.uint64)
         g_ref, r_ref = ref.acquire_batch(hk, np.ones(n, np.int32), ts, threads=THREADS)
         assert_replies(b, g.cpu().numpy(), r.cpu().numpy(), g_ref, r_ref)
         top = int(np.unique(hk[: 1 << 20], return_counts=True)[1].max()) * 64
         log(f"config C batch {b}: {n} replies identical (grant rate {g_ref.mean():.4f}, "
             f"hottest key ~{top} requests, hot-run time {hot_ms[-1]:.3f} ms)")
-    # hot runs exist from the third batch on (a key nominated by batch b runs in b+2);
-    # before that the hot-run kernels find an empty set and return
-    assert min(hot_ms[2:]) > 2 * max(hot_ms[:2]), hot_ms
+    # hot runs exist from the first batch on: a key nominated by batch b's fold runs in b+2,
+    # and the first two batches nominate their own dominant keys by sampling (cold start);
+    # without that, their folds walked the hottest key's ~7.4M requests in one workgroup
+    # (~27 ms each)
+    assert min(hot_ms) > 0.05, hot_ms
+    assert max(fold_ms) < 5.0, fold_ms
     assert_same_table(*eng.export_state(), *ref.export_state())
     log("config C slice: 1.25e8-row table identical")
 

@@ -175,6 +175,12 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
         "replynt_q": (["TBE_REPLY_NT=1"], ["--workload", "queue", "--no-drain-variant"]),
     },
+    "r04g": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "nosample_u": (["TBE_HOT_SAMPLE=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "nosample_z": (["TBE_HOT_SAMPLE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
