@@ -25,7 +25,7 @@ S_US = 1_760_572_800 * 1_000_000
     # and above take four-byte replies
     (2, OLDEST_FIRST, 8, True, True, 16382), (2, NEWEST_FIRST, 8, True, True, 16383),
     (2, OLDEST_FIRST, 0, False, True, 16382),
-    # 50k keys: two partition passes, so fold records and k_unrank (marked by a negative limit)
+    # 50k keys: two partition passes, so fold records (marked by a negative limit)
     (2, NEWEST_FIRST, 4, True, True, -20), (2, OLDEST_FIRST, 0, False, True, -20)])
 def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, limit):
     import torch

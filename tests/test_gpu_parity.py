@@ -448,14 +448,14 @@ def test_two_pass_partition_shapes(engine_lib, gpu, n_keys, n, batches):
                          ids=["fold_records", "unscatter_all", "hist_records", "rerank"])
 def test_fold_records_layouts(engine_lib, gpu, case, fold, digits, rerank):
     """Fold records (the last partition pass carries each request's position in its input;
-    the fold, the sparse fold and the hot runs reply straight there) and the recomputed
-    final un-partition (k_unrank), against TBE_FLAG_UNSCATTER_ALL and the C restatement:
+    the fold, the sparse fold and the hot runs reply straight there), against
+    TBE_FLAG_UNSCATTER_ALL and the C restatement:
     two passes; timestamps spread over hours (fold records escape to the previous pass's
     record, itself escaping to the caller's array); hot-key runs; three passes (> 2^27
     keys: 65536 reply regions); a sparse batch (the density gate sends its buckets to
     k_fold).  rerank: the final un-partition re-ranks pass 0's tiles (k_unrank) instead of
-    gathering through pass 0's permutation.  hist_records: the second pass's histogram reads the first pass's records
-    instead of the digit stream (k_hist_dig), whose tiles here lie inside one pass-0 digit,
+    gathering through pass 0's permutation.  hist_records: the second pass's histogram
+    reads the first pass's records instead of the digit stream (k_hist_dig), whose tiles here lie inside one pass-0 digit,
     straddle a few or (sparse) span many."""
     rng = np.random.default_rng(zlib.crc32(case.encode()) % 1000)
     n_keys = {"three_pass": 140_000_000, "sparse": 100_000_000}.get(case, 3_000_000)
