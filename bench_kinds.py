@@ -436,8 +436,15 @@ def run_approx(args, lib, dev, world, rank, dist):
 
     def refresh(s, mode, timed):
         t1 = time.perf_counter()
-        eng.collect(counts)             # A:430-435
         ts = T0_US + (s + 1) * args.interval_us
+        if mode == "node" and not dist:
+            # one client, nothing to exchange: RefreshAsync as one engine call (A:412-508)
+            eng.refresh(ts)
+            if timed:
+                refresh_s[mode][0] += time.perf_counter() - t1
+                refresh_s[mode][1] += 1
+            return
+        eng.collect(counts)             # A:430-435
         if mode == "node":
             if dist:                    # RCCL all-reduce over xGMI: the node is ONE client
                 cluster._all_reduce_sum(counts)

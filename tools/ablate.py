@@ -181,6 +181,10 @@ VARIANT_SETS = {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "nosample_z": (["TBE_HOT_SAMPLE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "wipE": {
+        "base_a": ([], ["--workload", "approx"]),
+        "fused_a": ([], ["--workload", "approx"], "wip_fused_refresh.patch"),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
@@ -192,6 +196,29 @@ VARIANT_SETS = {
 VARIANTS = VARIANT_SETS[os.environ.get("ABLATE_SET", "queue")]
 
 
+def lib_path(defs, patch=None):
+    tag = "_".join(defs).replace("=", "") or "base"
+    if patch:
+        tag = os.path.splitext(os.path.basename(patch))[0] + ("_" + tag if defs else "")
+    return os.path.join(OUTDIR, f"libtbe_{tag}.so")
+
+
+def build_patched(m, defs, patch, out):
+    """An experiment kept out of the tree's own sources: tools/<patch> (diff -ru of csrc/)
+    applied to a scratch copy of the sources, built like build.py builds libtbe.so."""
+    import shutil
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        pkg = os.path.join(tmp, "distributedratelimiting.redis_amd")
+        shutil.copytree(os.path.join(ROOT, "distributedratelimiting.redis_amd", "csrc"), os.path.join(pkg, "csrc"))
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+        subprocess.run(["patch", "-p1", "-s", "-d", pkg, "-i", os.path.join(ROOT, "tools", patch)], check=True)
+        srcs = [os.path.join(pkg, "csrc", os.path.basename(d)) for d in m.DEPS if d.endswith(".hip")]
+        cmd = [m.hipcc()] + list(m.HIPCC_FLAGS) + [f"-D{d}" for d in defs] + [
+            "-I", os.path.join(tmp, "include"), "-o", out] + srcs
+        subprocess.run(cmd, check=True)
+
+
 def build():
     import importlib.util
     spec = importlib.util.spec_from_file_location(
@@ -199,18 +226,22 @@ def build():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     os.makedirs(OUTDIR, exist_ok=True)
-    for name, (defs, _) in VARIANTS.items():
-        lib = os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so")
-        m.build_engine(defines=defs, out=lib)   # sha256-stamped: rebuilt when sources change
+    for name, v in VARIANTS.items():
+        defs, patch = v[0], (v[2] if len(v) > 2 else None)
+        lib = lib_path(defs, patch)
+        if patch:
+            build_patched(m, defs, patch, lib)
+        else:
+            m.build_engine(defines=defs, out=lib)   # sha256-stamped: rebuilt when sources change
         print("built", name)
 
 
 def run(rounds: int, steps: int):
     results = {}
     for r in range(rounds):
-        for name, (_, extra) in VARIANTS.items():
-            defs = VARIANTS[name][0]
-            env = dict(os.environ, TBE_LIB=os.path.join(OUTDIR, f"libtbe_{'_'.join(defs).replace('=', '') or 'base'}.so"))
+        for name, v in VARIANTS.items():
+            defs, extra = v[0], v[1]
+            env = dict(os.environ, TBE_LIB=lib_path(defs, v[2] if len(v) > 2 else None))
             args = ["--steps", str(steps), "--cpu-seconds", "0"] + ([] if "--no-strdir" in extra else ["--no-host-buffer", "--no-strdir"])
             if "--warmup" not in extra:
                 args += ["--warmup", "3"]
