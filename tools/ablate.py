@@ -184,6 +184,10 @@ VARIANT_SETS = {
     "wipE": {
         "base_a": ([], ["--workload", "approx"]),
         "fused_a": ([], ["--workload", "approx"], "wip_fused_refresh.patch"),
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "nomemset_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"], "wip_no_memsets.patch"),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "nomemset_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_no_memsets.patch"),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
