@@ -188,6 +188,7 @@ VARIANT_SETS = {
         "nomemset_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"], "wip_no_memsets.patch"),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "nomemset_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_no_memsets.patch"),
+        "hotpipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_hot_summary_pipelined.patch"),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
