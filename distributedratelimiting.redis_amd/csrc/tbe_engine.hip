@@ -3653,6 +3653,11 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride) {
+        // all_counts == nullptr: one client that collects here (A:430-435 fused into the
+        // epoch: the local count is swapped to 0 and used as this client's count)
+        ALocal a = alocal[k];
+        const int32_t own = a.local;
+        if (!all_counts) a.local = 0;
         double v = gv[k], p = gp[k];
         int64_t t = gt[k];
         int32_t my_global = 0;
@@ -3666,7 +3671,8 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
             const double pt = present ? new_t_of(t) : rq.new_t;
             const double dt = lua_max(0.0, rq.new_t - pt);                    // A:255
             const double decay = dt * A.decay_rate;
-            const double nv = lua_max(0.0, pv - decay) + (double)all_counts[(uint64_t)r * n_keys + k];  // A:258
+            const double nv = lua_max(0.0, pv - decay) +
+                              (double)(all_counts ? all_counts[(uint64_t)r * n_keys + k] : own);   // A:258
             const double a8 = pp * 0.8;                                       // A:262
             const double b2 = dt * 0.2;
             const double np = a8 + b2;
@@ -3690,7 +3696,6 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
         ac.global = my_global;
         ac.pad = 0;
         aclient[k] = ac;
-        ALocal a = alocal[k];
         const double lim = (double)wrap_sub(A.token_limit, my_global) / est;
         a.cap = dotnet_to_int(__builtin_ceil(lim));
         // drain (A:467-501)
@@ -5282,9 +5287,17 @@ tbe_status tbe_approx_collect(tbe_engine *e, int32_t *d_counts, void *stream) {
     return TBE_OK;
 }
 
+static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
+                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted);
 tbe_status tbe_approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
                            uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted) {
     if (!e || !d_all_counts || !n_granted) return TBE_EINVAL;
+    return approx_sync(e, d_all_counts, n_clients, my_client, ts_us, stagger_us, n_granted);
+}
+// d_all_counts == nullptr: a single client whose collect runs inside the sync kernel
+static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
+                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted) {
+    if (!e || !n_granted) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
     if (n_clients == 0 || my_client >= n_clients || ts_us < 0 || stagger_us < 0)
         return fail(e, TBE_EINVAL, "bad sync arguments");
@@ -5341,10 +5354,7 @@ tbe_status tbe_approx_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted)
     if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
     if (ts_us < 0) return fail(e, TBE_EINVAL, "ts_us < 0");
     HIP_TRY(e, hipSetDevice(e->device));
-    if (!e->acounts) HIP_TRY(e, hipMalloc(&e->acounts, e->cfg.n_keys * sizeof(int32_t)));
-    tbe_status rc = tbe_approx_collect(e, e->acounts, nullptr);
-    if (rc != TBE_OK) return rc;
-    return tbe_approx_sync(e, e->acounts, 1, 0, ts_us, 0, n_granted);
+    return approx_sync(e, nullptr, 1, 0, ts_us, 0, n_granted);
 }
 
 tbe_status tbe_approx_query(tbe_engine *e, uint64_t key, int32_t *local, int32_t *global_score,

@@ -317,9 +317,11 @@ tbe_status tbe_approx_collect(tbe_engine *engine, int32_t *d_counts, void *strea
 tbe_status tbe_approx_sync(tbe_engine *engine, const int32_t *d_all_counts, uint32_t n_clients,
                            uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted);
 
-/* RefreshAsync of a limiter that is the only client of its global tier (A:412-508):
- * tbe_approx_collect into an engine-owned buffer, then tbe_approx_sync with n_clients = 1.
- * Completed queued requests via tbe_refresh_log. */
+/* RefreshAsync of a limiter that is the only client of its global tier (A:412-508): the
+ * same as tbe_approx_collect followed by tbe_approx_sync with n_clients = 1, as one kernel
+ * pass over the local tier (each key's local count is swapped to 0 and used as the sync
+ * call's LocalCount; no host round trip between the two).  Completed queued requests via
+ * tbe_refresh_log. */
 tbe_status tbe_approx_refresh(tbe_engine *engine, int64_t ts_us, uint64_t *n_granted);
 
 /* Local-tier state of one key: _localThrottleScore, _globalThrottleScore,
