@@ -190,6 +190,10 @@ VARIANT_SETS = {
         "nomemset_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_no_memsets.patch"),
         "hotpipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_hot_summary_pipelined.patch"),
     },
+    "wipF": {
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "hotpipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_hot_summary_pipelined.patch"),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
