@@ -36,7 +36,8 @@ EXPORTED = ("tbe_fill_rate", "tbe_create", "tbe_destroy", "tbe_last_error", "tbe
             "tbe_approx_query", "tbe_layout", "tbe_stage_times", "tbe_wait_batch_device",
             "tbe_refresh_bound", "tbe_refresh_device", "tbe_approx_acquire_batch_device",
             "tbe_import_state", "tbe_queue_cancel", "tbe_alloc_host", "tbe_free_host",
-            "tbe_approx_export_state", "tbe_approx_import_state", "tbe_wait_batch_tick_device")
+            "tbe_approx_export_state", "tbe_approx_import_state", "tbe_wait_batch_tick_device",
+            "tbe_approx_sync_stream", "tbe_batch_format")
 TBE_WAIT_FAILED, TBE_WAIT_GRANTED, TBE_WAIT_QUEUED, TBE_WAIT_REJECTED = 0, 1, 2, 3
 
 
@@ -124,6 +125,11 @@ def load(path: str = None) -> ctypes.CDLL:
     lib.tbe_approx_sync.restype = c_int32
     lib.tbe_approx_sync.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_int64, c_int64,
                                     POINTER(c_uint64)]
+    lib.tbe_batch_format.restype = c_int32
+    lib.tbe_batch_format.argtypes = [c_void_p, c_uint64, c_void_p, c_uint32]
+    lib.tbe_approx_sync_stream.restype = c_int32
+    lib.tbe_approx_sync_stream.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_int64, c_int64, c_void_p,
+                                           POINTER(c_uint64)]
     lib.tbe_queue_attempt_batch.restype = c_int32
     lib.tbe_queue_attempt_batch.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
                                             c_void_p]

@@ -68,7 +68,7 @@ def key_owner(keys, world: int, owner_map=None) -> np.ndarray:
     >> 32, i.e. the top log2(world) bits of mix64(key) for a power-of-two world; with an
     owner map (include/tbe_cluster.h), owner_map[key_vnode(key)]."""
     if owner_map is not None:
-        return np.asarray(owner_map, dtype=np.int64)[key_vnode(keys)]
+        return np.asarray(check_owner_map(owner_map, world), dtype=np.int64)[key_vnode(keys)]
     h = _mix64(keys) >> np.uint64(32)
     with np.errstate(over="ignore"):
         return ((h * np.uint64(world)) >> np.uint64(32)).astype(np.int64)
@@ -82,6 +82,28 @@ OWNER_MAP_SIZE = 1 << OWNER_MAP_BITS
 def key_vnode(keys) -> np.ndarray:
     """Virtual node of each key: the top 12 bits of mix64(key) (tbe_key_vnode)."""
     return (_mix64(keys) >> np.uint64(64 - OWNER_MAP_BITS)).astype(np.int64)
+
+
+def check_owner_map(owner_map, world: int):
+    """Validate an owner map before any kernel reads it (include/tbe_cluster.h: a u8 array
+    of exactly 4096 entries, each < world).  A CUDA tensor's shape and dtype are checked
+    here; its values are not read back (that would synchronise every routed batch) -- the
+    route kernels clamp an entry >= world to world - 1, so a bad device map misroutes but
+    never writes out of bounds.  Returns the map unchanged; raises ValueError otherwise."""
+    if _is_cuda(owner_map):
+        import torch
+        if owner_map.dtype != torch.uint8 or owner_map.numel() != OWNER_MAP_SIZE:
+            raise ValueError(f"owner map must be {OWNER_MAP_SIZE} uint8 entries")
+        return owner_map
+    m = np.asarray(owner_map)
+    if m.shape != (OWNER_MAP_SIZE,):
+        raise ValueError(f"owner map must have exactly {OWNER_MAP_SIZE} entries, got shape {m.shape}")
+    if m.dtype != np.uint8:
+        if not np.issubdtype(m.dtype, np.integer) or m.min() < 0 or m.max() > 255:
+            raise ValueError("owner map entries must be uint8 owner ranks")
+    if int(m.max()) >= world:
+        raise ValueError(f"owner map entry {int(m.max())} >= world ({world})")
+    return m
 
 
 def hash_owner_map(world: int) -> np.ndarray:
@@ -221,7 +243,9 @@ class DeviceDirectory:
     batch.  ``strict=False``: near capacity each check enqueues an asynchronous copy of the
     directory's state (tbe_dir_state_async) and inspects the previous one, so an overflow
     raises one batch later without synchronising; the overflowing batch itself is still
-    refused, by the engine (its keys beyond capacity get UINT64_MAX ids, an invalid batch).
+    refused, by the engine (its keys beyond capacity get UINT64_MAX ids, an invalid batch:
+    TBE_EINVAL at the engine's next synchronisation, and that batch's reply buffers are left
+    unwritten).  Once an overflow has been seen every later check() raises, as in strict mode.
     bench.py --route timed uses it, so no synchronisation sits inside a timed step."""
 
     def __init__(self, capacity: int, device: int = -1, strict: bool = True):
@@ -240,6 +264,7 @@ class DeviceDirectory:
         self._bound = 0
         self.strict = strict
         self._pending = None     # (pinned state copy, event) of the last asynchronous check
+        self._overflowed = False  # an asynchronous check saw the (sticky) overflow bit
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -256,10 +281,13 @@ class DeviceDirectory:
             return
         import torch
         from . import _capi
+        if self._overflowed:   # the overflow bit is sticky: refuse every later batch too
+            raise _capi.TbeError(_capi.TBE_ERANGE, f"key directory over capacity ({self.capacity} ids)")
         if self._pending is not None and self._pending[1].query():
             st = self._pending[0]
             self._pending = None
             if int(st[1]) != 0:
+                self._overflowed = True
                 raise _capi.TbeError(_capi.TBE_ERANGE, f"key directory over capacity ({self.capacity} ids)")
         if self._pending is None:
             dev = torch.device("cuda", torch.cuda.current_device())
@@ -335,11 +363,13 @@ def vnode_loads(d_keys):
     return out
 
 
-def _device_map(owner_map, dev):
-    """The owner map as a u8 device tensor (NULL pointer for the hash partition)."""
+def _device_map(owner_map, dev, world: int):
+    """The owner map as a u8 device tensor (NULL pointer for the hash partition), validated
+    (check_owner_map) so that no route kernel sees an entry >= world."""
     if owner_map is None:
         return None
     import torch
+    check_owner_map(owner_map, world)
     m = owner_map if _is_cuda(owner_map) else torch.from_numpy(np.ascontiguousarray(owner_map, dtype=np.uint8))
     return m.to(device=dev, dtype=torch.uint8).contiguous()
 
@@ -464,7 +494,7 @@ def _route_device(keys, permits, payload, world, group, owner_map=None):
     pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     counts = torch.zeros(world, dtype=torch.int64, device=dev)
     work = torch.empty(max(1, lib.tbe_route_workspace_bytes(n, world)), dtype=torch.uint8, device=dev)
-    dmap = _device_map(owner_map, dev)
+    dmap = _device_map(owner_map, dev, world)
     _check(lib.tbe_route_plan_map_device(keys.data_ptr(), n, world, dmap.data_ptr() if dmap is not None else None,
                                          work.data_ptr(), pos.data_ptr(), counts.data_ptr(), stream))
     send = torch.empty((n, 3), dtype=torch.int64, device=dev)
@@ -635,22 +665,25 @@ def approx_epoch(engine, counts, ts_us: int, stagger_us: int, mode: str = "clien
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     engine.collect(counts)
     if world == 1:
-        return engine.sync(counts, 1, 0, ts_us, stagger_us)
+        return engine.sync(counts, 1, 0, ts_us, stagger_us, **_after_collective(counts))
     if mode == "clients":       # every rank is a client: exact prefix semantics
         allc = torch.empty(world * counts.numel(), dtype=counts.dtype, device=counts.device)
         _all_gather(allc, counts, group=group)
-        _wait_collective(counts)
-        return engine.sync(allc, world, rank, ts_us, stagger_us)
+        return engine.sync(allc, world, rank, ts_us, stagger_us, **_after_collective(counts))
     if mode == "node":          # the node is one client: sum of the ranks' counts
         _all_reduce_sum(counts, group=group)
-        _wait_collective(counts)
-        return engine.sync(counts, 1, 0, ts_us, stagger_us)
+        return engine.sync(counts, 1, 0, ts_us, stagger_us, **_after_collective(counts))
     raise ValueError(f"unknown mode {mode!r}")
 
 
-def _wait_collective(t) -> None:
-    """The engine's sync replay reads the exchanged counts on its own stream: wait for the
-    collective on the current stream first."""
-    if _is_cuda(t):
-        import torch
-        torch.cuda.current_stream(t.device).synchronize()
+def _after_collective(t) -> dict:
+    """The engine's sync replay reads the exchanged counts on its own stream: order it after
+    the collective on the current stream (tbe_approx_sync_stream: an event, no host wait)."""
+    if not _is_cuda(t):
+        return {}
+    import torch
+    cur = torch.cuda.current_stream(t.device)
+    if not cur.cuda_stream:     # the legacy default stream: no handle to order after
+        cur.synchronize()
+        return {}
+    return {"stream": cur.cuda_stream}

@@ -32,11 +32,22 @@ constexpr uint32_t kMaxOwners = 256;
 __device__ __forceinline__ uint32_t route_owner(uint64_t key, uint32_t G, const uint8_t *m) {
     return m ? (uint32_t)m[key_vnode(key)] : key_owner(key, G);
 }
-__device__ __forceinline__ const uint8_t *load_owner_map(const uint8_t *__restrict__ omap, uint8_t *lds) {
+// Entries >= G are clamped to G - 1 on the way into LDS, so a malformed map (the header
+// requires every entry < n_owners; cluster.py validates before calling) misroutes requests
+// but can never index the per-owner arrays out of bounds.
+__device__ __forceinline__ const uint8_t *load_owner_map(const uint8_t *__restrict__ omap, uint8_t *lds,
+                                                         uint32_t G) {
     if (!omap) return nullptr;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(omap);
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
-    for (uint32_t j = threadIdx.x; j < kOwnerMapSize / 4; j += blockDim.x) dst[j] = src[j];
+    const uint32_t top = G - 1u;
+    for (uint32_t j = threadIdx.x; j < kOwnerMapSize / 4; j += blockDim.x) {
+        const uint32_t w = src[j];
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) o |= min((w >> (8 * b)) & 0xFFu, top) << (8 * b);
+        dst[j] = o;
+    }
     __syncthreads();
     return lds;
 }
@@ -50,7 +61,7 @@ __global__ __launch_bounds__(kRtBlock) void k_route_count(const uint64_t *__rest
     const int tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kRtTile;
     for (uint32_t j = tid; j < G; j += kRtBlock) c[j] = 0;
-    const uint8_t *m = load_owner_map(omap, mlds);   // (its barrier also publishes c[])
+    const uint8_t *m = load_owner_map(omap, mlds, G);   // (its barrier also publishes c[])
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kRtItems; ++it) {
@@ -114,7 +125,7 @@ __global__ __launch_bounds__(kRtBlock) void k_route_pos(const uint64_t *__restri
     const int tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kRtTile;
     const int nvalid = (int)min<uint64_t>(kRtTile, n - base);
-    const uint8_t *m = load_owner_map(omap, mlds);
+    const uint8_t *m = load_owner_map(omap, mlds, G);
     uint32_t own[kRtItems], lpos[kRtItems];
 #pragma unroll
     for (int it = 0; it < kRtItems; ++it) {

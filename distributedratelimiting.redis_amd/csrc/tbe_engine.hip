@@ -2496,6 +2496,7 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
     // that lose both (~1% at load 1/4) are placed by thread 0 with cuckoo kicks.  A key
     // that still finds no slot after kCuckooKicks moves stays out of the table: its requests
     // take their ordinary buckets and its run is empty (speed only, never a decision).
+    static_assert(kHotSlots <= kHotCandMax, "the cuckoo table reuses c[kHotCandMax] as its kHotSlots slots");
     __shared__ uint64_t left[64];
     __shared__ uint32_t n_left;
     const uint32_t key = t < nh ? (uint32_t)c[t] : 0u;
@@ -4081,6 +4082,27 @@ uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #endif
 }
 
+// Fold records for a batch of n requests: the reply position takes ceil_log2(n) bits, the
+// time offset what is left (>= 8 bits, else the plain records).  tbe_batch_format reports it.
+FoldFmt batch_fold_fmt(const tbe_engine *e, uint64_t n) {
+    FoldFmt G{};
+    if (!e->foldrec) return G;
+    const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
+    const int pw = std::max(1, ceil_log2(n));
+    const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
+    if (tw >= (approx ? 1 : 8)) {   // (the approximate kind's records carry no time)
+        G.on = 1;
+        G.rb = e->r_bits;
+        G.pb = e->pf.pb;
+        G.pw = pw;
+        G.tw = tw;
+        G.nb = e->nbuckets;
+        G.region_bits = (uint32_t)(kDigitBits * (e->passes - 1));
+        G.n_hi = (uint32_t)(((uint64_t)e->nbuckets + (1ull << G.region_bits) - 1) >> G.region_bits);
+    }
+    return G;
+}
+
 // Enqueue the whole pipeline for one device-resident batch.  `caller` is the stream the
 // inputs were produced on and the replies are awaited on; NULL: the inputs are complete
 // at the call and the replies are ordered on the engine's stream.
@@ -4124,23 +4146,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
-    // fold records for this batch: the reply position takes ceil_log2(n) bits, the time
-    // offset what is left (>= 8 bits, else the plain records)
-    FoldFmt G{};
-    if (e->foldrec) {
-        const int pw = std::max(1, ceil_log2(n));
-        const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
-        if (tw >= (approx ? 1 : 8)) {   // (the approximate kind's records carry no time)
-            G.on = 1;
-            G.rb = e->r_bits;
-            G.pb = e->pf.pb;
-            G.pw = pw;
-            G.tw = tw;
-            G.nb = e->nbuckets;
-            G.region_bits = (uint32_t)(kDigitBits * (e->passes - 1));
-            G.n_hi = (uint32_t)(((uint64_t)e->nbuckets + (1ull << G.region_bits) - 1) >> G.region_bits);
-        }
-    }
+    const FoldFmt G = batch_fold_fmt(e, n);
     const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
     const bool unrank = e->unrank;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
@@ -5288,15 +5294,25 @@ tbe_status tbe_approx_collect(tbe_engine *e, int32_t *d_counts, void *stream) {
 }
 
 static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
-                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted);
+                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted,
+                              hipStream_t producer = nullptr);
 tbe_status tbe_approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
                            uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted) {
     if (!e || !d_all_counts || !n_granted) return TBE_EINVAL;
     return approx_sync(e, d_all_counts, n_clients, my_client, ts_us, stagger_us, n_granted);
 }
-// d_all_counts == nullptr: a single client whose collect runs inside the sync kernel
+tbe_status tbe_approx_sync_stream(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
+                                  uint32_t my_client, int64_t ts_us, int64_t stagger_us, void *stream,
+                                  uint64_t *n_granted) {
+    if (!e || !d_all_counts || !n_granted) return TBE_EINVAL;
+    return approx_sync(e, d_all_counts, n_clients, my_client, ts_us, stagger_us, n_granted, (hipStream_t)stream);
+}
+// d_all_counts == nullptr: a single client whose collect runs inside the sync kernel.
+// producer != nullptr: the counts are written by work enqueued on that stream (e.g. the
+// collective that exchanged them); the sync kernel is ordered after it by an event.
 static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32_t n_clients,
-                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted) {
+                              uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted,
+                              hipStream_t producer) {
     if (!e || !n_granted) return TBE_EINVAL;
     if (e->cfg.kind != TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not an approximate engine");
     if (n_clients == 0 || my_client >= n_clients || ts_us < 0 || stagger_us < 0)
@@ -5304,6 +5320,10 @@ static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32
     *n_granted = 0;
     e->drained.clear();
     HIP_TRY(e, hipSetDevice(e->device));
+    if (producer && producer != e->stream) {
+        HIP_TRY(e, hipEventRecord(e->ev_in, producer));
+        HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev_in, 0));
+    }
     {
         tbe_status qrc = sync_queued(e);
         if (qrc != TBE_OK) return qrc;
@@ -5585,6 +5605,20 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
               (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
               (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u);
+    return TBE_OK;
+}
+
+tbe_status tbe_batch_format(const tbe_engine *e, uint64_t n, uint32_t *out, uint32_t n_out) {
+    if (!e || !out || n_out < 8) return TBE_EINVAL;
+    const FoldFmt G = batch_fold_fmt(e, n);
+    out[0] = (uint32_t)e->passes;
+    out[1] = (uint32_t)G.on;
+    out[2] = (uint32_t)G.pw;                       // reply-position bits of a fold record
+    out[3] = (uint32_t)G.tw;                       // time-offset bits of a fold record
+    out[4] = (uint32_t)e->pf.kb;                   // pass-0 record: key bits
+    out[5] = (uint32_t)e->pf.pb;                   // permit-code bits
+    out[6] = (uint32_t)e->pf.wb;                   // pass-0 time-offset bits
+    out[7] = (uint32_t)e->r_bits;
     return TBE_OK;
 }
 

@@ -185,6 +185,14 @@ class TokenBucketEngine:
                 "medium": bool(c.value & 16), "fold_records": bool(c.value & 32),
                 "digit_stream": bool(c.value & 64), "rerank": bool(c.value & 128)}
 
+    def batch_format(self, n: int) -> dict:
+        """The record layout a batch of n requests takes (tbe_batch_format)."""
+        out = (c_uint32 * 8)()
+        self._check(self._lib.tbe_batch_format(self.handle, n, out, 8))
+        names = ("passes", "fold_records", "position_bits", "fold_time_bits", "key_bits", "permit_bits",
+                 "pass0_time_bits", "r_bits")
+        return {k: (bool(out[i]) if k == "fold_records" else out[i]) for i, k in enumerate(names)}
+
     def stage_times(self) -> dict:
         out = (c_double * len(_capi.STAGES))()
         nw = c_uint32()
@@ -374,11 +382,19 @@ class ApproximateEngine(QueueingTokenBucketEngine):
         """Local scores of every key into the int32 device tensor `d_counts` [n_keys]."""
         self._check(self._lib.tbe_approx_collect(self.handle, d_counts.data_ptr(), None))
 
-    def sync(self, d_all_counts, n_clients: int, my_client: int, ts_us: int, stagger_us: int):
-        """Replay the epoch's sync calls; returns the drain log (keys, request ids, available)."""
+    def sync(self, d_all_counts, n_clients: int, my_client: int, ts_us: int, stagger_us: int,
+             stream: Optional[int] = None):
+        """Replay the epoch's sync calls; returns the drain log (keys, request ids, available).
+        stream=None: d_all_counts must be complete at the call (tbe_approx_sync); a stream
+        handle: the replay is ordered after the work enqueued on that stream so far
+        (tbe_approx_sync_stream), e.g. the collective or copy that produced the counts."""
         n = ctypes.c_uint64()
-        self._check(self._lib.tbe_approx_sync(self.handle, d_all_counts.data_ptr(), n_clients, my_client,
-                                              ts_us, stagger_us, byref(n)))
+        if stream is None:
+            self._check(self._lib.tbe_approx_sync(self.handle, d_all_counts.data_ptr(), n_clients, my_client,
+                                                  ts_us, stagger_us, byref(n)))
+        else:
+            self._check(self._lib.tbe_approx_sync_stream(self.handle, d_all_counts.data_ptr(), n_clients,
+                                                         my_client, ts_us, stagger_us, stream, byref(n)))
         return self._drain_log(n.value)
 
     def refresh(self, ts_us: int):

@@ -313,9 +313,22 @@ tbe_status tbe_approx_collect(tbe_engine *engine, int32_t *d_counts, void *strea
  * (device memory, n_clients * n_keys int32), keep client `my_client`'s reply (global
  * score, period via "%.14g" -> est), then drain the queues; fetch the completed queued
  * requests with tbe_refresh_log.  n_clients = 1 with summed counts makes the node one
- * client (an all-reduce instead of an all-gather). */
+ * client (an all-reduce instead of an all-gather).
+ * Completion contract: the kernel runs on the engine's stream, ordered after the engine's
+ * own earlier batches but after NO other stream, so d_all_counts must be complete when
+ * this is called (e.g. the producer stream synchronised).  A caller whose counts come from
+ * work still in flight on another stream (an RCCL all-gather, torch.cat on a side stream)
+ * uses tbe_approx_sync_stream.  Returns when the replay and the drain log are done. */
 tbe_status tbe_approx_sync(tbe_engine *engine, const int32_t *d_all_counts, uint32_t n_clients,
                            uint32_t my_client, int64_t ts_us, int64_t stagger_us, uint64_t *n_granted);
+
+/* tbe_approx_sync ordered after `stream` (a hipStream_t; NULL = tbe_approx_sync): the
+ * engine records an event on it and its stream waits for that event before the replay
+ * reads d_all_counts, so the counts may still be being produced on `stream` at the call
+ * (A:439).  No host synchronisation of `stream` is needed. */
+tbe_status tbe_approx_sync_stream(tbe_engine *engine, const int32_t *d_all_counts, uint32_t n_clients,
+                                  uint32_t my_client, int64_t ts_us, int64_t stagger_us, void *stream,
+                                  uint64_t *n_granted);
 
 /* RefreshAsync of a limiter that is the only client of its global tier (A:412-508): the
  * same as tbe_approx_collect followed by tbe_approx_sync with n_clients = 1, as one kernel
@@ -355,6 +368,14 @@ tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t 
  * bit 7 set when the final un-partition re-ranks pass 0's tiles (TBE_FLAG_RERANK sets
  * it). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
+
+/* The record layout a batch of n requests takes (diagnostics and tests):
+ * out[0] partition passes, out[1] 1 if the last pass writes fold records, out[2] their
+ * reply-position bits (ceil_log2 n), out[3] their time-offset bits, out[4] the pass-0
+ * record's key bits, out[5] permit-code bits, out[6] pass-0 time-offset bits, out[7]
+ * r_bits.  n_out must be >= 8.  A request whose time offset does not fit takes the
+ * escape form (its time is read from the previous record / the caller's array). */
+tbe_status tbe_batch_format(const tbe_engine *engine, uint64_t n, uint32_t *out, uint32_t n_out);
 
 /* Per-stage device time (ms) accumulated since the last call, when
  * TBE_FLAG_STAGE_TIMING is set: out[0..n_out) = {hist, colscan, scatter, bounds,

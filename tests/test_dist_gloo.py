@@ -63,6 +63,23 @@ def test_route_batch_matches_serial_reference(oracle_lib, tmp_path, map_kind):
     check_tb_route([np.load(tmp_path / f"tb_{r}.npz") for r in range(WORLD)])
 
 
+def test_owner_map_validation():
+    """a map that is not 4096 u8 owners below the world size is refused before
+    any kernel reads it (route_requests / route_batch / route_cancel call key_owner or
+    _device_map first)."""
+    from distributedratelimiting.redis_amd import cluster
+    keys = np.arange(1000, dtype=np.uint64)
+    good = cluster.hash_owner_map(4)
+    assert np.array_equal(cluster.key_owner(keys, 4, good), cluster.key_owner(keys, 4))
+    for bad in (good[:100], np.concatenate([good, good]), np.full(4096, 4, np.uint8),
+                np.full(4096, -1, np.int64), np.full(4096, 300, np.int64)):
+        with pytest.raises(ValueError):
+            cluster.key_owner(keys, 4, bad)
+        with pytest.raises(ValueError):
+            cluster._device_map(bad, None, 4)
+    assert cluster._device_map(None, None, 4) is None
+
+
 def test_owner_maps():
     """Table-driven ownership (include/tbe_cluster.h owner maps): the hash map reproduces
     the hash partition; the balanced map evens out a Zipf stream's owner loads that the

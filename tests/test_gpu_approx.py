@@ -82,6 +82,48 @@ def test_clients_epochs(engine_lib, gpu, n_clients, order, qlimit, wait, pack, l
                 assert (lo, gl, est, av, q) == (s.local, s.global_, s.est, clients[r].available(s), len(s.queue))
 
 
+def test_sync_stream_orders_after_producer(engine_lib, gpu):
+    """tbe_approx_sync_stream orders the replay after the stream that
+    produces the exchanged counts.  Here the counts are concatenated by torch.cat on a side
+    stream behind a long spin, with no host synchronisation before the call; the replay
+    must equal that of twin engines whose counts were complete at the call (A:439)."""
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    n_keys, n, clients = 200_000, 1 << 20, 3
+    rng = np.random.default_rng(11)
+    twins = [[ApproximateEngine(n_keys, 20, 10, 10_000_000, 4, 0, device=0) for _ in range(clients)]
+             for _ in range(2)]
+    counts = [[torch.zeros(n_keys, dtype=torch.int32, device=gpu) for _ in range(clients)] for _ in range(2)]
+    side = torch.cuda.Stream(gpu)
+    for epoch in range(3):
+        batches = [rng.integers(0, n_keys, n).astype(np.uint64) for _ in range(clients)]
+        for engs in twins:
+            for r in range(clients):
+                engs[r].acquire_batch(batches[r], np.ones(n, np.int32), wait=True, id_base=epoch * n)
+        ts = S_US + epoch * 1_000_000
+        for engs, cs in zip(twins, counts):
+            for r in range(clients):
+                engs[r].collect(cs[r])
+        torch.cuda.synchronize()
+        ref_all = torch.cat(counts[1])
+        torch.cuda.synchronize()
+        want = [twins[1][r].sync(ref_all, clients, r, ts, 1000) for r in range(clients)]
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(200_000_000)              # the producer is still busy at the call
+            allc = torch.cat(counts[0])
+        got = [twins[0][r].sync(allc, clients, r, ts, 1000, stream=side.cuda_stream) for r in range(clients)]
+        for g, w in zip(got, want):
+            for a, b in zip(g, w):
+                assert np.array_equal(a, b)
+        for key in range(0, n_keys, 997):
+            for r in range(clients):
+                assert twins[0][r].local_state(key) == twins[1][r].local_state(key)
+        side.synchronize()
+    a, b = twins[0][0].export_global(), twins[1][0].export_global()
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+
+
 GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
                                     "golden")
 

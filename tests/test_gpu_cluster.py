@@ -92,6 +92,35 @@ def test_route_plan_owner_map_matches_host(engine_lib, gpu, n_owners, n):
         assert np.array_equal(counts.cpu().numpy(), np.bincount(owner, minlength=n_owners))
 
 
+def test_route_plan_bad_owner_map_is_bounds_safe(engine_lib, gpu):
+    """a device owner map with entries >= n_owners is clamped to n_owners - 1 in
+    the route kernels (include/tbe_cluster.h), so every position stays inside [0, n) and
+    every count inside the n_owners array -- never an out-of-bounds write."""
+    import torch
+    from distributedratelimiting.redis_amd import _capi, cluster
+    lib = _capi.load()
+    n, n_owners = 100_000, 4
+    k = _keys(n, 77, hot=0.1)
+    dk = torch.from_numpy(k.view(np.int64)).to(gpu)
+    bad = np.full(cluster.OWNER_MAP_SIZE, 200, dtype=np.uint8)
+    bad[::3] = 1
+    dmap = torch.from_numpy(bad).to(gpu)
+    pos = torch.empty(n, dtype=torch.int32, device=gpu)
+    counts = torch.zeros(n_owners + 8, dtype=torch.int64, device=gpu)   # guard words past n_owners
+    work = torch.empty(lib.tbe_route_workspace_bytes(n, n_owners), dtype=torch.uint8, device=gpu)
+    assert lib.tbe_route_plan_map_device(dk.data_ptr(), n, n_owners, dmap.data_ptr(), work.data_ptr(),
+                                         pos.data_ptr(), counts.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    clamped = np.minimum(bad, n_owners - 1)
+    owner = cluster.key_owner(k, n_owners, clamped)
+    order = np.argsort(owner, kind="stable")
+    want = np.empty(n, dtype=np.int64)
+    want[order] = np.arange(n)
+    assert np.array_equal(pos.cpu().numpy().astype(np.int64), want)
+    c = counts.cpu().numpy()
+    assert np.array_equal(c[:n_owners], np.bincount(owner, minlength=n_owners)) and not c[n_owners:].any()
+
+
 def test_directory_matches_host(engine_lib, gpu):
     import torch
     with torch.cuda.stream(torch.cuda.Stream(gpu)):   # the device path needs a real stream

@@ -183,7 +183,6 @@ VARIANT_SETS = {
     },
     "wipE": {
         "base_a": ([], ["--workload", "approx"]),
-        "fused_a": ([], ["--workload", "approx"], "wip_fused_refresh.patch"),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "nomemset_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"], "wip_no_memsets.patch"),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
