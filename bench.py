@@ -103,7 +103,7 @@ def parse():
     ap.add_argument("--no-narrow", action="store_true",
                     help="4-byte replies even where TokenLimit <= 127 allows 1-byte ones (A/B)")
     ap.add_argument("--no-sparse", action="store_true",
-                    help="skip the sparse-batch leg (2^20-request batches over config B's keys)")
+                    help="skip the batch-size sweep (2^14 .. 2^26-request batches over config B's keys)")
     ap.add_argument("--no-strdir", action="store_true",
                     help="skip the string-key directory leg (config B batches as key text)")
     ap.add_argument("--unscatter-all", action="store_true",
@@ -500,12 +500,13 @@ def main():
     if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_strdir:
         strdir = bench_strdir(bufs[:6], keys_local, dev)
 
-    # a sparse batch on the same key space: 2^20 requests over 1e8 keys touch
-    # ~1% of the table's lines, so the fold gathers the rows of its sparse buckets
-    # (k_fold) instead of pulling every slice whole
-    sparse = None
+    # batch sizes 2^14 .. 2^26 on the same key space; "sparse_batch" is
+    # its 2^20 point (2^20 requests over 1e8 keys touch ~1% of the table's lines: the sparse
+    # buckets go one wave each to k_fold_sparse, which gathers only their rows)
+    sparse = sweep = None
     if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_sparse:
-        sparse = bench_sparse(args, lib, keys_local, dev)
+        sweep = bench_batch_sweep(args, lib, keys_local, dev)
+        sparse = next((x for x in sweep if x["batch"] == 1 << 20), None)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -549,6 +550,7 @@ def main():
                if host_rate_pinned is not None else {}),
             **({"string_directory": strdir} if strdir is not None else {}),
             **({"sparse_batch": sparse} if sparse is not None else {}),
+            **({"batch_sweep": sweep} if sweep is not None else {}),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}
@@ -562,42 +564,65 @@ def main():
         td.destroy_process_group()
 
 
-def bench_sparse(args, lib, n_keys: int, dev, n: int = 1 << 20, warm: int = 3, timed: int = 10):
-    """Batches of `n` requests (config B's trace shape, keys uniform over the same key
-    space) on a fresh engine, after the timed region: HIP-event stage times per batch.
-    Shows the fold's density gate (fold_wide_min): the sparse buckets' rows are gathered,
-    not their whole slices."""
+SWEEP_LOG2 = (14, 16, 18, 20, 22, 24, 26)
+
+
+def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
+    """Config B's key space at batch sizes 2^14 .. 2^26 (the regime of
+    the host's micro-batching submitter, SURVEY §8(b) threading), after the timed region.
+    Per size a fresh engine (pipeline off, one stream) decides warm-up + timed batches of
+    uniform keys; reported: decisions/s over the back-to-back timed batches, the per-batch
+    latency (enqueue one batch + synchronise, wall clock, median of 5), and HIP-event stage
+    times.  Sparse batches (below R/32 requests per bucket on average: up to 2^21 here) send
+    their sparse buckets to k_fold_sparse, one wave each; from 2^22 every bucket takes
+    k_fold_wide."""
     from distributedratelimiting.redis_amd import TokenBucketEngine
-    eng = TokenBucketEngine(n_keys, args.token_limit, args.tokens_per_period, args.period_ticks,
-                            device=dev.index, stage_timing=True, max_batch=n, pipeline=False)
+    out = []
     gen_stream = torch.cuda.current_stream(dev).cuda_stream or None
-    bufs = []
-    for s in range(warm + timed):
-        k = torch.empty(n, dtype=torch.int64, device=dev)
-        p = torch.empty(n, dtype=torch.int32, device=dev)
-        t = torch.empty(n, dtype=torch.int64, device=dev)
-        assert lib.tbe_gen_batch_device(SEED_B ^ 0x5A, n_keys, s * n, n, 1, 1, T0_US + s * args.interval_us,
-                                        args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(), gen_stream) == 0
-        bufs.append((k, p, t))
-    g = torch.empty(n, dtype=torch.uint8, device=dev)
-    r = torch.empty(n, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
-    for s in range(warm):
-        eng.acquire_batch_device(*bufs[s], g, r)
-    eng.synchronize()
-    eng.stage_times()
-    t0 = time.perf_counter()
-    for s in range(warm, warm + timed):
-        eng.acquire_batch_device(*bufs[s], g, r)
-    eng.synchronize()
-    elapsed = time.perf_counter() - t0
-    st = eng.stage_times()
-    eng.close()
-    return {"batch": n, "batches_timed": timed, "ms_per_batch": round(elapsed / timed * 1e3, 4),
-            "decisions_per_s": round(n * timed / elapsed, 1),
-            "stage_ms_per_batch": {k: round(v / timed, 4) for k, v in st.items()},
-            "note": f"2^{n.bit_length() - 1} uniform requests over the same {n_keys} keys on a fresh engine, "
-                    "one stream; buckets below R/8 requests take the sparse fold (k_fold: touched rows only)"}
+    for lg in sizes:
+        n = 1 << lg
+        warm, timed = (3, 10) if lg <= 22 else (2, 5)
+        eng = TokenBucketEngine(n_keys, args.token_limit, args.tokens_per_period, args.period_ticks,
+                                device=dev.index, stage_timing=True, max_batch=n, pipeline=False)
+        bufs = []
+        for s in range(warm + timed + 5):
+            k = torch.empty(n, dtype=torch.int64, device=dev)
+            p = torch.empty(n, dtype=torch.int32, device=dev)
+            t = torch.empty(n, dtype=torch.int64, device=dev)
+            assert lib.tbe_gen_batch_device(SEED_B ^ 0x5A, n_keys, s * n, n, 1, 1, T0_US + s * args.interval_us,
+                                            args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(),
+                                            gen_stream) == 0
+            bufs.append((k, p, t))
+        g = torch.empty(n, dtype=torch.uint8, device=dev)
+        r = torch.empty(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        for s in range(warm):
+            eng.acquire_batch_device(*bufs[s], g, r)
+        eng.synchronize()
+        eng.stage_times()
+        t0 = time.perf_counter()
+        for s in range(warm, warm + timed):
+            eng.acquire_batch_device(*bufs[s], g, r)
+        eng.synchronize()
+        elapsed = time.perf_counter() - t0
+        st = eng.stage_times()
+        lat = []
+        for s in range(warm + timed, warm + timed + 5):
+            t1 = time.perf_counter()
+            eng.acquire_batch_device(*bufs[s], g, r)
+            eng.synchronize()
+            lat.append(time.perf_counter() - t1)
+        eng.stage_times()
+        eng.close()
+        del bufs
+        out.append({"batch": n, "batches_timed": timed, "ms_per_batch": round(elapsed / timed * 1e3, 4),
+                    "decisions_per_s": round(n * timed / elapsed, 1),
+                    "latency_ms": round(float(np.median(lat)) * 1e3, 4),
+                    "stage_ms_per_batch": {k: round(v / timed, 4) for k, v in st.items()},
+                    "fold": ("k_fold_sparse (one wave per sparse bucket) + k_fold_wide (listed dense buckets)"
+                             if n < (-(-n_keys // 2048)) * 64 else "k_fold_wide (every bucket)")})
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_strdir(batches, n_keys: int, dev):

@@ -494,6 +494,10 @@ def run_approx(args, lib, dev, world, rank, dist):
     refresh_ms = {m: round(v[0] / v[1] * 1e3, 4) if v[1] else None for m, v in refresh_s.items()}
     if dist:
         refresh_ms = {m: round(reduce_max(v, dev), 4) if v is not None else None for m, v in refresh_ms.items()}
+    # config E's 8-GPU refresh on this one GPU: the all-gather layout of
+    # 8 clients' counts -- 8 consecutive batches' collected local scores stand in for the 8
+    # ranks' -- and the client-ordered replay of 8 sync calls per key with staggered times
+    eight = approx_eight_clients(args, eng, bufs, st, av, kshared, n, total + 5, dev) if not dist else None
     # bytes each GPU receives per refresh: ring all-reduce 2 (N-1)/N * 4K, all-gather (N-1) * 4K
     xbytes = {"node": int(2 * (world - 1) * kshared * 4 // world), "clients": int((world - 1) * kshared * 4)}
 
@@ -541,6 +545,7 @@ def run_approx(args, lib, dev, world, rank, dist):
                                        f"{min(steps, 5)} epochs after the timed region"}
                           for m in ("node", "clients")},
         "roofline": _roofline(name, alg, ms, note, "approx", fp),
+        **({"eight_client_refresh": eight} if eight is not None else {}),
         "cpu_baseline": None,
     }
     # SURVEY.md §8(d) config E, whole step: 8+4+1 in/out + 8 local-tier state per decision,
@@ -550,6 +555,38 @@ def run_approx(args, lib, dev, world, rank, dist):
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_approx(args, kshared)
     return line
+
+
+def approx_eight_clients(args, eng, bufs, st, av, kshared, n, s0, dev, clients: int = 8, epochs: int = 5):
+    """The refresh epoch an 8-GPU node runs in config E's clients mode (§8e option 2), on one
+    GPU: the counts of `clients` consecutive batches of this engine (each collected after its
+    batch: one client's local scores) laid out as RCCL's all-gather lays them out, then
+    tbe_approx_sync with n_clients = 8 -- every key's sync script replayed 8 times in client
+    order at T + r * P/8 (A:241-270) on this rank's replica.  Wall time per epoch (one engine
+    call, synchronous) and the kernel's algorithmic bytes: per key 4 B per client count +
+    local tier and client view read/written (16 + 16) + the global tier v, p, t read and
+    written (48) = 80 + 4N B, over the bytes the one-client fused refresh moves."""
+    allc = torch.empty(clients * kshared, dtype=torch.int32, device=dev)
+    for r in range(clients):
+        k, p = bufs[r % len(bufs)]
+        eng.acquire_batch_device(k, p, st, av, wait=False, id_base=(s0 + r) * n)
+        eng.collect(allc[r * kshared:(r + 1) * kshared])
+    torch.cuda.synchronize()
+    period_us = args.period_ticks // 10
+    stagger = period_us // clients
+    wall = []
+    for j in range(epochs):
+        ts = T0_US + (s0 + clients + j) * args.interval_us
+        t1 = time.perf_counter()
+        eng.sync(allc, clients, 0, ts, stagger)
+        wall.append(time.perf_counter() - t1)
+    ms = float(np.median(wall)) * 1e3
+    alg = kshared * (80 + 4 * clients)
+    return {"clients": clients, "epochs_timed": epochs, "ms_per_epoch_wall": round(ms, 4),
+            "alg_bytes": alg, "alg_note": f"K_shared * (80 + 4 * {clients}) B",
+            "achieved_GBs_wall": round(alg / (ms * 1e-3) / 1e9, 1),
+            "counts": f"{clients} consecutive config-E batches' collected local scores, all-gather layout",
+            "stagger_us": stagger}
 
 
 def cpu_approx(args, kshared):

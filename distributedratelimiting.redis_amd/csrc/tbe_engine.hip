@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -535,6 +536,175 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
     }
 }
 
+// k_hist_dig's work with one WAVE per tile and one barrier per block (round 5).  k_hist_dig
+// walks its block's tiles one after another, three barriers and one memory round trip per
+// tile: 63 us per config-B batch for 64 MB of digits, latency-bound.  Here every wave
+// issues the loads of all its tiles at once (lane l reads 16-byte pieces of the tile), counts
+// each tile into its own LDS histogram (wave-private, no barrier), and one barrier later
+// the 256 digit-owner threads turn the block's tile histograms into the running prefixes
+// (tileprefix), the block's totals and the per-bucket counts.  A tile inside one pass-0
+// digit (the common case: pass 0's output is sorted by it) adds its histogram to the
+// buckets (d1 << 8) | d0 through the digit owners' running sums; a tile that straddles pass-0
+// digits is counted per pass-0 segment by its wave (global atomics).
+#ifndef TBE_HIST_DIG_WAVE
+#define TBE_HIST_DIG_WAVE 0                  // A/B: 0.077 against 0.063 ms for k_hist_dig (profiles/r05e_*)
+#endif
+typedef uint32_t dg4_t __attribute__((ext_vector_type(4)));   // 16 digit bytes
+constexpr int kDigWTiles = 32;                       // tiles per block per round (LDS: 32 KB of histograms)
+constexpr int kDigWPer = kDigWTiles / (kHBlock / 64);   // tiles per wave per round
+__global__ __launch_bounds__(kHBlock, 4) void k_hist_dig_w(
+    const uint8_t *__restrict__ dig, uint64_t n, uint32_t tiles_per_blk, uint32_t ntiles,
+    uint32_t *__restrict__ tileprefix, uint32_t *__restrict__ blocksum,
+    const uint32_t *__restrict__ dtot0, uint32_t *__restrict__ bcount, uint32_t nbt) {
+    __shared__ uint32_t th[kDigWTiles][kDigits];
+    __shared__ uint32_t dstart[kDigits + 1];
+    __shared__ uint32_t wsum[kHBlock / 64];
+    __shared__ uint32_t tlo[kDigWTiles];             // a tile's pass-0 digit, or 0xFFFFFFFF if it straddles
+    __shared__ uint32_t seg1[kHBlock / 64][kDigits]; // per wave: a straddling tile's first pass-0 segment
+    static_assert(kDigWPer * (kHBlock / 64) == kDigWTiles && kTile == 4096, "16-byte pieces: 4 per lane per tile");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool own = tid < kDigits;
+    {
+        uint32_t all;
+        const uint32_t pre = block_excl_scan<kHBlock>(own ? dtot0[tid] : 0u, wsum, &all);
+        if (own) dstart[tid] = pre;
+        if (tid == 0) dstart[kDigits] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    auto d0_of = [&](uint32_t i) {
+        uint32_t lo = 0, hi = kDigits;               // dstart[lo] <= i < dstart[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (dstart[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint32_t t0 = blockIdx.x * tiles_per_blk;
+    const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
+    uint32_t run = 0, acc = 0, acc_lo = 0;
+    // one tile's 4096 digits as 4 x 16 bytes per lane (lane l: bytes q*1024 + l*16 .. +16)
+    auto load_tile = [&](uint32_t t, dg4_t (&v)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            v[q] = dg4_t{0u, 0u, 0u, 0u};
+            const uint64_t i = (uint64_t)t * kTile + (uint64_t)q * 1024 + (uint64_t)lane * 16;
+            if (t < t1 && i < n) {
+                if (i + 16 <= n) {
+                    v[q] = LD_P(reinterpret_cast<const dg4_t *>(dig + i));
+                } else {
+#pragma unroll
+                    for (int x = 0; x < 16; ++x)
+                        if (i + x < n) v[q][x >> 2] |= (uint32_t)dig[i + x] << (8 * (x & 3));
+                }
+            }
+        }
+    };
+    for (uint32_t r0 = t0; r0 < t1; r0 += kDigWTiles) {
+        const uint32_t nt = min<uint32_t>(kDigWTiles, t1 - r0);
+        // this wave's tiles r0 + w * kDigWPer + u, the next one's loads in flight while one is counted
+        dg4_t v[4], vn[4];
+        load_tile(r0 + (uint32_t)(w * kDigWPer), vn);
+        for (int u = 0; u < kDigWPer; ++u) {
+            const uint32_t li = (uint32_t)(w * kDigWPer + u);
+            if (li >= nt) break;                     // wave-uniform
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = vn[q];
+            if (u + 1 < kDigWPer && li + 1 < nt) load_tile(r0 + li + 1, vn);
+            uint32_t *h = th[li];
+            uint32_t *s1 = seg1[w];
+            const uint64_t base = (uint64_t)(r0 + li) * kTile;
+            const uint32_t cnt = (uint32_t)min<uint64_t>(kTile, n - base);
+            const uint32_t lo0 = d0_of((uint32_t)base), lo1 = d0_of((uint32_t)(base + cnt - 1));
+            // two pass-0 segments (the usual straddle): count the first apart, the second is
+            // the rest; more (sparse batches: small pass-0 digits): each request on its own
+            const uint32_t split = (lo1 == lo0 + 1) ? dstart[lo1] - (uint32_t)base : 0u;
+#pragma unroll
+            for (int x = 0; x < kDigits / 64; ++x) {
+                h[x * 64 + lane] = 0;
+                s1[x * 64 + lane] = 0;
+            }
+            if (lane == 0) tlo[li] = (lo0 == lo1) ? lo0 : 0xFFFFFFFFu;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // runs of one digit in this lane's 16 consecutive requests take one atomic
+                // (a hot key's tiles are nearly all one digit)
+                const uint32_t off0 = (uint32_t)q * 1024 + (uint32_t)lane * 16;
+                uint32_t rd = 0xFFFFFFFFu, rc = 0;
+#pragma unroll
+                for (int bt = 0; bt < 16; ++bt) {
+                    const uint32_t d = (v[q][bt >> 2] >> (8 * (bt & 3))) & (kDigits - 1);
+                    if (off0 + bt < cnt) {
+                        if (d != rd) {
+                            if (rc) atomicAdd(&h[rd], rc);
+                            rd = d;
+                            rc = 0;
+                        }
+                        ++rc;
+                    }
+                }
+                if (rc) atomicAdd(&h[rd], rc);
+            }
+            if (lo1 != lo0) {
+                // a tile across pass-0 digits (rare in dense batches: <= 255 of them)
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t off0 = (uint32_t)q * 1024 + (uint32_t)lane * 16;
+                    for (int bt = 0; bt < 16; ++bt) {
+                        const uint32_t off = off0 + bt;
+                        if (off >= cnt) break;
+                        const uint32_t d = (v[q][bt >> 2] >> (8 * (bt & 3))) & (kDigits - 1);
+                        if (split != 0u) {
+                            if (off < split) atomicAdd(&s1[d], 1u);
+                        } else {
+                            const uint32_t pos = (uint32_t)(base + off);
+                            uint32_t lo = lo0;
+                            while (dstart[lo + 1] <= pos) ++lo;
+                            const uint32_t bk = (d << kDigitBits) | lo;
+                            if (bk < nbt) atomicAdd(&bcount[bk], 1u);
+                        }
+                    }
+                }
+            }
+            if (lo1 == lo0 + 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+                for (int x = 0; x < kDigits / 64; ++x) {
+                    const uint32_t d = (uint32_t)(x * 64 + lane);
+                    const uint32_t a = s1[d], b = h[d] - a;
+                    const uint32_t bk0 = (d << kDigitBits) | lo0, bk1 = (d << kDigitBits) | lo1;
+                    if (a && bk0 < nbt) atomicAdd(&bcount[bk0], a);
+                    if (b && bk1 < nbt) atomicAdd(&bcount[bk1], b);
+                }
+            }
+        }
+        __syncthreads();                              // every tile histogram of the round
+        if (own) {
+            for (uint32_t li = 0; li < nt; ++li) {
+                const uint32_t c = th[li][tid];
+                tileprefix[(uint64_t)(r0 + li) * kDigits + tid] = run;
+                run += c;
+                const uint32_t lo = tlo[li];
+                if (lo != 0xFFFFFFFFu) {
+                    if (lo != acc_lo) {
+                        const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
+                        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+                        acc = 0;
+                        acc_lo = lo;
+                    }
+                    acc += c;
+                }
+            }
+        }
+        __syncthreads();                              // th[] and tlo[] are free for the next round
+    }
+    if (own) {
+        const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
+        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
+        blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
+    }
+}
+
 // Digit-column scan, one workgroup per digit d: blockprefix[j][d] = number of digit-d
 // elements in blocks < j; digit_total[d] = all of them.  The digit bases (exclusive scan
 // of digit_total) are formed by each consumer workgroup itself.
@@ -689,10 +859,19 @@ __global__ __launch_bounds__(kPartBlock) void k_scatter(
 // a coalesced load into LDS, each thread scans its 16 consecutive counts, one block
 // scan of the thread sums, and a coalesced store back through LDS.
 constexpr int kScanPer = 16;
+// dlist (sparse batches): dlist[0] = the number of ordinary buckets (< nb) with at least
+// wide_min requests, dlist[1..] their ids (any order): k_fold_wide's whole grid then walks
+// only those, and k_fold_sparse takes the rest.
 __global__ __launch_bounds__(1024) void k_bscan(const uint32_t *__restrict__ bcount, uint32_t nbt,
-                                                uint32_t *__restrict__ bstart) {
-    __shared__ uint32_t tile[1024 * kScanPer];
+                                                uint32_t *__restrict__ bstart, uint32_t nb = 0,
+                                                uint32_t wide_min = 0, uint32_t *__restrict__ dlist = nullptr) {
+    // row-major [1024][kScanPer] padded to kScanPer + 1 words per thread: a thread's 16
+    // consecutive counts no longer sit 16 words apart from its neighbours' (bank conflicts)
+    __shared__ uint32_t tile[1024 * (kScanPer + 1)];
+    auto pad = [](uint32_t j) { return (j / kScanPer) * (kScanPer + 1) + (j % kScanPer); };
     __shared__ uint32_t wsum[16];
+    __shared__ uint32_t n_dense;
+    if (threadIdx.x == 0) n_dense = 0;
     const uint32_t t = threadIdx.x;
     constexpr uint32_t kRow = 1024 * kScanPer;
     constexpr int kGroup = 4;   // rows whose loads are all issued before the first is scanned
@@ -711,32 +890,98 @@ __global__ __launch_bounds__(1024) void k_bscan(const uint32_t *__restrict__ bco
             const uint32_t r0 = g0 + r * kRow;
             if (r0 >= nbt) break;                      // uniform across the block
 #pragma unroll
-            for (int k = 0; k < kScanPer; ++k) tile[k * 1024 + t] = ld[r][k];
+            for (int k = 0; k < kScanPer; ++k) tile[pad(k * 1024 + t)] = ld[r][k];
             __syncthreads();
             uint32_t v[kScanPer], sum = 0;
 #pragma unroll
             for (int k = 0; k < kScanPer; ++k) {
-                v[k] = tile[t * kScanPer + k];
+                v[k] = tile[t * (kScanPer + 1) + k];
                 sum += v[k];
+            }
+            if (dlist) {
+#pragma unroll
+                for (int k = 0; k < kScanPer; ++k) {
+                    const uint32_t bk = r0 + t * kScanPer + k;
+                    if (bk < nb && v[k] >= wide_min) dlist[1 + atomicAdd(&n_dense, 1u)] = bk;
+                }
             }
             uint32_t total;
             uint32_t pre = carry + block_excl_scan<1024>(sum, wsum, &total);
 #pragma unroll
             for (int k = 0; k < kScanPer; ++k) {
-                tile[t * kScanPer + k] = pre;
+                tile[t * (kScanPer + 1) + k] = pre;
                 pre += v[k];
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < kScanPer; ++k) {
                 const uint32_t j = r0 + k * 1024 + t;
-                if (j < nbt) bstart[j] = tile[k * 1024 + t];
+                if (j < nbt) bstart[j] = tile[pad(k * 1024 + t)];
             }
             carry += total;
             __syncthreads();
         }
     }
     if (t == 0) bstart[nbt] = carry;
+    if (dlist) {
+        __syncthreads();
+        if (t == 0) dlist[0] = n_dense;
+    }
+}
+
+// Bucket starts of a dense batch by decoupled look-back (round 5): k_bscan is one
+// workgroup walking ~50K counts (17-21 us per config-B batch, latency-bound).  Here each
+// 1024-thread workgroup scans 4096 consecutive counts, publishes its total tagged with the
+// batch number (flags[blk] = tag << 32 | total; no reset between batches), and one wave
+// sums the totals of every earlier workgroup once they are published.  Workgroups are
+// dispatched in index order, so an earlier one is always running or done: the wait ends.
+constexpr int kBsPer = 4;
+constexpr uint32_t kBsTile = 1024u * kBsPer;
+constexpr uint32_t kBsMaxBlocks = 64;        // nb_total <= 2^16 buckets (two 8-bit passes)
+__global__ __launch_bounds__(1024) void k_bscan_lb(const uint32_t *__restrict__ bcount, uint32_t nbt,
+                                                   uint32_t *__restrict__ bstart,
+                                                   unsigned long long *__restrict__ flags, uint32_t tag) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t excl;
+    const uint32_t t = threadIdx.x, blk = blockIdx.x;
+    const uint32_t b0 = blk * kBsTile + t * kBsPer;
+    uint32_t v[kBsPer];
+#pragma unroll
+    for (int k = 0; k < kBsPer; ++k) v[k] = (b0 + k < nbt) ? bcount[b0 + k] : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kBsPer; ++k) sum += v[k];
+    uint32_t total;
+    const uint32_t pre = block_excl_scan<1024>(sum, wsum, &total);
+    if (t == 0)
+        __hip_atomic_store(&flags[blk], ((unsigned long long)tag << 32) | total, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 64) {
+        uint32_t acc = 0;
+        for (uint32_t j0 = 0; j0 < blk; j0 += 64) {
+            const uint32_t j = j0 + t;
+            uint32_t val = 0;
+            if (j < blk) {
+                unsigned long long f;
+                do {
+                    f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                } while ((uint32_t)(f >> 32) != tag);
+                val = (uint32_t)f;
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
+            acc += val;
+        }
+        if (t == 0) excl = acc;
+    }
+    __syncthreads();
+    uint32_t run = excl + pre;
+#pragma unroll
+    for (int k = 0; k < kBsPer; ++k) {
+        if (b0 + k < nbt) bstart[b0 + k] = run;
+        run += v[k];
+    }
+    if (blk == gridDim.x - 1 && t == 0) bstart[nbt] = excl + total;
 }
 
 // Packed request records (token-bucket kind).  When the key, a permit code and a
@@ -760,7 +1005,31 @@ struct PackFmt {
     int32_t pb;
     int32_t pc_max;     // TokenLimit + 1
     int32_t wb;
+    // Narrow pass-0 records (round 5; token bucket, two passes, fold records, digit stream):
+    // pass 0 writes a u32 per request -- row within the bucket (rb bits), permit code,
+    // escape, ts - base0 (w0 = 32 - rb - pb - 1 bits, base0 = ts[0] - 2^(w0-1)) -- beside
+    // the one-byte digit stream that already carries the pass-1 digit; the pass-0 digit is
+    // the record's position.  An escaped request (time outside the window) also writes its
+    // timestamp to a side array at its pass-0 output position, where the fold finds it.
+    // 4 + 1 bytes instead of 8 + 1 written by pass 0 and read by pass 1.
+    int32_t n0;         // 1: pass 0 writes narrow records
+    int32_t rb;         // row bits (r_bits) of a narrow record
+    int32_t w0;         // time-offset bits of a narrow record
 };
+__device__ __forceinline__ int64_t pack_base32(const int64_t *__restrict__ ts, const PackFmt &F) {
+    return ts[0] - ((int64_t)1 << (F.w0 - 1));
+}
+// A narrow pass-0 record from the partition key (row = its low rb bits); *esc: the time did
+// not fit and goes to the side array.
+__device__ __forceinline__ uint32_t pack_rec32(uint32_t pkey, int32_t p, int64_t ts, int64_t tbase, const PackFmt &F,
+                                               bool &esc) {
+    const uint32_t pc = (uint32_t)(p < 0 ? 0 : (p > F.pc_max ? F.pc_max : p));
+    const uint64_t d = (uint64_t)ts - (uint64_t)tbase;
+    const bool fits = ts >= tbase && (d >> F.w0) == 0;
+    esc = !fits;
+    return (pkey & ((1u << F.rb) - 1u)) | (pc << F.rb) | ((uint32_t)!fits << (F.rb + F.pb)) |
+           (fits ? (uint32_t)d << (F.rb + F.pb + 1) : 0u);
+}
 __device__ __forceinline__ int64_t pack_base(const int64_t *__restrict__ ts, const PackFmt &F) {
     return ts[0] - ((int64_t)1 << (F.wb - 1));
 }
@@ -799,6 +1068,7 @@ __device__ __forceinline__ void unpack_rec(uint64_t rec, const int64_t *__restri
 // batch's first request; the batch spans 10 ms).  Used when tw >= 8.
 struct FoldFmt {
     int32_t on;
+    int32_t n0;             // pass 0 wrote narrow records: an escaped record's time is rec0[pos] itself
     int32_t rb, pb, pw, tw;
     uint32_t nb;            // ordinary buckets
     uint32_t region_bits;   // 8 * (passes - 1): buckets with equal low region_bits share a reply region
@@ -818,6 +1088,17 @@ __device__ __forceinline__ uint64_t fold_rec(uint64_t rec0, uint32_t pos, int64_
     return row | (pc << G.rb) | ((uint64_t)!fits << (G.rb + G.pb)) | ((uint64_t)pos << (G.rb + G.pb + 1)) |
            ((fits ? d : 0ull) << (G.rb + G.pb + 1 + G.pw));
 }
+__device__ __forceinline__ uint64_t fold_rec32(uint32_t r32, uint32_t pos, int64_t tbase0, int64_t tbase1,
+                                               const PackFmt &F, const FoldFmt &G) {
+    const uint64_t row = r32 & ((1u << F.rb) - 1u);
+    const uint64_t pc = (r32 >> F.rb) & ((1u << F.pb) - 1u);
+    const bool esc0 = (r32 >> (F.rb + F.pb)) & 1u;
+    const int64_t ts = (int64_t)((uint64_t)tbase0 + (uint64_t)(r32 >> (F.rb + F.pb + 1)));
+    const uint64_t d = (uint64_t)ts - (uint64_t)tbase1;
+    const bool fits = !esc0 && ts >= tbase1 && (d >> G.tw) == 0;
+    return row | (pc << G.rb) | ((uint64_t)!fits << (G.rb + G.pb)) | ((uint64_t)pos << (G.rb + G.pb + 1)) |
+           ((fits ? d : 0ull) << (G.rb + G.pb + 1 + G.pw));
+}
 // Decode a fold record: row, permit code, time (escaped: through the previous pass's
 // record `rec0[pos]`, itself possibly escaped to the caller's ts array) and reply position.
 __device__ __forceinline__ void unfold_rec(uint64_t rec, const FoldFmt &G, int64_t tbase1,
@@ -828,9 +1109,13 @@ __device__ __forceinline__ void unfold_rec(uint64_t rec, const FoldFmt &G, int64
     p = (int32_t)((rec >> G.rb) & ((1ull << G.pb) - 1));
     pos = (uint32_t)((rec >> (G.rb + G.pb + 1)) & ((1ull << G.pw) - 1));
     if ((rec >> (G.rb + G.pb)) & 1) {
-        uint32_t k;
-        int32_t p0;
-        unpack_rec(rec0[pos], ts_orig, tbase0, F, k, p0, ts);
+        if (G.n0) {
+            ts = (int64_t)rec0[pos];   // the side array of narrow pass-0 records' escaped times
+        } else {
+            uint32_t k;
+            int32_t p0;
+            unpack_rec(rec0[pos], ts_orig, tbase0, F, k, p0, ts);
+        }
     } else {
         ts = (int64_t)((uint64_t)tbase1 + (rec >> (G.rb + G.pb + 1 + G.pw)));
     }
@@ -879,6 +1164,12 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 #ifndef TBE_LAST_PRESTAGE
 #define TBE_LAST_PRESTAGE 0                  // A/B: fold records formed before staging
 #endif
+#ifndef TBE_BSCAN_LB
+#define TBE_BSCAN_LB 1                       // bucket starts by decoupled look-back; 0: one workgroup (A/B)
+#endif
+#ifndef TBE_NARROW0
+#define TBE_NARROW0 1                        // narrow pass-0 records (PackFmt::n0); 0: A/B
+#endif
 #ifndef TBE_SCATTER0_WAVES
 #define TBE_SCATTER0_WAVES 1
 #endif
@@ -890,8 +1181,13 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
     uint32_t *__restrict__ perm, uint32_t *__restrict__ err, const HotSet *__restrict__ hot = nullptr,
     uint32_t nb = 0, int r_bits = 0, const uint32_t *__restrict__ iin = nullptr,
-    uint32_t *__restrict__ iout = nullptr, FoldFmt G = FoldFmt{}, uint8_t *__restrict__ dig_next = nullptr) {
+    uint32_t *__restrict__ iout = nullptr, FoldFmt G = FoldFmt{}, uint8_t *__restrict__ dig_next = nullptr,
+    const uint8_t *__restrict__ din = nullptr, int64_t *__restrict__ ts0 = nullptr) {
     static_assert(!(FIRST && LAST), "fold records come from a pass after the first");
+    // narrow pass-0 records (F.n0): FIRST writes u32 records (+ escaped times to ts0), LAST
+    // reads them with the pass-1 digit from the digit stream `din`; the LDS stage then holds
+    // record | digit(s) << 32, since the record no longer carries the key
+    const bool n0 = F.n0 != 0 && !IDX && !NOTS;
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
@@ -912,6 +1208,7 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     uint32_t key[kPartItems], lpos[kPartItems];
     bool bad = false;
     bool any_hot = false;
+    int64_t tv_keep[FIRST ? kPartItems : 1];   // narrow records: escaped times go to ts0
     if (FIRST) {
         uint64_t kv[kPartItems];
         int32_t pv[kPartItems];
@@ -926,7 +1223,7 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         }
         // the table fill overlaps the tile loads above
         any_hot = HOT && hot_load<kPartBlock>(hot, hs);
-        const int64_t tbase = NOTS ? 0 : pack_base(tin, F);
+        const int64_t tbase = NOTS ? 0 : (n0 ? pack_base32(tin, F) : pack_base(tin, F));
         uint32_t skv[kPartItems];
         if (HOT && any_hot) {
             hot_sortkeys<kPartItems>(kv, hot_table(hot, hs), nb, r_bits, skv);
@@ -938,22 +1235,48 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         for (int it = 0; it < kPartItems; ++it) {
             const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             bad |= (e < nvalid) && (pv[it] < 0 || (!NOTS && tv[it] < 0));
-            rec[it] = pack_rec(skv[it], pv[it], tv[it], base + e, tbase, F);
+            if (n0) {
+                bool esc;
+                const uint32_t r32 = pack_rec32(skv[it], pv[it], tv[it], tbase, F, esc);
+                // stage: record | pass-0 digit << 32 | pass-1 digit << 40; escape flag in bit 48
+                rec[it] = (uint64_t)r32 | ((uint64_t)((skv[it] >> shift) & (kDigits - 1)) << 32) |
+                          ((uint64_t)((skv[it] >> (shift + kDigitBits)) & (kDigits - 1)) << 40) |
+                          ((uint64_t)esc << 48);
+            } else {
+                rec[it] = pack_rec(skv[it], pv[it], tv[it], base + e, tbase, F);
+            }
             key[it] = skv[it];
+            tv_keep[FIRST ? it : 0] = tv[it];
         }
     } else {
+        if (n0) {
+            const uint32_t *rin32 = reinterpret_cast<const uint32_t *>(rin);
+            uint8_t dv[kPartItems];
 #pragma unroll
-        for (int it = 0; it < kPartItems; ++it) {
-            const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
-            rec[it] = (e < nvalid) ? LD_P(rin + base + e) : 0ull;
-            key[it] = (uint32_t)(rec[it] & F.kmask);
+            for (int it = 0; it < kPartItems; ++it) {
+                const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
+                rec[it] = (e < nvalid) ? (uint64_t)LD_P(rin32 + base + e) : 0ull;
+                dv[it] = (e < nvalid) ? din[base + e] : (uint8_t)0;
+            }
+#pragma unroll
+            for (int it = 0; it < kPartItems; ++it) {
+                key[it] = (uint32_t)dv[it] << shift;
+                rec[it] |= (uint64_t)dv[it] << 32;
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < kPartItems; ++it) {
+                const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
+                rec[it] = (e < nvalid) ? LD_P(rin + base + e) : 0ull;
+                key[it] = (uint32_t)(rec[it] & F.kmask);
+            }
         }
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
     rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
     int64_t tbase0 = 0, tbase1 = 0;
     if (LAST && tin) {   // (the approximate kind has no timestamps: its records all escape)
-        tbase0 = pack_base(tin, F);
+        tbase0 = n0 ? pack_base32(tin, F) : pack_base(tin, F);
         tbase1 = fold_base(tin, G);
     }
     __syncthreads();   // the counts in `stage` are dead from here on
@@ -969,12 +1292,14 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
             if (LAST)
                 stage_d[lpos[it]] = (uint8_t)d;
 #else
-            stage[lpos[it]] = rec[it];
+            stage[lpos[it]] = n0 ? (rec[it] & 0x0000FFFFFFFFFFFFull) : rec[it];
             if (LAST)
                 stage_e[lpos[it]] = (uint16_t)e;
 #endif
             else if (perm)   // (null: k_unrank recomputes the positions)
                 ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
+            if (FIRST && n0 && ((rec[it] >> 48) & 1u))   // escaped: its time beside its position
+                ts0[goff[d] + lpos[it] - L.lstart[d]] = tv_keep[FIRST ? it : 0];
         }
     }
     __syncthreads();
@@ -989,14 +1314,21 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             rout[gpos[it]] = s;   // runs merge in L2: keep cached
 #else
-            const uint32_t d = ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
+            const uint32_t d = n0 ? (uint32_t)(s >> 32) & (kDigits - 1)
+                                  : ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
             // runs merge in L2: keep cached
-            rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
+            if (n0 && !LAST)
+                reinterpret_cast<uint32_t *>(rout)[gpos[it]] = (uint32_t)s;
+            else if (n0)
+                rout[gpos[it]] = fold_rec32((uint32_t)s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G);
+            else
+                rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
 #endif
             // the next pass's digit, one byte beside the record (k_hist_dig reads these)
             if (!LAST && dig_next)
-                dig_next[gpos[it]] = (uint8_t)(((uint32_t)(s & F.kmask) >> (shift + kDigitBits)) & (kDigits - 1));
+                dig_next[gpos[it]] = n0 ? (uint8_t)(s >> 40)
+                                        : (uint8_t)(((uint32_t)(s & F.kmask) >> (shift + kDigitBits)) & (kDigits - 1));
         }
     }
     if (IDX) {
@@ -1189,7 +1521,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
     int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0) {
+    uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0,
+    const uint32_t *__restrict__ dlist = nullptr) {
     __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -1215,7 +1548,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 #endif
 
     const int tid = threadIdx.x;
-    const uint32_t b = fold_bucket(G);
+    // sparse batch: the dense buckets k_bscan listed (dlist); otherwise this block's bucket
+    if (dlist && blockIdx.x >= dlist[0]) return;
+    const uint32_t b = dlist ? dlist[1 + blockIdx.x] : fold_bucket(G);
     if (G.on && b >= G.nb) return;
     const uint32_t R = 1u << r_bits;
     const uint32_t rmask = R - 1;
@@ -1324,7 +1659,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         // barrier before this workgroup's write-back.  384 blocks = half of the 768
         // workgroups in flight: config B fold 0.93 -> 0.85 ms; 768 -> 0.90, 1536 -> 0.93
         // (profiles/r04d_ablate_perm0_prefetch.log)
-        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN && !dlist) {
             const uint32_t fblk = blockIdx.x + TBE_FOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
@@ -1976,6 +2311,105 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
     }
 }
 
+// Sparse buckets of a sparse batch (fewer than wide_min requests; 2^20 requests over 1e8
+// keys put ~21 in each of 48,829 buckets): ONE WAVE per bucket, no LDS.  A workgroup per
+// bucket (k_fold) spent its time on dispatch and on the serial latency of its few loads --
+// 48,829 workgroups at 3 per CU, 0.38 ms for a 2^20 batch -- while a wave needs nothing a
+// workgroup has: its <= 64 requests of a chunk are one per lane, the lanes of one key are
+// found by ballot-matching the 11 row bits, and the key's first lane (the earliest: a
+// bucket's requests are in arrival order) walks the key's requests in lane order, which
+// is the reference's serial order (TB:202-238 per request).  Waves stride over the
+// buckets, and each wave fetches the bounds of all its buckets with one load per lane.
+// A bucket of more than 64 requests goes in chunks of 64; a key's row written back by one
+// chunk is re-read by the next after an agent-scope fence (rare in sparse batches).
+#ifndef TBE_SPARSE_WAVE
+#define TBE_SPARSE_WAVE 1
+#endif
+constexpr int kSpBlock = 256;
+constexpr int kSpWaves = kSpBlock / 64;
+template <bool PACKED>
+__global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
+    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
+    const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
+    const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
+    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
+    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow, uint32_t wide_min,
+    FoldFmt G, const uint64_t *__restrict__ rec0, uint32_t n_walk) {
+    if (*err) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * kSpWaves + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * kSpWaves;
+    const uint32_t rmask = (1u << r_bits) - 1u;
+    const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
+    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
+    const TimeBase TB = time_base(PACKED ? tbase - kRowWindow : -1, P.ttl_ms);
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t bb0 = wave; bb0 < n_walk; bb0 += nwaves * 64u) {
+        // the bounds of this wave's next 64 buckets: lane j holds bucket bb0 + j * nwaves
+        const uint32_t my_bb = bb0 + (uint32_t)lane * nwaves;
+        uint32_t my_b = 0xFFFFFFFFu, my_s = 0, my_e = 0;
+        if (my_bb < n_walk) {
+            my_b = fold_bucket_at(G, my_bb);
+            if (!G.on || my_b < G.nb) {
+                my_s = bstart[my_b];
+                my_e = bstart[my_b + 1];
+            }
+        }
+        uint64_t work = __ballot(my_e > my_s && my_e - my_s < wide_min);
+        while (work) {
+            const int j = __ffsll((long long)work) - 1;
+            work &= work - 1;
+            const uint32_t b = __shfl(my_b, j, 64);
+            const uint32_t s = __shfl(my_s, j, 64), e = __shfl(my_e, j, 64);
+            Slot *__restrict__ rows = table + ((uint64_t)b << r_bits);
+            for (uint32_t c = s; c < e; c += 64) {
+                if (c != s) __threadfence();   // the previous chunk's row stores are visible
+                const uint32_t q = c + (uint32_t)lane;
+                const bool v = q < e;
+                uint32_t kl = 0, pos = q;
+                int32_t pm = 0;
+                int64_t tsv = 0;
+                if (v) {
+                    if (PACKED) {
+                        fold_input(LD_F(srec + q), q, G, tbase1, rec0, ts_orig, tbase, F, rmask, kl, pm, tsv, pos);
+                    } else {
+                        kl = skeys[q] & rmask;
+                        pm = sperm[q];
+                        tsv = sts[q];
+                    }
+                }
+                // lanes of the same key (row): ballot-match the row bits
+                uint64_t peers = __ballot(v);
+                for (int bit = 0; bit < r_bits; ++bit) {
+                    const bool x = (kl >> bit) & 1u;
+                    const uint64_t m = __ballot(x);
+                    peers &= x ? m : ~m;
+                }
+                const bool leader = v && (peers & lt) == 0;   // the key's earliest request here
+                Slot st = Slot{0.0, 0};
+                if (leader) st = rows[kl];
+                uint64_t todo = leader ? peers : 0ull;
+                bool mod = false;
+                while (__any(todo != 0ull)) {
+                    const int m = todo ? __ffsll((long long)todo) - 1 : lane;
+                    const int32_t pm_m = __shfl(pm, m, 64);
+                    const int64_t ts_m = __shfl(tsv, m, 64);
+                    const uint32_t pos_m = __shfl(pos, m, 64);
+                    if (todo) {
+                        const ReqTime rq = PACKED ? req_time_rel(ts_m, TB, P.ttl_ms) : req_time(ts_m, P.ttl_ms);
+                        bool md;
+                        const uint32_t rep = tb_step_ft(st, field_t(st.t_us, TB), pm_m, rq, P, md);
+                        mod |= md;
+                        put_reply(res, pos_m, rep, narrow);
+                        todo &= todo - 1;
+                    }
+                }
+                if (leader && mod) rows[kl] = st;
+            }
+        }
+    }
+}
+
 // Inverse of one k_scatter pass: out[i] = in[perm[i]] with perm the positions that pass
 // wrote (runs of ~32 consecutive positions per digit and tile, so the gather coalesces).
 // FINAL: unpack into granted/status (u8) and remaining (i32) in arrival order.
@@ -2013,10 +2447,14 @@ __global__ __launch_bounds__(kUnBlock) void k_unscatter(uint64_t n, const uint32
                                                           const uint32_t *__restrict__ res_in,
                                                           uint32_t *__restrict__ res_out,
                                                           uint8_t *__restrict__ granted,
-                                                          int32_t *__restrict__ remaining) {
+                                                          int32_t *__restrict__ remaining,
+                                                          const uint32_t *__restrict__ err = nullptr,
+                                                          uint32_t *__restrict__ sticky = nullptr) {
     // One workgroup per 8192 positions, XCD-aware like k_scatter: the tile's gathers land
     // in the digit runs of the partition tiles it covers, which stay in this XCD's L2.
     const int tid = threadIdx.x;
+    // the batch's last kernel carries k_sticky's work (every kernel that sets err ran before)
+    if (sticky && blockIdx.x == 0 && tid == 0 && *err) *sticky = 1u;
     const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t base = (uint64_t)tile * kUnTile;
     const int nvalid = (int)min<uint64_t>(kUnTile, n - base);
@@ -2196,7 +2634,7 @@ __global__ __launch_bounds__(1024) void k_hot_plan(const HotSet *__restrict__ ho
 }
 
 // Run h of segment j: the last h with segbase[h] <= j.
-__device__ __forceinline__ uint32_t seg_run(const uint32_t *__restrict__ segbase, uint32_t j) {
+__device__ __forceinline__ uint32_t seg_run(const uint32_t *segbase, uint32_t j) {
     uint32_t lo = 0, hi = kHotKeysMax;   // segbase[lo] <= j < segbase[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -2214,15 +2652,39 @@ __device__ __forceinline__ uint32_t seg_run(const uint32_t *__restrict__ segbase
 template <bool SPEC>
 __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
-    const uint32_t *__restrict__ bstart, uint32_t nb, const uint32_t *__restrict__ segbase,
+    const uint32_t *__restrict__ bstart, uint32_t nb, uint32_t *segbase,
     SegSummary *__restrict__ summ, const uint32_t *__restrict__ err, FoldFmt G, const uint64_t *__restrict__ rec0,
     const HotSet *__restrict__ hot = nullptr, const Slot *__restrict__ table = nullptr, TbParams P = TbParams{},
-    uint32_t *__restrict__ res = nullptr, uint32_t narrow = 0) {
+    uint32_t *__restrict__ res = nullptr, uint32_t narrow = 0, uint32_t plan = 0) {
     __shared__ int64_t wts[kSegBlock / 64];
     __shared__ int32_t wp[kSegBlock / 64];
     __shared__ uint32_t pass_s0;
+    __shared__ uint32_t sb[kHotKeysMax + 1];
+    __shared__ uint32_t sbw[kSegBlock / 64];
     if (*err) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (plan) {
+        // k_hot_plan's scan, done by every workgroup (1024 run lengths from the bucket
+        // starts); workgroup 0 publishes segbase for k_hot_chain and k_hot_replies
+        static_assert(kHotKeysMax == 2 * kSegBlock, "two runs per thread");
+        const uint32_t cnt = hot->count;
+        uint32_t ns[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t h = 2 * tid + u;
+            ns[u] = h < cnt ? (bstart[nb + h + 1] - bstart[nb + h] + kSeg - 1) / kSeg : 0u;
+        }
+        uint32_t all;
+        const uint32_t pre = block_excl_scan<kSegBlock>(ns[0] + ns[1], sbw, &all);
+        sb[2 * tid] = pre;
+        sb[2 * tid + 1] = pre + ns[0];
+        if (tid == 0) sb[kHotKeysMax] = all;
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            for (uint32_t j = tid; j <= kHotKeysMax; j += kSegBlock) segbase[j] = sb[j];
+        }
+        segbase = sb;
+    }
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
@@ -2467,12 +2929,18 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
 __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, uint32_t cap,
                                                      const uint32_t *__restrict__ err) {
     __shared__ uint64_t c[kHotCandMax];
-    if (*err) return;
+    // The nominations are consumed here: n_cand restarts at 0 for the fold that next
+    // nominates into this set (three batches later), so no separate reset is launched.
+    if (*err) {
+        if (threadIdx.x == 0) next->n_cand = 0;
+        return;
+    }
     const uint32_t t = threadIdx.x;
     const uint32_t nc = min(next->n_cand, kHotCandMax);
     for (uint32_t j = t; j < kHotCandMax; j += 1024) c[j] = j < nc ? next->cand[j] : 0ull;
     for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot[j] = kHotSlotEmpty;
     __syncthreads();
+    if (t == 0) next->n_cand = 0;
     for (uint32_t k = 2; nc > cap && k <= kHotCandMax; k <<= 1) {   // select only when over capacity
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t i = t; i < kHotCandMax; i += 1024) {
@@ -2566,6 +3034,7 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
 constexpr uint32_t kHotSampleN = 16384;
 constexpr uint32_t kHotSampleSlots = 32768;
 constexpr uint64_t kHotSampleMin = 65536;   // estimated requests of the batch
+#if TBE_HOT_SAMPLE && !TBE_HOT_CUCKOO        // (the cuckoo table's path samples every batch: k_hot_sample)
 __global__ __launch_bounds__(1024) void k_hot_sample_count(const uint64_t *__restrict__ keys, uint64_t n,
                                                            uint64_t n_keys, uint32_t S,
                                                            uint32_t *__restrict__ skey, uint32_t *__restrict__ scnt) {
@@ -2602,6 +3071,116 @@ __global__ __launch_bounds__(1024) void k_hot_sample_pick(const uint32_t *__rest
     }
     __syncthreads();
     if (threadIdx.x == 0) hot->n_cand = nc;
+}
+#endif
+
+// Every batch is sampled (rounds 3-4 sampled only an engine's first
+// two batches): a key that turns hot in a running engine would otherwise fill one ordinary
+// bucket for the two batches its fold nomination takes, and that workgroup walks its
+// millions of requests (~27 ms at config C's hottest key).  One 1024-thread workgroup, on
+// the partition stream before the batch's first histogram:
+//   1. kHotSampleN requests, one per stratum of the batch; keys already in its hot set are
+//      skipped, the others counted in an LDS hash (kHsSlots slots, bounded probing: a
+//      sample that finds no slot is dropped -- speed only);
+//   2. every key estimated at >= kHotSampleMin requests of the batch is appended to the
+//      hot set (new run index, cuckoo placement in the LDS copy of the table), up to the
+//      set's capacity -- fold nominations fill at most cap - kHotSampleReserve of it;
+//   3. only if a key was added, the table goes back to global memory.
+// The steady state (every dominant key already hot, or none) reads 16,384 keys and writes
+// nothing.  Which keys run apart only changes speed, never a decision.
+constexpr uint32_t kHsSlots = 8192;
+constexpr int kHsProbes = 8;
+constexpr uint32_t kHsNewMax = 256;   // config C: ~71 keys above kHotSampleMin at cold start
+__global__ __launch_bounds__(1024) void k_hot_sample(const uint64_t *__restrict__ keys, uint64_t n,
+                                                     uint64_t n_keys, HotSet *__restrict__ hot, uint32_t cap) {
+    __shared__ uint32_t skey[kHsSlots];
+    __shared__ uint32_t scnt[kHsSlots];
+    __shared__ uint64_t tab[kHotSlots];
+    __shared__ uint64_t newk[kHsNewMax];
+    __shared__ uint32_t nnew, count;
+    const uint32_t t = threadIdx.x;
+    const uint32_t S = (uint32_t)min<uint64_t>(n, kHotSampleN);
+    if (t == 0) {
+        nnew = 0;
+        count = hot->count;
+    }
+    for (uint32_t j = t; j < kHsSlots; j += 1024) {
+        skey[j] = 0xFFFFFFFFu;
+        scnt[j] = 0;
+    }
+    __syncthreads();
+    const bool any = count != 0;
+    for (uint32_t j = t; j < kHotSlots; j += 1024) tab[j] = any ? hot->slot[j] : kHotSlotEmpty;
+    __syncthreads();
+    // one request from each of S equal strata, at a hashed offset inside the stratum: a
+    // fixed stride would alias with periodic traffic (a key at every 10th position is
+    // never sampled at stride 4096).  All of a thread's loads are issued before any is used.
+    constexpr int kPerThread = kHotSampleN / 1024;
+    uint64_t kv[kPerThread];
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+        const uint32_t i = t + 1024u * j;
+        kv[j] = ~0ull;
+        if (i < S) {
+            const uint64_t lo = (uint64_t)i * n / S, hi = (uint64_t)(i + 1) * n / S;
+            uint32_t hx = (i + 0x9E3779B9u) * 0x85EBCA6Bu;
+            hx ^= hx >> 13;
+            hx *= 0xC2B2AE35u;
+            hx ^= hx >> 16;
+            kv[j] = keys[lo + (uint64_t)hx % (hi - lo)];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+        const uint64_t key = kv[j];
+        if (key >= n_keys || key >= 0xFFFFFFFFull) continue;   // invalid keys fail the batch anyway
+        const uint32_t k = (uint32_t)key;
+        if ((uint32_t)tab[hot_h1(k)] == k || (uint32_t)tab[hot_h2(k)] == k) continue;   // already hot
+        uint32_t h = (k * 0x9E3779B1u) >> (32 - 13);
+        static_assert(kHsSlots == 1u << 13, "13-bit sample slots");
+        for (int probe = 0; probe < kHsProbes; ++probe) {
+            const uint32_t old = atomicCAS(&skey[h], 0xFFFFFFFFu, k);
+            if (old == 0xFFFFFFFFu || old == k) {
+                atomicAdd(&scnt[h], 1u);
+                break;
+            }
+            h = (h + 1) & (kHsSlots - 1);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < kHsSlots; j += 1024) {
+        const uint32_t c = scnt[j];
+        if (c != 0 && (uint64_t)c * n / S >= kHotSampleMin) {
+            const uint32_t at = atomicAdd(&nnew, 1u);
+            if (at < kHsNewMax) newk[at] = skey[j];
+        }
+    }
+    __syncthreads();
+    if (nnew == 0) return;                    // workgroup-uniform
+    if (t == 0) {
+        uint32_t cnt = count;
+        for (uint32_t u = 0; u < min(nnew, kHsNewMax) && cnt < cap; ++u) {
+            const uint32_t key = (uint32_t)newk[u];
+            hot->key[cnt] = key;
+            uint64_t cur = ((uint64_t)cnt << 32) | key;
+            ++cnt;
+            uint32_t at = hot_h1(key);
+            if (tab[at] != kHotSlotEmpty && tab[hot_h2(key)] == kHotSlotEmpty) at = hot_h2(key);
+            // cuckoo kicks; an entry left without a slot keeps its run index and runs empty
+            for (int m = 0; m < 64 && cur != kHotSlotEmpty; ++m) {
+                const uint64_t old = tab[at];
+                tab[at] = cur;
+                cur = old;
+                if (cur == kHotSlotEmpty) break;
+                const uint32_t k = (uint32_t)cur;
+                at = (at == hot_h1(k)) ? hot_h2(k) : hot_h1(k);
+            }
+        }
+        count = cnt;
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < kHotSlots; j += 1024) hot->slot[j] = tab[j];
+    if (t == 0) hot->count = count;
 }
 
 // ----------------------------------------------------------------------------- queueing kind
@@ -3467,7 +4046,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
 #if TBE_AFOLD_PREFETCH
         // as k_fold_wide: touch the local-tier slice and records of the workgroup
         // TBE_AFOLD_PREFETCH blocks later (same XCD); waited for at the write-back barrier
-        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN && !dlist) {
             const uint32_t fblk = blockIdx.x + TBE_AFOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
@@ -3797,8 +4376,11 @@ struct Workspace {
     uint32_t *res[2] = {nullptr, nullptr};
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
+    uint32_t *dlist = nullptr;    // sparse batches: count + ids of the dense buckets (k_bscan)
+    unsigned long long *bsflags = nullptr;   // k_bscan_lb's published totals (tagged per batch)
     uint8_t *dig0 = nullptr;      // each request's pass-0 digit (k_unrank re-ranks from it)
     uint8_t *dig1 = nullptr;      // pass 1's digit of pass 0's output, in that order (k_hist_dig)
+    int64_t *ts0 = nullptr;       // narrow pass-0 records: escaped requests' times at their pass-0 position
     uint32_t *err = nullptr;      // the batch's invalid-request flag
     hipEvent_t hot_done = nullptr;   // pipelined: k_hot_update of the last batch on this workspace
     bool hot_pending = false;
@@ -3844,6 +4426,9 @@ struct tbe_engine {
     // byte in its output order, and pass 1's histogram (k_hist_dig) reads 1 byte per
     // request instead of 8 (TBE_FLAG_HIST_RECORDS: off)
     bool dig1 = false;
+    // narrow pass-0 records (PackFmt::n0): token bucket, packed, two passes, fold records and
+    // the digit stream, and at least 8 time-offset bits left in 32
+    bool n0 = false;
     // hot runs (token bucket, packed): bucket ids [nbuckets, nb_total) belong to hot keys.
     // Batch b is partitioned by hot[b % 3] and nominates into hot[(b + 2) % 3], so the set
     // batch b+1 is partitioned by was complete before batch b's fold began.
@@ -3967,9 +4552,12 @@ void free_workspace(Workspace &w) {
     dfree(w.res[1]);
     dfree(w.bstart);
     dfree(w.bcount);
+    w.err = nullptr;   // (the word after the bucket counts)
+    dfree(w.dlist);
+    dfree(w.bsflags);
     dfree(w.dig0);
     dfree(w.dig1);
-    dfree(w.err);
+    dfree(w.ts0);
     w.cap_n = 0;
     w.used = false;
 }
@@ -4021,10 +4609,16 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.res[0], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.res[1], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
-    HIP_TRY(e, hipMalloc(&w.bcount, (uint64_t)e->nb_total * sizeof(uint32_t)));
+    // the batch's error flag is the word after its bucket counts: one memset clears both
+    HIP_TRY(e, hipMalloc(&w.bcount, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
+    w.err = w.bcount + e->nb_total;
+    HIP_TRY(e, hipMalloc(&w.dlist, ((uint64_t)e->nbuckets + 1) * sizeof(uint32_t)));
+    HIP_TRY(e, hipMalloc(&w.bsflags, kBsMaxBlocks * sizeof(unsigned long long)));
+    HIP_TRY(e, hipMemset(w.bsflags, 0, kBsMaxBlocks * sizeof(unsigned long long)));
+    HIP_TRY(e, hipDeviceSynchronize());   // (allocation time only) zeroed before any stream reads it
     if (e->unrank) HIP_TRY(e, hipMalloc(&w.dig0, cap));
     if (e->dig1) HIP_TRY(e, hipMalloc(&w.dig1, cap));
-    HIP_TRY(e, hipMalloc(&w.err, sizeof(uint32_t)));
+    if (e->n0) HIP_TRY(e, hipMalloc(&w.ts0, cap * sizeof(int64_t)));
     w.cap_n = cap;
     return TBE_OK;
 }
@@ -4082,6 +4676,15 @@ uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #endif
 }
 
+// Run slots the per-batch sampler keeps free of fold nominations (k_hot_sample)
+inline uint32_t hot_reserve_host(uint32_t cap) {
+#if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
+    return std::min(32u, cap / 4u);
+#else
+    return 0u;
+#endif
+}
+
 // Fold records for a batch of n requests: the reply position takes ceil_log2(n) bits, the
 // time offset what is left (>= 8 bits, else the plain records).  tbe_batch_format reports it.
 FoldFmt batch_fold_fmt(const tbe_engine *e, uint64_t n) {
@@ -4092,6 +4695,7 @@ FoldFmt batch_fold_fmt(const tbe_engine *e, uint64_t n) {
     const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
     if (tw >= (approx ? 1 : 8)) {   // (the approximate kind's records carry no time)
         G.on = 1;
+        G.n0 = e->n0 ? 1 : 0;
         G.rb = e->r_bits;
         G.pb = e->pf.pb;
         G.pw = pw;
@@ -4143,18 +4747,25 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     } else if (in_ready) {            // chunked host-buffer path (queueing / approximate)
         HIP_TRY(e, hipStreamWaitEvent(sf, in_ready, 0));
     }
-    HIP_TRY(e, hipMemsetAsync(w.err, 0, sizeof(uint32_t), sp));
+    HIP_TRY(e, hipMemsetAsync(w.bcount, 0, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t), sp));   // + err
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
     const FoldFmt G = batch_fold_fmt(e, n);
-    const uint64_t *rec0 = G.on ? w.pass[e->passes - 2].rec : nullptr;
+    // narrow pass-0 records only with this batch's fold records; the folds then find an
+    // escaped request's time in ts0 (FoldFmt::n0)
+    PackFmt pf = e->pf;
+    pf.n0 = G.n0;
+    const uint64_t *rec0 = G.on ? (G.n0 ? reinterpret_cast<const uint64_t *>(w.ts0) : w.pass[e->passes - 2].rec)
+                                : nullptr;
     const bool unrank = e->unrank;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
-    HIP_TRY(e, hipMemsetAsync(w.bcount, 0, (uint64_t)e->nb_total * sizeof(uint32_t), sp));
     // hot runs: see tbe_engine::hot
     HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
     HotSet *hot_next = e->hot_cap ? e->hot[(e->nbatch + 2) % 3] : nullptr;
-#if TBE_HOT_SAMPLE
+#if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
+    // every batch: its dominant keys join its own hot set (k_hot_sample)
+    if (hot && n >= kHotSampleMin) k_hot_sample<<<1, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, hot, e->hot_cap);
+#elif TBE_HOT_SAMPLE
     if (hot && e->nbatch < 2 && e->hs_key && n >= kHotSampleMin) {
         // cold start: nominate this batch's dominant keys into its own (still empty) hot set
         const uint32_t S = (uint32_t)std::min<uint64_t>(n, kHotSampleN);
@@ -4184,6 +4795,9 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total, dig);
+        else if (e->dig1 && p == 1 && TBE_HIST_DIG_WAVE)
+            k_hist_dig_w<<<nblk, kHBlock, 0, sp>>>(w.dig1, n, tpb, ntiles, out.tileprefix, w.blocksum,
+                                                   w.pass[0].digit_total, bc, e->nb_total);
         else if (e->dig1 && p == 1)
             k_hist_dig<<<nblk, kHBlock, 0, sp>>>(w.dig1, n, tpb, ntiles, out.tileprefix, w.blocksum,
                                                  w.pass[0].digit_total, bc, e->nb_total);
@@ -4233,19 +4847,19 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 w.pass[p - 1].idx, out.idx);
         else if (e->packed && p == 0 && hot)
             k_scatter_rec<true, true><<<ntiles, kPartBlock, 0, sp>>>(
-                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                keys, permits, ts, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, hot, e->nbuckets, e->r_bits,
-                nullptr, nullptr, FoldFmt{}, dnext);
+                nullptr, nullptr, FoldFmt{}, dnext, nullptr, w.ts0);
         else if (e->packed && p == 0)
             k_scatter_rec<true><<<ntiles, kPartBlock, 0, sp>>>(
-                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                keys, permits, ts, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
-                nullptr, FoldFmt{}, dnext);
+                nullptr, FoldFmt{}, dnext, nullptr, w.ts0);
         else if (e->packed && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
-                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, pf, out.tileprefix,
                 out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0, nullptr,
-                nullptr, G);
+                nullptr, G, nullptr, w.dig1, nullptr);
         else if (e->packed)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -4280,15 +4894,25 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         stage_end(e, ST_SCATTER, sp);
     }
     const PassBufs &sorted = w.pass[e->passes - 1];
+    // token bucket: a sparse batch's dense buckets are listed for k_fold_wide, the rest go to
+    // one wave each (k_fold_sparse)
+    const uint32_t tb_wmin = (!approx && !wait) ? fold_wide_min(e, n) : 1u;
+    const bool sparse_tb = TBE_SPARSE_WAVE && tb_wmin > 1u;
     stage_begin(e, ST_BOUNDS, sp);
-    k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart);
+    const uint32_t bs_blocks = (e->nb_total + kBsTile - 1) / kBsTile;
+    if (sparse_tb)
+        k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, e->nbuckets, tb_wmin, w.dlist);
+    else if (TBE_BSCAN_LB && bs_blocks <= kBsMaxBlocks)
+        k_bscan_lb<<<bs_blocks, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, w.bsflags,
+                                               (uint32_t)(e->nbatch + 1));
+    else
+        k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart);
     stage_end(e, ST_BOUNDS, sp);
     if (pipe) {
         HIP_TRY(e, hipEventRecord(e->ev_part, sp));
         HIP_TRY(e, hipStreamWaitEvent(sf, e->ev_part, 0));
     }
-    // hot_next was last read by batch b-1's partition and hot runs, both done by now
-    if (hot_next) HIP_TRY(e, hipMemsetAsync(&hot_next->n_cand, 0, sizeof(uint32_t), sf));
+    // hot_next->n_cand was reset by the k_hot_update that consumed its last nominations
     stage_begin(e, ST_FOLD, sf);
     if (approx) {
         AParams a = e->ap;
@@ -4322,9 +4946,30 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
                 e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
                 e->wait_rw(), e->qtick, G, rec0);
+    } else if (sparse_tb) {
+        // sparse batch: at most n / wmin buckets are dense (k_bscan listed them); one wave per
+        // other bucket
+        const unsigned dgrid = (unsigned)std::min<uint64_t>(e->nbuckets, n / tb_wmin + 1);
+        const uint32_t walk = e->packed ? fold_grid : e->nbuckets;
+        const unsigned sgrid = (unsigned)std::min<uint64_t>((walk + kSpWaves - 1) / kSpWaves, 2048);
+        if (e->packed) {
+            k_fold_wide<true><<<dgrid, kWideBlock, 0, sf>>>(
+                nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0, w.dlist);
+            k_fold_sparse<true><<<sgrid, kSpBlock, 0, sf>>>(
+                nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
+                e->table, e->params, w.res[0], w.err, e->narrow ? 1u : 0u, tb_wmin, G, rec0, walk);
+        } else {
+            k_fold_wide<false><<<dgrid, kWideBlock, 0, sf>>>(
+                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
+                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0, w.dlist);
+            k_fold_sparse<false><<<sgrid, kSpBlock, 0, sf>>>(
+                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
+                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, 0u, tb_wmin, G, rec0, walk);
+        }
     } else if (e->packed) {
         // dense buckets in k_fold_wide, the others in k_fold (each skips the other's)
-        const uint32_t wmin = fold_wide_min(e, n);
+        const uint32_t wmin = tb_wmin;
         k_fold_wide<true><<<fold_grid, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
@@ -4333,7 +4978,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
                 e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
     } else {
-        const uint32_t wmin = fold_wide_min(e, n);
+        const uint32_t wmin = tb_wmin;
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
             e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin, G, rec0);
@@ -4348,12 +4993,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         // unchanged row as part of its bucket's slice), then the hot set of batch b+2
         stage_begin(e, ST_HOT, sf);
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
-        k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
-        if (TBE_HOT_SPEC)
+        if (TBE_HOT_SPEC)   // (the summary kernel also does k_hot_plan's scan)
             k_hot_summary<true><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                              w.segbase, w.summ, w.err, G, rec0, hot, e->table,
-                                                             e->params, w.res[0], e->narrow ? 1u : 0u);
+                                                             e->params, w.res[0], e->narrow ? 1u : 0u, 1u);
         else
+            k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
+        if (!TBE_HOT_SPEC)
             k_hot_summary<false><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                               w.segbase, w.summ, w.err, G, rec0);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
@@ -4368,11 +5014,11 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
             // un-partition; batch b+2 (same workspace) waits for it before its partition.
             HIP_TRY(e, hipEventRecord(e->ev_hot, sf));
             HIP_TRY(e, hipStreamWaitEvent(e->hstream, e->ev_hot, 0));
-            k_hot_update<<<1, 1024, 0, e->hstream>>>(hot_next, e->hot_cap, w.err);
+            k_hot_update<<<1, 1024, 0, e->hstream>>>(hot_next, e->hot_cap - hot_reserve_host(e->hot_cap), w.err);
             HIP_TRY(e, hipEventRecord(w.hot_done, e->hstream));
             w.hot_pending = true;
         } else {
-            k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap, w.err);
+            k_hot_update<<<1, 1024, 0, sf>>>(hot_next, e->hot_cap - hot_reserve_host(e->hot_cap), w.err);
         }
         stage_end(e, ST_HOT, sf);
     }
@@ -4408,21 +5054,26 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
 #undef TBE_UNRANK
     else if (e->narrow && !wait && !approx)
         k_unscatter<true, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                                  nullptr, granted, remaining);
+                                                                  nullptr, granted, remaining,
+            w.err, e->sticky);
     else if (wait && e->narrow)
         k_unscatter<true, true, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                                 nullptr, granted, remaining);
+                                                                 nullptr, granted, remaining,
+            w.err, e->sticky);
     else if (wait && e->medium)
         k_unscatter<true, true, 2><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                                 nullptr, granted, remaining);
+                                                                 nullptr, granted, remaining,
+            w.err, e->sticky);
     else if (wait)
         k_unscatter<true, true><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                              nullptr, granted, remaining);
+                                                              nullptr, granted, remaining,
+            w.err, e->sticky);
     else
         k_unscatter<true, false><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
-                                                               nullptr, granted, remaining);
+                                                               nullptr, granted, remaining,
+            w.err, e->sticky);
     stage_end(e, ST_UNSCATTER, sf);
-    k_sticky<<<1, 64, 0, sf>>>(w.err, e->sticky);
+    if (unrank) k_sticky<<<1, 64, 0, sf>>>(w.err, e->sticky);   // (otherwise the final unscatter did it)
     HIP_TRY(e, hipGetLastError());
     if (pipe) {
         HIP_TRY(e, hipEventRecord(w.done, sf));
@@ -4545,6 +5196,13 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->foldrec = e->packed && e->passes >= 2 && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0;
         e->unrank = e->packed && (c.flags & TBE_FLAG_UNSCATTER_ALL) == 0 && (c.flags & TBE_FLAG_RERANK) != 0;
         e->dig1 = e->packed && e->passes == 2 && (c.flags & TBE_FLAG_HIST_RECORDS) == 0;
+        {
+            const int w0 = 32 - e->r_bits - pbits - 1;
+            e->n0 = TBE_NARROW0 && e->dig1 && e->foldrec && c.kind == TBE_KIND_TOKEN_BUCKET && w0 >= 8;
+            e->pf.n0 = 0;                  // per batch (run_batch): only with this batch's fold records
+            e->pf.rb = e->r_bits;
+            e->pf.w0 = w0;
+        }
         e->narrow = (c.flags & TBE_FLAG_NO_NARROW) == 0 &&
                     ((e->packed && c.kind == TBE_KIND_TOKEN_BUCKET && c.token_limit <= 127) ||
                      (c.kind == TBE_KIND_QUEUEING && c.token_limit <= 62));
@@ -4563,11 +5221,30 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         return bail(TBE_EDEVICE);
     }
     e->pipeline = c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_NO_PIPELINE) == 0;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
-        return bail(TBE_EDEVICE);
-    e->own_stream = true;
-    if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
-        return bail(TBE_EDEVICE);
+    // CU split (A/B, env TBE_CU_SPLIT = d in {2, 4, 8}): the partition stream gets 1/d of the
+    // CUs and the fold stream the rest, so batch b+1's bandwidth-bound partition runs beside
+    // batch b's latency-bound fold instead of waiting for CUs the fold's LDS fills.  CU i goes
+    // to the partition when (i / 8 + i) % d == 0: 1/d of every XCD whether CU ids are
+    // contiguous per XCD or interleaved across XCDs.
+    int cu_split = 0;
+    if (const char *cs = std::getenv("TBE_CU_SPLIT")) cu_split = std::atoi(cs);
+    if (e->pipeline && (cu_split == 2 || cu_split == 4 || cu_split == 8)) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, e->device) != hipSuccess) return bail(TBE_EDEVICE);
+        const int ncu = prop.multiProcessorCount;
+        std::vector<uint32_t> mp((ncu + 31) / 32, 0u), mf((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) ((i / 8 + i) % cu_split == 0 ? mp : mf)[i / 32] |= 1u << (i % 32);
+        if (hipExtStreamCreateWithCUMask(&e->stream, (uint32_t)mf.size(), mf.data()) != hipSuccess ||
+            hipExtStreamCreateWithCUMask(&e->pstream, (uint32_t)mp.size(), mp.data()) != hipSuccess)
+            return bail(TBE_EDEVICE);
+        e->own_stream = true;
+    } else {
+        if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(TBE_EDEVICE);
+        e->own_stream = true;
+        if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
+            return bail(TBE_EDEVICE);
+    }
     if (e->pipeline && hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
     for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ev_hot, &e->ws[0].done, &e->ws[1].done,
@@ -5604,7 +6281,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
               (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
-              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u);
+              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u) | (e->n0 ? 256u : 0u);
     return TBE_OK;
 }
 
@@ -5617,7 +6294,7 @@ tbe_status tbe_batch_format(const tbe_engine *e, uint64_t n, uint32_t *out, uint
     out[3] = (uint32_t)G.tw;                       // time-offset bits of a fold record
     out[4] = (uint32_t)e->pf.kb;                   // pass-0 record: key bits
     out[5] = (uint32_t)e->pf.pb;                   // permit-code bits
-    out[6] = (uint32_t)e->pf.wb;                   // pass-0 time-offset bits
+    out[6] = (uint32_t)(G.n0 ? e->pf.w0 : e->pf.wb);   // pass-0 time-offset bits (narrow records: w0)
     out[7] = (uint32_t)e->r_bits;
     return TBE_OK;
 }

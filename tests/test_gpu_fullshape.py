@@ -250,6 +250,21 @@ def test_config_e_full_shape_queued_waits(engine_lib, gpu):
     assert queued > 1_000_000 and drained > 1_000_000, (queued, drained)
 
 
+@pytest.mark.timeout(900)
+def test_config_e_full_shape_eight_clients(engine_lib, gpu):
+    """the refresh an 8-GPU node runs in config E -- 1e7 shared keys, 8
+    clients, each client's counts all-gathered and every key's sync script replayed 8 times
+    in client order with staggered timestamps (A:241-270, A:430-443) -- at full size: 8
+    client engines (2^25 requests each per epoch), two epochs, every status, the whole
+    global-tier replica and sampled local tiers against 8 C restatements (tba_*)."""
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    kshared, n, tl, tpp, interval, clients, epochs = 10_000_000, 1 << 25, 100, 10, 10_000, 8, 2
+    ticks = interval * 10
+    engs = [ApproximateEngine(kshared, tl, tpp, ticks, 0, 0, device=0, max_batch=n) for _ in range(clients)]
+    refs = [cref.CApprox(kshared, tl, tpp, ticks, 0, 0, 4) for _ in range(clients)]
+    run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait=False)
+
+
 def run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait):
     """Epochs of 2^26 requests per client, then collect -> the all-gather's layout ->
     client-ordered sync replay with staggered timestamps; returns (drained, queued)."""
@@ -310,3 +325,43 @@ def run_approx_epochs(gpu, engs, refs, kshared, n, interval, ticks, epochs, wait
         log(f"config E epoch {e}: global tier replica (1e7 keys) and sampled local tiers identical "
             f"({drained} queued requests drained so far)")
     return drained, queued
+
+
+@pytest.mark.timeout(900)
+def test_key_turns_hot_mid_run(engine_lib, gpu):
+    """a key that turns hot in a running engine.  Uniform 2^26-request
+    batches over 1.25e8 keys; from batch 5 on, 10% of every batch (6.7M requests) is one key
+    that was cold before.  Every batch is sampled (k_hot_sample), so the key runs apart in
+    the very batch it turns hot -- no fold walks its millions of requests in one workgroup
+    (~27 ms before) -- and replies and table stay identical to the C restatement."""
+    import torch
+    from distributedratelimiting.redis_amd import TokenBucketEngine, _capi, fill_rate
+    lib = _capi.load()
+    n_keys, n, batches, turn, hot_key = 125_000_000, 1 << 26, 8, 5, 98_765_432
+    eng = TokenBucketEngine(n_keys, 10, 1, 10_000_000, device=0, max_batch=n, stage_timing=True)
+    assert eng.layout()["hot"]
+    ref = cref.CTokenBucket(n_keys, 10, fill_rate(1, 10_000_000))
+    k = torch.empty(n, dtype=torch.int64, device=gpu)
+    p = torch.empty(n, dtype=torch.int32, device=gpu)
+    t = torch.empty(n, dtype=torch.int64, device=gpu)
+    g = torch.empty(n, dtype=torch.uint8, device=gpu)
+    r = torch.empty(n, dtype=torch.int32, device=gpu)
+    sel = (torch.arange(n, device=gpu) % 10) == 3
+    for b in range(batches):
+        assert lib.tbe_gen_batch_device(0x5EED00F0, n_keys, b * n, n, 1, 1, T0_US + b * 10_000, 10_000,
+                                        k.data_ptr(), p.data_ptr(), t.data_ptr(), None) == 0
+        if b >= turn:
+            k[sel] = hot_key
+        torch.cuda.synchronize()
+        eng.acquire_batch_device(k, p, t, g, r)
+        eng.synchronize()
+        st = eng.stage_times()
+        hk = k.cpu().numpy().view(np.uint64)
+        g_ref, r_ref = ref.acquire_batch(hk, p.cpu().numpy(), t.cpu().numpy(), threads=THREADS)
+        assert_replies(b, g.cpu().numpy(), r.cpu().numpy(), g_ref, r_ref)
+        log(f"mid-run hot key, batch {b}: replies identical; fold {st.get('fold', 0):.3f} ms, "
+            f"hot runs {st.get('hot', 0):.3f} ms")
+        if b >= turn:
+            assert st.get("fold", 0.0) < 5.0, (b, st)
+            assert st.get("hot", 0.0) > 0.05, (b, st)
+    assert_same_table(*eng.export_state(), *ref.export_state())

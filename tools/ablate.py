@@ -199,6 +199,14 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "r05": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "digold_u": (["TBE_HIST_DIG_WAVE=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "n0off_u": (["TBE_NARROW0=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "digold_z": (["TBE_HIST_DIG_WAVE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "n0off_z": (["TBE_NARROW0=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
