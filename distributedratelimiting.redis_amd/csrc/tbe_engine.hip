@@ -1355,6 +1355,89 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     if (FIRST && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
 }
 
+// The last partition pass of the token-bucket path with narrow pass-0 records, as
+// persistent workgroups (A/B, TBE_LAST_PERSIST = number of workgroups, a multiple of 8):
+// each walks tiles it, it + gridDim, ... of one XCD's range, sets up the digit bases and
+// record bases once, and loads its next tile's records and digit bytes while the current
+// tile is ranked, staged and written.  Same output as k_scatter_rec<false, ..., LAST>.
+#ifndef TBE_LAST_PERSIST
+#define TBE_LAST_PERSIST 0
+#endif
+#ifndef TBE_LAST_PERSIST_WAVES
+#define TBE_LAST_PERSIST_WAVES 4                 // 2 workgroups per CU; 5 spills 16 VGPRs
+#endif
+__global__ __launch_bounds__(kPartBlock, TBE_LAST_PERSIST_WAVES) void k_scatter_last_p(
+    const uint32_t *__restrict__ rin32, const uint8_t *__restrict__ din, uint64_t n, int shift, PackFmt F,
+    const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
+    const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
+    const int64_t *__restrict__ tin, FoldFmt G) {
+    __shared__ RankLds<kPartBlock> L;
+    __shared__ uint32_t goff[kDigits];
+    __shared__ uint32_t dbase[kDigits];
+    __shared__ uint64_t stage[kTile];
+    __shared__ uint16_t stage_e[kTile];
+    const int tid = threadIdx.x;
+    const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
+    {
+        const uint32_t tot = (tid < kDigits) ? digit_total[tid] : 0u;
+        uint32_t all;
+        const uint32_t b0 = block_excl_scan<kPartBlock>(tot, L.wsum, &all);
+        if (tid < kDigits) dbase[tid] = b0;
+    }
+    const int64_t tbase0 = pack_base32(tin, F);
+    const int64_t tbase1 = fold_base(tin, G);
+    uint32_t nr[kPartItems], nd[kPartItems];
+    auto load = [&](uint32_t it_t) {
+        const uint64_t b = (uint64_t)xcd_swizzle(it_t, ntiles) * kTile;
+        const int nv = (int)min<uint64_t>(kTile, n - b);
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = wb_elem<kPartBlock, kPartItems>(it);
+            nr[it] = (e < nv) ? LD_P(rin32 + b + e) : 0u;
+            nd[it] = (e < nv) ? (uint32_t)din[b + e] : 0u;
+        }
+    };
+    if (blockIdx.x < ntiles) load(blockIdx.x);
+    __syncthreads();                                  // dbase
+    for (uint32_t it_t = blockIdx.x; it_t < ntiles; it_t += gridDim.x) {
+        const uint32_t tile = xcd_swizzle(it_t, ntiles);
+        const uint64_t base = (uint64_t)tile * kTile;
+        const int nvalid = (int)min<uint64_t>(kTile, n - base);
+        uint32_t rec[kPartItems], key[kPartItems], lpos[kPartItems];
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            rec[it] = nr[it];
+            key[it] = nd[it] << shift;
+        }
+        if (it_t + gridDim.x < ntiles) load(it_t + gridDim.x);   // in flight during this tile
+        if (tid < kDigits)
+            goff[tid] = dbase[tid] + blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
+                        tileprefix[(uint64_t)tile * kDigits + tid];
+        rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
+        __syncthreads();   // the counts in `stage` are dead from here on
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int e = wb_elem<kPartBlock, kPartItems>(it);
+            if (e < nvalid) {
+                stage[lpos[it]] = (uint64_t)rec[it] | ((uint64_t)(key[it] >> shift) << 32);
+                stage_e[lpos[it]] = (uint16_t)e;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const int j = it * kPartBlock + tid;
+            if (j < nvalid) {
+                const uint64_t sv = stage[j];
+                const uint32_t d = (uint32_t)(sv >> 32) & (kDigits - 1);
+                const uint32_t gp = goff[d] + (uint32_t)j - L.lstart[d];
+                rout[gp] = fold_rec32((uint32_t)sv, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G);
+            }
+        }
+        __syncthreads();   // stage[] and goff[] are reused by the next tile
+    }
+}
+
 // Decide every request of one bucket (see file header).  res[q] is the packed reply of
 // sorted request q (bit 31 granted, bits 0-30 remaining).
 //
@@ -4855,6 +4938,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 keys, permits, ts, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
                 nullptr, FoldFmt{}, dnext, nullptr, w.ts0);
+        else if (e->packed && G.on && p == e->passes - 1 && pf.n0 && TBE_LAST_PERSIST > 0)
+            k_scatter_last_p<<<std::min<unsigned>(ntiles, TBE_LAST_PERSIST), kPartBlock, 0, sp>>>(
+                reinterpret_cast<const uint32_t *>(w.pass[p - 1].rec), w.dig1, n, shift, pf, out.tileprefix,
+                out.blockprefix, out.digit_total, tpb, out.rec, ts, G);
         else if (e->packed && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, pf, out.tileprefix,

@@ -207,6 +207,16 @@ VARIANT_SETS = {
         "digold_z": (["TBE_HIST_DIG_WAVE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "n0off_z": (["TBE_NARROW0=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
+    "r05b": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "split8_u": (["ENV:TBE_CU_SPLIT=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "split4_u": (["ENV:TBE_CU_SPLIT=4"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "split2_u": (["ENV:TBE_CU_SPLIT=2"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "lastp512_u": (["TBE_LAST_PERSIST=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "split4_z": (["ENV:TBE_CU_SPLIT=4"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "lastp512_z": (["TBE_LAST_PERSIST=512"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
@@ -218,7 +228,18 @@ VARIANT_SETS = {
 VARIANTS = VARIANT_SETS[os.environ.get("ABLATE_SET", "queue")]
 
 
+def _build_defs(defs):
+    """Compiler defines of a variant; entries "ENV:NAME=VALUE" are run-time environment
+    settings of the child process instead (e.g. ENV:TBE_CU_SPLIT=4) and share the base build."""
+    return [d for d in defs if not d.startswith("ENV:")]
+
+
+def _env_defs(defs):
+    return dict(d[4:].split("=", 1) for d in defs if d.startswith("ENV:"))
+
+
 def lib_path(defs, patch=None):
+    defs = _build_defs(defs)
     tag = "_".join(defs).replace("=", "") or "base"
     if patch:
         tag = os.path.splitext(os.path.basename(patch))[0] + ("_" + tag if defs else "")
@@ -249,7 +270,7 @@ def build():
     spec.loader.exec_module(m)
     os.makedirs(OUTDIR, exist_ok=True)
     for name, v in VARIANTS.items():
-        defs, patch = v[0], (v[2] if len(v) > 2 else None)
+        defs, patch = _build_defs(v[0]), (v[2] if len(v) > 2 else None)
         lib = lib_path(defs, patch)
         if patch:
             build_patched(m, defs, patch, lib)
@@ -263,7 +284,7 @@ def run(rounds: int, steps: int):
     for r in range(rounds):
         for name, v in VARIANTS.items():
             defs, extra = v[0], v[1]
-            env = dict(os.environ, TBE_LIB=lib_path(defs, v[2] if len(v) > 2 else None))
+            env = dict(os.environ, TBE_LIB=lib_path(defs, v[2] if len(v) > 2 else None), **_env_defs(defs))
             args = ["--steps", str(steps), "--cpu-seconds", "0"] + ([] if "--no-strdir" in extra else ["--no-host-buffer", "--no-strdir"])
             if "--warmup" not in extra:
                 args += ["--warmup", "3"]
