@@ -536,175 +536,6 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
     }
 }
 
-// k_hist_dig's work with one WAVE per tile and one barrier per block (round 5).  k_hist_dig
-// walks its block's tiles one after another, three barriers and one memory round trip per
-// tile: 63 us per config-B batch for 64 MB of digits, latency-bound.  Here every wave
-// issues the loads of all its tiles at once (lane l reads 16-byte pieces of the tile), counts
-// each tile into its own LDS histogram (wave-private, no barrier), and one barrier later
-// the 256 digit-owner threads turn the block's tile histograms into the running prefixes
-// (tileprefix), the block's totals and the per-bucket counts.  A tile inside one pass-0
-// digit (the common case: pass 0's output is sorted by it) adds its histogram to the
-// buckets (d1 << 8) | d0 through the digit owners' running sums; a tile that straddles pass-0
-// digits is counted per pass-0 segment by its wave (global atomics).
-#ifndef TBE_HIST_DIG_WAVE
-#define TBE_HIST_DIG_WAVE 0                  // A/B: 0.077 against 0.063 ms for k_hist_dig (profiles/r05e_*)
-#endif
-typedef uint32_t dg4_t __attribute__((ext_vector_type(4)));   // 16 digit bytes
-constexpr int kDigWTiles = 32;                       // tiles per block per round (LDS: 32 KB of histograms)
-constexpr int kDigWPer = kDigWTiles / (kHBlock / 64);   // tiles per wave per round
-__global__ __launch_bounds__(kHBlock, 4) void k_hist_dig_w(
-    const uint8_t *__restrict__ dig, uint64_t n, uint32_t tiles_per_blk, uint32_t ntiles,
-    uint32_t *__restrict__ tileprefix, uint32_t *__restrict__ blocksum,
-    const uint32_t *__restrict__ dtot0, uint32_t *__restrict__ bcount, uint32_t nbt) {
-    __shared__ uint32_t th[kDigWTiles][kDigits];
-    __shared__ uint32_t dstart[kDigits + 1];
-    __shared__ uint32_t wsum[kHBlock / 64];
-    __shared__ uint32_t tlo[kDigWTiles];             // a tile's pass-0 digit, or 0xFFFFFFFF if it straddles
-    __shared__ uint32_t seg1[kHBlock / 64][kDigits]; // per wave: a straddling tile's first pass-0 segment
-    static_assert(kDigWPer * (kHBlock / 64) == kDigWTiles && kTile == 4096, "16-byte pieces: 4 per lane per tile");
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const bool own = tid < kDigits;
-    {
-        uint32_t all;
-        const uint32_t pre = block_excl_scan<kHBlock>(own ? dtot0[tid] : 0u, wsum, &all);
-        if (own) dstart[tid] = pre;
-        if (tid == 0) dstart[kDigits] = 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    auto d0_of = [&](uint32_t i) {
-        uint32_t lo = 0, hi = kDigits;               // dstart[lo] <= i < dstart[hi]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (dstart[mid] <= i) lo = mid;
-            else hi = mid;
-        }
-        return lo;
-    };
-    const uint32_t t0 = blockIdx.x * tiles_per_blk;
-    const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
-    uint32_t run = 0, acc = 0, acc_lo = 0;
-    // one tile's 4096 digits as 4 x 16 bytes per lane (lane l: bytes q*1024 + l*16 .. +16)
-    auto load_tile = [&](uint32_t t, dg4_t (&v)[4]) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            v[q] = dg4_t{0u, 0u, 0u, 0u};
-            const uint64_t i = (uint64_t)t * kTile + (uint64_t)q * 1024 + (uint64_t)lane * 16;
-            if (t < t1 && i < n) {
-                if (i + 16 <= n) {
-                    v[q] = LD_P(reinterpret_cast<const dg4_t *>(dig + i));
-                } else {
-#pragma unroll
-                    for (int x = 0; x < 16; ++x)
-                        if (i + x < n) v[q][x >> 2] |= (uint32_t)dig[i + x] << (8 * (x & 3));
-                }
-            }
-        }
-    };
-    for (uint32_t r0 = t0; r0 < t1; r0 += kDigWTiles) {
-        const uint32_t nt = min<uint32_t>(kDigWTiles, t1 - r0);
-        // this wave's tiles r0 + w * kDigWPer + u, the next one's loads in flight while one is counted
-        dg4_t v[4], vn[4];
-        load_tile(r0 + (uint32_t)(w * kDigWPer), vn);
-        for (int u = 0; u < kDigWPer; ++u) {
-            const uint32_t li = (uint32_t)(w * kDigWPer + u);
-            if (li >= nt) break;                     // wave-uniform
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = vn[q];
-            if (u + 1 < kDigWPer && li + 1 < nt) load_tile(r0 + li + 1, vn);
-            uint32_t *h = th[li];
-            uint32_t *s1 = seg1[w];
-            const uint64_t base = (uint64_t)(r0 + li) * kTile;
-            const uint32_t cnt = (uint32_t)min<uint64_t>(kTile, n - base);
-            const uint32_t lo0 = d0_of((uint32_t)base), lo1 = d0_of((uint32_t)(base + cnt - 1));
-            // two pass-0 segments (the usual straddle): count the first apart, the second is
-            // the rest; more (sparse batches: small pass-0 digits): each request on its own
-            const uint32_t split = (lo1 == lo0 + 1) ? dstart[lo1] - (uint32_t)base : 0u;
-#pragma unroll
-            for (int x = 0; x < kDigits / 64; ++x) {
-                h[x * 64 + lane] = 0;
-                s1[x * 64 + lane] = 0;
-            }
-            if (lane == 0) tlo[li] = (lo0 == lo1) ? lo0 : 0xFFFFFFFFu;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                // runs of one digit in this lane's 16 consecutive requests take one atomic
-                // (a hot key's tiles are nearly all one digit)
-                const uint32_t off0 = (uint32_t)q * 1024 + (uint32_t)lane * 16;
-                uint32_t rd = 0xFFFFFFFFu, rc = 0;
-#pragma unroll
-                for (int bt = 0; bt < 16; ++bt) {
-                    const uint32_t d = (v[q][bt >> 2] >> (8 * (bt & 3))) & (kDigits - 1);
-                    if (off0 + bt < cnt) {
-                        if (d != rd) {
-                            if (rc) atomicAdd(&h[rd], rc);
-                            rd = d;
-                            rc = 0;
-                        }
-                        ++rc;
-                    }
-                }
-                if (rc) atomicAdd(&h[rd], rc);
-            }
-            if (lo1 != lo0) {
-                // a tile across pass-0 digits (rare in dense batches: <= 255 of them)
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t off0 = (uint32_t)q * 1024 + (uint32_t)lane * 16;
-                    for (int bt = 0; bt < 16; ++bt) {
-                        const uint32_t off = off0 + bt;
-                        if (off >= cnt) break;
-                        const uint32_t d = (v[q][bt >> 2] >> (8 * (bt & 3))) & (kDigits - 1);
-                        if (split != 0u) {
-                            if (off < split) atomicAdd(&s1[d], 1u);
-                        } else {
-                            const uint32_t pos = (uint32_t)(base + off);
-                            uint32_t lo = lo0;
-                            while (dstart[lo + 1] <= pos) ++lo;
-                            const uint32_t bk = (d << kDigitBits) | lo;
-                            if (bk < nbt) atomicAdd(&bcount[bk], 1u);
-                        }
-                    }
-                }
-            }
-            if (lo1 == lo0 + 1) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-                for (int x = 0; x < kDigits / 64; ++x) {
-                    const uint32_t d = (uint32_t)(x * 64 + lane);
-                    const uint32_t a = s1[d], b = h[d] - a;
-                    const uint32_t bk0 = (d << kDigitBits) | lo0, bk1 = (d << kDigitBits) | lo1;
-                    if (a && bk0 < nbt) atomicAdd(&bcount[bk0], a);
-                    if (b && bk1 < nbt) atomicAdd(&bcount[bk1], b);
-                }
-            }
-        }
-        __syncthreads();                              // every tile histogram of the round
-        if (own) {
-            for (uint32_t li = 0; li < nt; ++li) {
-                const uint32_t c = th[li][tid];
-                tileprefix[(uint64_t)(r0 + li) * kDigits + tid] = run;
-                run += c;
-                const uint32_t lo = tlo[li];
-                if (lo != 0xFFFFFFFFu) {
-                    if (lo != acc_lo) {
-                        const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
-                        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
-                        acc = 0;
-                        acc_lo = lo;
-                    }
-                    acc += c;
-                }
-            }
-        }
-        __syncthreads();                              // th[] and tlo[] are free for the next round
-    }
-    if (own) {
-        const uint32_t bk = ((uint32_t)tid << kDigitBits) | acc_lo;
-        if (acc && bk < nbt) atomicAdd(&bcount[bk], acc);
-        blocksum[(uint64_t)blockIdx.x * kDigits + tid] = run;
-    }
-}
-
 // Digit-column scan, one workgroup per digit d: blockprefix[j][d] = number of digit-d
 // elements in blocks < j; digit_total[d] = all of them.  The digit bases (exclusive scan
 // of digit_total) are formed by each consumer workgroup itself.
@@ -1353,89 +1184,6 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         }
     }
     if (FIRST && __any(bad) && (tid & 63) == 0) atomicOr(err, 1u);
-}
-
-// The last partition pass of the token-bucket path with narrow pass-0 records, as
-// persistent workgroups (A/B, TBE_LAST_PERSIST = number of workgroups, a multiple of 8):
-// each walks tiles it, it + gridDim, ... of one XCD's range, sets up the digit bases and
-// record bases once, and loads its next tile's records and digit bytes while the current
-// tile is ranked, staged and written.  Same output as k_scatter_rec<false, ..., LAST>.
-#ifndef TBE_LAST_PERSIST
-#define TBE_LAST_PERSIST 0
-#endif
-#ifndef TBE_LAST_PERSIST_WAVES
-#define TBE_LAST_PERSIST_WAVES 4                 // 2 workgroups per CU; 5 spills 16 VGPRs
-#endif
-__global__ __launch_bounds__(kPartBlock, TBE_LAST_PERSIST_WAVES) void k_scatter_last_p(
-    const uint32_t *__restrict__ rin32, const uint8_t *__restrict__ din, uint64_t n, int shift, PackFmt F,
-    const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
-    const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint64_t *__restrict__ rout,
-    const int64_t *__restrict__ tin, FoldFmt G) {
-    __shared__ RankLds<kPartBlock> L;
-    __shared__ uint32_t goff[kDigits];
-    __shared__ uint32_t dbase[kDigits];
-    __shared__ uint64_t stage[kTile];
-    __shared__ uint16_t stage_e[kTile];
-    const int tid = threadIdx.x;
-    const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
-    {
-        const uint32_t tot = (tid < kDigits) ? digit_total[tid] : 0u;
-        uint32_t all;
-        const uint32_t b0 = block_excl_scan<kPartBlock>(tot, L.wsum, &all);
-        if (tid < kDigits) dbase[tid] = b0;
-    }
-    const int64_t tbase0 = pack_base32(tin, F);
-    const int64_t tbase1 = fold_base(tin, G);
-    uint32_t nr[kPartItems], nd[kPartItems];
-    auto load = [&](uint32_t it_t) {
-        const uint64_t b = (uint64_t)xcd_swizzle(it_t, ntiles) * kTile;
-        const int nv = (int)min<uint64_t>(kTile, n - b);
-#pragma unroll
-        for (int it = 0; it < kPartItems; ++it) {
-            const int e = wb_elem<kPartBlock, kPartItems>(it);
-            nr[it] = (e < nv) ? LD_P(rin32 + b + e) : 0u;
-            nd[it] = (e < nv) ? (uint32_t)din[b + e] : 0u;
-        }
-    };
-    if (blockIdx.x < ntiles) load(blockIdx.x);
-    __syncthreads();                                  // dbase
-    for (uint32_t it_t = blockIdx.x; it_t < ntiles; it_t += gridDim.x) {
-        const uint32_t tile = xcd_swizzle(it_t, ntiles);
-        const uint64_t base = (uint64_t)tile * kTile;
-        const int nvalid = (int)min<uint64_t>(kTile, n - base);
-        uint32_t rec[kPartItems], key[kPartItems], lpos[kPartItems];
-#pragma unroll
-        for (int it = 0; it < kPartItems; ++it) {
-            rec[it] = nr[it];
-            key[it] = nd[it] << shift;
-        }
-        if (it_t + gridDim.x < ntiles) load(it_t + gridDim.x);   // in flight during this tile
-        if (tid < kDigits)
-            goff[tid] = dbase[tid] + blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
-                        tileprefix[(uint64_t)tile * kDigits + tid];
-        rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
-        __syncthreads();   // the counts in `stage` are dead from here on
-#pragma unroll
-        for (int it = 0; it < kPartItems; ++it) {
-            const int e = wb_elem<kPartBlock, kPartItems>(it);
-            if (e < nvalid) {
-                stage[lpos[it]] = (uint64_t)rec[it] | ((uint64_t)(key[it] >> shift) << 32);
-                stage_e[lpos[it]] = (uint16_t)e;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < kPartItems; ++it) {
-            const int j = it * kPartBlock + tid;
-            if (j < nvalid) {
-                const uint64_t sv = stage[j];
-                const uint32_t d = (uint32_t)(sv >> 32) & (kDigits - 1);
-                const uint32_t gp = goff[d] + (uint32_t)j - L.lstart[d];
-                rout[gp] = fold_rec32((uint32_t)sv, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G);
-            }
-        }
-        __syncthreads();   // stage[] and goff[] are reused by the next tile
-    }
 }
 
 // Decide every request of one bucket (see file header).  res[q] is the packed reply of
@@ -4878,9 +4626,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                                        w.blocksum, e->cfg.n_keys, w.err, 1, kmask,
                                                        nullptr, e->nbuckets, e->r_bits, bc, lowbits,
                                                        e->nb_total, dig);
-        else if (e->dig1 && p == 1 && TBE_HIST_DIG_WAVE)
-            k_hist_dig_w<<<nblk, kHBlock, 0, sp>>>(w.dig1, n, tpb, ntiles, out.tileprefix, w.blocksum,
-                                                   w.pass[0].digit_total, bc, e->nb_total);
         else if (e->dig1 && p == 1)
             k_hist_dig<<<nblk, kHBlock, 0, sp>>>(w.dig1, n, tpb, ntiles, out.tileprefix, w.blocksum,
                                                  w.pass[0].digit_total, bc, e->nb_total);
@@ -4938,10 +4683,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 keys, permits, ts, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
                 nullptr, FoldFmt{}, dnext, nullptr, w.ts0);
-        else if (e->packed && G.on && p == e->passes - 1 && pf.n0 && TBE_LAST_PERSIST > 0)
-            k_scatter_last_p<<<std::min<unsigned>(ntiles, TBE_LAST_PERSIST), kPartBlock, 0, sp>>>(
-                reinterpret_cast<const uint32_t *>(w.pass[p - 1].rec), w.dig1, n, shift, pf, out.tileprefix,
-                out.blockprefix, out.digit_total, tpb, out.rec, ts, G);
         else if (e->packed && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, pf, out.tileprefix,
@@ -5308,30 +5049,11 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         return bail(TBE_EDEVICE);
     }
     e->pipeline = c.kind == TBE_KIND_TOKEN_BUCKET && (c.flags & TBE_FLAG_NO_PIPELINE) == 0;
-    // CU split (A/B, env TBE_CU_SPLIT = d in {2, 4, 8}): the partition stream gets 1/d of the
-    // CUs and the fold stream the rest, so batch b+1's bandwidth-bound partition runs beside
-    // batch b's latency-bound fold instead of waiting for CUs the fold's LDS fills.  CU i goes
-    // to the partition when (i / 8 + i) % d == 0: 1/d of every XCD whether CU ids are
-    // contiguous per XCD or interleaved across XCDs.
-    int cu_split = 0;
-    if (const char *cs = std::getenv("TBE_CU_SPLIT")) cu_split = std::atoi(cs);
-    if (e->pipeline && (cu_split == 2 || cu_split == 4 || cu_split == 8)) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, e->device) != hipSuccess) return bail(TBE_EDEVICE);
-        const int ncu = prop.multiProcessorCount;
-        std::vector<uint32_t> mp((ncu + 31) / 32, 0u), mf((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i) ((i / 8 + i) % cu_split == 0 ? mp : mf)[i / 32] |= 1u << (i % 32);
-        if (hipExtStreamCreateWithCUMask(&e->stream, (uint32_t)mf.size(), mf.data()) != hipSuccess ||
-            hipExtStreamCreateWithCUMask(&e->pstream, (uint32_t)mp.size(), mp.data()) != hipSuccess)
-            return bail(TBE_EDEVICE);
-        e->own_stream = true;
-    } else {
-        if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
-            return bail(TBE_EDEVICE);
-        e->own_stream = true;
-        if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
-            return bail(TBE_EDEVICE);
-    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(TBE_EDEVICE);
+    e->own_stream = true;
+    if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess)
+        return bail(TBE_EDEVICE);
     if (e->pipeline && hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess)
         return bail(TBE_EDEVICE);
     for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ev_hot, &e->ws[0].done, &e->ws[1].done,

@@ -199,24 +199,6 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
-    "r05": {
-        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "digold_u": (["TBE_HIST_DIG_WAVE=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "n0off_u": (["TBE_NARROW0=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "digold_z": (["TBE_HIST_DIG_WAVE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "n0off_z": (["TBE_NARROW0=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-    },
-    "r05b": {
-        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "split8_u": (["ENV:TBE_CU_SPLIT=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "split4_u": (["ENV:TBE_CU_SPLIT=4"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "split2_u": (["ENV:TBE_CU_SPLIT=2"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "lastp512_u": (["TBE_LAST_PERSIST=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "split4_z": (["ENV:TBE_CU_SPLIT=4"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "lastp512_z": (["TBE_LAST_PERSIST=512"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
