@@ -846,10 +846,6 @@ struct PackFmt {
     int32_t n0;         // 1: pass 0 writes narrow records
     int32_t rb;         // row bits (r_bits) of a narrow record
     int32_t w0;         // time-offset bits of a narrow record
-    // 1: pass 0's permutation holds each request's u16 tile-local staging position for
-    // k_unscatter_runs instead of its u32 output position (set per batch by run_batch,
-    // together with the choice of that final un-partition: one flag decides both)
-    int32_t run_inv;
 };
 __device__ __forceinline__ int64_t pack_base32(const int64_t *__restrict__ ts, const PackFmt &F) {
     return ts[0] - ((int64_t)1 << (F.w0 - 1));
@@ -999,9 +995,6 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 #ifndef TBE_LAST_PRESTAGE
 #define TBE_LAST_PRESTAGE 0                  // A/B: fold records formed before staging
 #endif
-#ifndef TBE_UNSCATTER_RUNS
-#define TBE_UNSCATTER_RUNS 1                 // pass 0's inverse by runs (k_unscatter_runs); 0: A/B
-#endif
 #ifndef TBE_BSCAN_LB
 #define TBE_BSCAN_LB 1                       // bucket starts by decoupled look-back; 0: one workgroup (A/B)
 #endif
@@ -1134,8 +1127,6 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
             if (LAST)
                 stage_e[lpos[it]] = (uint16_t)e;
 #endif
-            else if (perm && F.run_inv)   // tile-local staging position (k_unscatter_runs)
-                ST_PERM(reinterpret_cast<uint16_t *>(perm) + base + e, (uint16_t)lpos[it]);
             else if (perm)   // (null: k_unrank recomputes the positions)
                 ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
             if (FIRST && n0 && ((rec[it] >> 48) & 1u))   // escaped: its time beside its position
@@ -2407,77 +2398,6 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
         } else {
             ST_U(granted + i, (uint8_t)(r[it] >> 31));
             ST_U(remaining + i, (int32_t)(r[it] & 0x7FFFFFFFu));
-        }
-    }
-}
-
-// Pass 0's inverse by runs (round 5; token bucket with narrow pass-0 records, one-byte
-// replies).  The element-wise inverse (k_unscatter) gathers one reply byte per request
-// through the 4-byte permutation: consecutive requests sit in different digit runs, so a
-// wave's 64 gathers touch ~64 cache lines -- the kernel is bound by those transactions,
-// not by bytes.  Here one workgroup per pass-0 tile rebuilds the tile's staging buffer: run
-// d of the tile (the replies of its digit-d requests, contiguous in pass 0's output at
-// goff[d], cnt[d] of them) is read in staging order, so a wave's reads cover a few runs and
-// a few lines; then each request takes its reply from LDS at the tile-local staging
-// position pass 0 stored as a 2-byte permutation, and granted/remaining leave coalesced.
-// goff and cnt follow from pass 0's own prefix arrays (cnt[d] = the next tile's goff[d] -
-// goff[d]; the last tile ends at the digit's end).
-__global__ __launch_bounds__(kPartBlock) void k_unscatter_runs(
-    uint64_t n, const uint16_t *__restrict__ lpos16, const uint8_t *__restrict__ res,
-    const uint32_t *__restrict__ tileprefix, const uint32_t *__restrict__ blockprefix,
-    const uint32_t *__restrict__ digit_total, uint32_t tiles_per_blk, uint8_t *__restrict__ granted,
-    int32_t *__restrict__ remaining, const uint32_t *__restrict__ err, uint32_t *__restrict__ sticky) {
-    __shared__ uint32_t goff[kDigits], lstart[kDigits + 1];
-    __shared__ uint32_t wsum[kPartBlock / 64];
-    __shared__ uint8_t stage[kTile];
-    const int tid = threadIdx.x;
-    if (sticky && blockIdx.x == 0 && tid == 0 && *err) *sticky = 1u;
-    const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
-    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kTile;
-    const int nvalid = (int)min<uint64_t>(kTile, n - base);
-    // digit bases (exclusive scan of the digit totals), this tile's run starts and lengths
-    const uint32_t tot = (tid < kDigits) ? digit_total[tid] : 0u;
-    uint32_t all;
-    const uint32_t dbase = block_excl_scan<kPartBlock>(tot, wsum, &all);
-    uint32_t cnt = 0;
-    if (tid < kDigits) {
-        const uint32_t g0 = dbase + blockprefix[(uint64_t)(tile / tiles_per_blk) * kDigits + tid] +
-                            tileprefix[(uint64_t)tile * kDigits + tid];
-        const uint32_t g1 = (tile + 1 < ntiles)
-                                ? dbase + blockprefix[(uint64_t)((tile + 1) / tiles_per_blk) * kDigits + tid] +
-                                      tileprefix[(uint64_t)(tile + 1) * kDigits + tid]
-                                : dbase + tot;
-        goff[tid] = g0;
-        cnt = g1 - g0;
-    }
-    const uint32_t ls = block_excl_scan<kPartBlock>(cnt, wsum, &all);
-    if (tid < kDigits) lstart[tid] = ls;
-    if (tid == 0) lstart[kDigits] = 0xFFFFFFFFu;
-    __syncthreads();
-    // the runs, in staging order: staging position j belongs to the last digit whose run
-    // starts at or before j
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int j = it * kPartBlock + tid;
-        if (j < nvalid) {
-            uint32_t lo = 0, hi = kDigits;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (lstart[mid] <= (uint32_t)j) lo = mid;
-                else hi = mid;
-            }
-            stage[j] = LD_U(res + goff[lo] + ((uint32_t)j - lstart[lo]));
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int e = it * kPartBlock + tid;
-        if (e < nvalid) {
-            const uint32_t r = stage[LD_U(lpos16 + base + e)];
-            ST_U(granted + base + e, (uint8_t)(r >> 7));
-            ST_U(remaining + base + e, (int32_t)(r & 0x7Fu));
         }
     }
 }
@@ -4666,10 +4586,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // escaped request's time in ts0 (FoldFmt::n0)
     PackFmt pf = e->pf;
     pf.n0 = G.n0;
-    // pass 0's inverse by runs: token bucket, narrow records, one-byte replies, a stored
-    // permutation.  The same flag makes pass 0 store u16 staging positions and selects
-    // k_unscatter_runs below; every other final un-partition reads u32 positions.
-    pf.run_inv = (TBE_UNSCATTER_RUNS && G.n0 && e->narrow && !e->unrank && !approx && !wait) ? 1 : 0;
     const uint64_t *rec0 = G.on ? (G.n0 ? reinterpret_cast<const uint64_t *>(w.ts0) : w.pass[e->passes - 2].rec)
                                 : nullptr;
     const bool unrank = e->unrank;
@@ -4964,12 +4880,6 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     else if (unrank)
         TBE_UNRANK(k_unrank<4, true>);
 #undef TBE_UNRANK
-    else if (pf.run_inv)
-        k_unscatter_runs<<<ntiles, kPartBlock, 0, sf>>>(n, reinterpret_cast<const uint16_t *>(w.pass[0].perm),
-                                                         reinterpret_cast<const uint8_t *>(w.res[cur]),
-                                                         w.pass[0].tileprefix, w.pass[0].blockprefix,
-                                                         w.pass[0].digit_total, tpb, granted, remaining, w.err,
-                                                         e->sticky);
     else if (e->narrow && !wait && !approx)
         k_unscatter<true, false, 1><<<untiles, kUnBlock, 0, sf>>>(n, w.pass[0].perm, w.res[cur],
                                                                   nullptr, granted, remaining,

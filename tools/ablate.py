@@ -199,12 +199,6 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
-    "unruns": {
-        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "elemwise_u": (["TBE_UNSCATTER_RUNS=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "elemwise_z": (["TBE_UNSCATTER_RUNS=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
