@@ -104,6 +104,8 @@ def parse():
                     help="4-byte replies even where TokenLimit <= 127 allows 1-byte ones (A/B)")
     ap.add_argument("--no-sparse", action="store_true",
                     help="skip the batch-size sweep (2^14 .. 2^26-request batches over config B's keys)")
+    ap.add_argument("--sweep-log2", default=None,
+                    help="comma-separated log2 batch sizes of the sweep (default 14,16,...,26)")
     ap.add_argument("--no-strdir", action="store_true",
                     help="skip the string-key directory leg (config B batches as key text)")
     ap.add_argument("--unscatter-all", action="store_true",
@@ -505,7 +507,8 @@ def main():
     # buckets go one wave each to k_fold_sparse, which gathers only their rows)
     sparse = sweep = None
     if args.workload == "uniform" and rank == 0 and world == 1 and not args.no_sparse:
-        sweep = bench_batch_sweep(args, lib, keys_local, dev)
+        sizes = tuple(int(x) for x in args.sweep_log2.split(",")) if args.sweep_log2 else SWEEP_LOG2
+        sweep = bench_batch_sweep(args, lib, keys_local, dev, sizes)
         sparse = next((x for x in sweep if x["batch"] == 1 << 20), None)
 
     cpu = None
@@ -572,8 +575,10 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
     the host's micro-batching submitter, SURVEY §8(b) threading), after the timed region.
     Per size a fresh engine (pipeline off, one stream) decides warm-up + timed batches of
     uniform keys; reported: decisions/s over the back-to-back timed batches, the per-batch
-    latency (enqueue one batch + synchronise, wall clock, median of 5), and HIP-event stage
-    times.  Sparse batches (below R/32 requests per bucket on average: up to 2^21 here) send
+    latency (enqueue one batch + synchronise, wall clock, median of 5), both on an engine
+    without stage events, and the HIP-event stage times of the same batches on a second
+    engine that records them (at small sizes the ~14 events per batch are themselves a
+    visible share of its time).  Sparse batches (below R/32 requests per bucket on average: up to 2^21 here) send
     their sparse buckets to k_fold_sparse, one wave each; from 2^22 every bucket takes
     k_fold_wide."""
     from distributedratelimiting.redis_amd import TokenBucketEngine
@@ -583,7 +588,8 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
         n = 1 << lg
         warm, timed = (3, 10) if lg <= 22 else (2, 5)
         eng = TokenBucketEngine(n_keys, args.token_limit, args.tokens_per_period, args.period_ticks,
-                                device=dev.index, stage_timing=True, max_batch=n, pipeline=False)
+                                device=dev.index, stage_timing=False, max_batch=n, pipeline=False)
+        sparse = eng.batch_format(n)["sparse"]
         bufs = []
         for s in range(warm + timed + 5):
             k = torch.empty(n, dtype=torch.int64, device=dev)
@@ -599,20 +605,28 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
         for s in range(warm):
             eng.acquire_batch_device(*bufs[s], g, r)
         eng.synchronize()
-        eng.stage_times()
         t0 = time.perf_counter()
         for s in range(warm, warm + timed):
             eng.acquire_batch_device(*bufs[s], g, r)
         eng.synchronize()
         elapsed = time.perf_counter() - t0
-        st = eng.stage_times()
         lat = []
         for s in range(warm + timed, warm + timed + 5):
             t1 = time.perf_counter()
             eng.acquire_batch_device(*bufs[s], g, r)
             eng.synchronize()
             lat.append(time.perf_counter() - t1)
-        eng.stage_times()
+        eng.close()
+        # the same batches on an engine that records stage events
+        eng = TokenBucketEngine(n_keys, args.token_limit, args.tokens_per_period, args.period_ticks,
+                                device=dev.index, stage_timing=True, max_batch=n, pipeline=False)
+        for s in range(warm + timed):
+            if s == warm:
+                eng.synchronize()
+                eng.stage_times()
+            eng.acquire_batch_device(*bufs[s], g, r)
+        eng.synchronize()
+        st = eng.stage_times()
         eng.close()
         del bufs
         out.append({"batch": n, "batches_timed": timed, "ms_per_batch": round(elapsed / timed * 1e3, 4),
@@ -620,7 +634,7 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
                     "latency_ms": round(float(np.median(lat)) * 1e3, 4),
                     "stage_ms_per_batch": {k: round(v / timed, 4) for k, v in st.items()},
                     "fold": ("k_fold_sparse (one wave per sparse bucket) + k_fold_wide (listed dense buckets)"
-                             if n < (-(-n_keys // 2048)) * 64 else "k_fold_wide (every bucket)")})
+                             if sparse else "k_fold_wide (every bucket)")})
     torch.cuda.empty_cache()
     return out
 

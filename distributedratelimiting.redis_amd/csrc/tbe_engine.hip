@@ -46,7 +46,6 @@ using namespace tbe;
 
 namespace {
 
-#ifndef TBE_PART_BLOCK
 // Non-temporal hints where data is touched once (tools/ablate.py A/B, profiles/
 // r01_v10_ablate.log): partition-pass input loads and permutation stores, the
 // un-partition passes, the fold's table slices.  NOT the partition passes' record runs
@@ -79,6 +78,7 @@ namespace {
 #endif
 #define ST_F(p, v) (*(p) = (v))
 
+#ifndef TBE_PART_BLOCK
 #define TBE_PART_BLOCK 512
 #endif
 #ifndef TBE_PART_ITEMS
@@ -417,9 +417,12 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
     __shared__ uint32_t h8[kDigits * 8];
     __shared__ uint32_t dstart[kDigits + 1];
     __shared__ uint32_t wsum[kHBlock / 64];
-    __shared__ uint32_t tile_lo[2];
+    // first and last pass-0 digit of each of the next kHBlock / 2 tiles, found by one
+    // binary search per thread instead of two serial ones per tile
+    __shared__ uint32_t tlo[kHBlock];
     static_assert(kHBlock == 2 * kDigits && kDigits * 8 == 4 * kHBlock, "two threads per digit; 4 counters each");
-    static_assert(kHItems == 8, "one 8-byte load per thread per tile");
+    static_assert(kHItems % 8 == 0, "8-byte loads");
+    constexpr int kW = kHItems / 8;                  // 8-byte words per thread per tile
     const int tid = threadIdx.x;
     const bool own = tid < kDigits;                  // this thread owns digit `tid`'s totals
     {
@@ -441,33 +444,44 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
     const uint32_t t0 = blockIdx.x * tiles_per_blk;
     const uint32_t t1 = min(t0 + tiles_per_blk, ntiles);
     uint32_t run = 0, acc = 0, acc_lo = 0;
-    auto load = [&](uint32_t t) -> uint64_t {
-        const uint64_t i = (uint64_t)t * kTile + (uint64_t)tid * kHItems;
-        if (t >= t1 || i >= n) return 0ull;
-        if (i + kHItems <= n) return LD_P(reinterpret_cast<const uint64_t *>(dig + i));
-        uint64_t v = 0;
-        for (int u = 0; i + u < n; ++u) v |= (uint64_t)dig[i + u] << (8 * u);
-        return v;
+    auto load = [&](uint32_t t, uint64_t (&dst)[kW]) {
+#pragma unroll
+        for (int q = 0; q < kW; ++q) {
+            const uint64_t i = (uint64_t)t * kTile + (uint64_t)tid * kHItems + 8 * q;
+            uint64_t v = 0;
+            if (t < t1 && i + 8 <= n) {
+                v = LD_P(reinterpret_cast<const uint64_t *>(dig + i));
+            } else if (t < t1) {
+                for (int u = 0; i + u < n; ++u) v |= (uint64_t)dig[i + u] << (8 * u);
+            }
+            dst[q] = v;
+        }
     };
-    uint64_t vn = load(t0);
+    uint64_t vn[kW];
+    load(t0, vn);
     __syncthreads();                                 // dstart
     for (uint32_t t = t0; t < t1; ++t) {
-        const uint64_t v = vn;
-        vn = load(t + 1);                            // in flight while this tile is counted
+        uint64_t vw[kW];
+#pragma unroll
+        for (int q = 0; q < kW; ++q) vw[q] = vn[q];
+        load(t + 1, vn);                             // in flight while this tile is counted
 #pragma unroll
         for (int u = 0; u < 4; ++u) h8[u * kHBlock + tid] = 0;
         const uint64_t base = (uint64_t)t * kTile;
-        const uint64_t last = min<uint64_t>(base + kTile, n) - 1;
-        if (tid == 0) {
-            tile_lo[0] = d0_of((uint32_t)base);
-            tile_lo[1] = d0_of((uint32_t)last);
+        const uint32_t tk = (t - t0) % (kHBlock / 2);
+        if (tk == 0) {   // (the previous tile's reads of tlo are behind the loop's last barrier)
+            const uint32_t tt = t + (uint32_t)(tid >> 1);
+            if (tt < t1) {
+                const uint64_t b = (uint64_t)tt * kTile;
+                tlo[tid] = d0_of((uint32_t)((tid & 1) ? min<uint64_t>(b + kTile, n) - 1 : b));
+            }
         }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kHItems; ++u) {
             const uint64_t i = base + (uint64_t)tid * kHItems + u;
             const bool valid = i < n;
-            const uint32_t d = (uint32_t)(v >> (8 * u)) & (kDigits - 1);
+            const uint32_t d = (uint32_t)(vw[u >> 3] >> (8 * (u & 7))) & (kDigits - 1);
             const uint64_t vmask = __ballot(valid);
             const uint32_t dw = __shfl(d, vmask ? __ffsll((long long)vmask) - 1 : 0, 64);
             if (__all(!valid || d == dw)) {
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
             run += c;
         }
         // per-bucket counts, as k_hist's last pass
-        const uint32_t lo0 = tile_lo[0], lo1 = tile_lo[1];
+        const uint32_t lo0 = tlo[2 * tk], lo1 = tlo[2 * tk + 1];
         if (lo0 == lo1) {
             if (own) {
                 if (lo0 != acc_lo) {
@@ -507,7 +521,7 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
                 if (i >= n) continue;
                 uint32_t lo = 0;
                 for (uint32_t x = 1; x <= lo1 - lo0; ++x) lo += dstart[lo0 + x] <= (uint32_t)i;
-                const uint32_t d = (uint32_t)(v >> (8 * u)) & (kDigits - 1);
+                const uint32_t d = (uint32_t)(vw[u >> 3] >> (8 * (u & 7))) & (kDigits - 1);
                 atomicAdd(&h8[lo * kDigits + d], 1u);
             }
             __syncthreads();
@@ -523,7 +537,7 @@ __global__ __launch_bounds__(kHBlock, TBE_HIST_WAVES) void k_hist_dig(
             for (int u = 0; u < kHItems; ++u) {
                 const uint64_t i = base + (uint64_t)tid * kHItems + u;
                 if (i >= n) continue;
-                const uint32_t bk = (((uint32_t)(v >> (8 * u)) & (kDigits - 1)) << kDigitBits) | d0_of((uint32_t)i);
+                const uint32_t bk = (((uint32_t)(vw[u >> 3] >> (8 * (u & 7))) & (kDigits - 1)) << kDigitBits) | d0_of((uint32_t)i);
                 if (bk < nbt) atomicAdd(&bcount[bk], 1u);
             }
         }
@@ -769,9 +783,13 @@ __global__ __launch_bounds__(1024) void k_bscan(const uint32_t *__restrict__ bco
 constexpr int kBsPer = 4;
 constexpr uint32_t kBsTile = 1024u * kBsPer;
 constexpr uint32_t kBsMaxBlocks = 64;        // nb_total <= 2^16 buckets (two 8-bit passes)
+// Sparse batches also list their dense buckets (dlist, as k_bscan; dlist[0] was zeroed with
+// the counts): one global atomic per dense bucket, of which a sparse batch has few.
 __global__ __launch_bounds__(1024) void k_bscan_lb(const uint32_t *__restrict__ bcount, uint32_t nbt,
                                                    uint32_t *__restrict__ bstart,
-                                                   unsigned long long *__restrict__ flags, uint32_t tag) {
+                                                   unsigned long long *__restrict__ flags, uint32_t tag,
+                                                   uint32_t nb = 0, uint32_t wide_min = 0,
+                                                   uint32_t *__restrict__ dlist = nullptr) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t excl;
     const uint32_t t = threadIdx.x, blk = blockIdx.x;
@@ -779,6 +797,11 @@ __global__ __launch_bounds__(1024) void k_bscan_lb(const uint32_t *__restrict__ 
     uint32_t v[kBsPer];
 #pragma unroll
     for (int k = 0; k < kBsPer; ++k) v[k] = (b0 + k < nbt) ? bcount[b0 + k] : 0u;
+    if (dlist) {
+#pragma unroll
+        for (int k = 0; k < kBsPer; ++k)
+            if (b0 + k < nb && v[k] >= wide_min) dlist[1 + atomicAdd(dlist, 1u)] = b0 + k;
+    }
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kBsPer; ++k) sum += v[k];
@@ -2526,6 +2549,8 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
         const uint32_t b = min(a + kSeg, bstart[nb + h + 1]);
         int64_t mx = INT64_MIN;
         int32_t mn = INT32_MAX;
+        // the run's row before the batch, in flight with the records (SPEC)
+        const Slot s0 = SPEC ? table[hot->key[h]] : Slot{0.0, 0};
         uint64_t rv[kSegItems];   // every record of the segment in flight at once
 #pragma unroll
         for (int it = 0; it < kSegItems; ++it) {
@@ -2561,7 +2586,6 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
             summ[j] = SegSummary{mx, mn, 0u};
         }
         if (SPEC) {
-            const Slot s0 = table[hot->key[h]];
             const double ft0 = new_t_of(s0.t_us == kAbsent ? 0 : s0.t_us);
             if (tid == 0) {
                 Slot c = s0;
@@ -4384,7 +4408,7 @@ void free_workspace(Workspace &w) {
     dfree(w.bstart);
     dfree(w.bcount);
     w.err = nullptr;   // (the word after the bucket counts)
-    dfree(w.dlist);
+    w.dlist = nullptr;   // (after err)
     dfree(w.bsflags);
     dfree(w.dig0);
     dfree(w.dig1);
@@ -4440,10 +4464,11 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.res[0], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.res[1], cap * sizeof(uint32_t)));
     HIP_TRY(e, hipMalloc(&w.bstart, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
-    // the batch's error flag is the word after its bucket counts: one memset clears both
-    HIP_TRY(e, hipMalloc(&w.bcount, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t)));
+    // the batch's error flag is the word after its bucket counts and the dense-bucket list
+    // (sparse batches) follows it: one memset clears the counts, the flag and the list's count
+    HIP_TRY(e, hipMalloc(&w.bcount, ((uint64_t)e->nb_total + 2 + e->nbuckets) * sizeof(uint32_t)));
     w.err = w.bcount + e->nb_total;
-    HIP_TRY(e, hipMalloc(&w.dlist, ((uint64_t)e->nbuckets + 1) * sizeof(uint32_t)));
+    w.dlist = w.bcount + e->nb_total + 1;
     HIP_TRY(e, hipMalloc(&w.bsflags, kBsMaxBlocks * sizeof(unsigned long long)));
     HIP_TRY(e, hipMemset(w.bsflags, 0, kBsMaxBlocks * sizeof(unsigned long long)));
     HIP_TRY(e, hipDeviceSynchronize());   // (allocation time only) zeroed before any stream reads it
@@ -4494,6 +4519,9 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 // of at least the returned number of requests, k_fold the rest (launched only when this is
 // above 1).  Dense batches give every nonempty bucket to k_fold_wide; sparse ones only the
 // buckets of >= R/8 requests.  TBE_FOLD_NARROW_ONLY (A/B): k_fold takes every bucket.
+#ifndef TBE_SPARSE_GATE_SHIFT
+#define TBE_SPARSE_GATE_SHIFT 5              // sparse batch: fewer than R >> this requests per bucket
+#endif
 uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #ifdef TBE_FOLD_NARROW_ONLY
     (void)e;
@@ -4502,7 +4530,7 @@ uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #else
     const uint32_t R = 1u << e->r_bits;
     const uint32_t all = std::max(1u, R >> kWideMinShift);
-    if (n >= (uint64_t)e->nbuckets * std::max(1u, R >> 5)) return all;
+    if (n >= (uint64_t)e->nbuckets * std::max(1u, R >> TBE_SPARSE_GATE_SHIFT)) return all;
     return std::max(all, R >> 3);
 #endif
 }
@@ -4578,7 +4606,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     } else if (in_ready) {            // chunked host-buffer path (queueing / approximate)
         HIP_TRY(e, hipStreamWaitEvent(sf, in_ready, 0));
     }
-    HIP_TRY(e, hipMemsetAsync(w.bcount, 0, ((uint64_t)e->nb_total + 1) * sizeof(uint32_t), sp));   // + err
+    HIP_TRY(e, hipMemsetAsync(w.bcount, 0, ((uint64_t)e->nb_total + 2) * sizeof(uint32_t), sp));   // + err, dlist[0]
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
     const FoldFmt G = batch_fold_fmt(e, n);
@@ -4590,9 +4618,18 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                                 : nullptr;
     const bool unrank = e->unrank;
     const unsigned fold_grid = G.on ? (unsigned)((1ull << G.region_bits) * G.n_hi) : e->nbuckets;
-    // hot runs: see tbe_engine::hot
-    HotSet *hot = e->hot_cap ? e->hot[e->nbatch % 3] : nullptr;
-    HotSet *hot_next = e->hot_cap ? e->hot[(e->nbatch + 2) % 3] : nullptr;
+    // token bucket: a sparse batch's dense buckets are listed for k_fold_wide, the rest go to
+    // one wave each (k_fold_sparse)
+    const uint32_t tb_wmin = (!approx && !wait) ? fold_wide_min(e, n) : 1u;
+    const bool sparse_tb = TBE_SPARSE_WAVE && tb_wmin > 1u;
+    // hot runs: see tbe_engine::hot.  Not in a sparse batch (the micro-batch regime): a key
+    // busy enough to matter fills one dense bucket, which k_fold_wide takes whole, and the
+    // hot machinery (its LDS tables in the first pass, four launches) costs more than it
+    // saves there.  Which keys are hot never changes a decision; the hot sets keep their
+    // contents for the next dense batch.
+    const bool hot_on = e->hot_cap && !sparse_tb;
+    HotSet *hot = hot_on ? e->hot[e->nbatch % 3] : nullptr;
+    HotSet *hot_next = hot_on ? e->hot[(e->nbatch + 2) % 3] : nullptr;
 #if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
     // every batch: its dominant keys join its own hot set (k_hot_sample)
     if (hot && n >= kHotSampleMin) k_hot_sample<<<1, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, hot, e->hot_cap);
@@ -4722,17 +4759,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         stage_end(e, ST_SCATTER, sp);
     }
     const PassBufs &sorted = w.pass[e->passes - 1];
-    // token bucket: a sparse batch's dense buckets are listed for k_fold_wide, the rest go to
-    // one wave each (k_fold_sparse)
-    const uint32_t tb_wmin = (!approx && !wait) ? fold_wide_min(e, n) : 1u;
-    const bool sparse_tb = TBE_SPARSE_WAVE && tb_wmin > 1u;
     stage_begin(e, ST_BOUNDS, sp);
     const uint32_t bs_blocks = (e->nb_total + kBsTile - 1) / kBsTile;
-    if (sparse_tb)
-        k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, e->nbuckets, tb_wmin, w.dlist);
-    else if (TBE_BSCAN_LB && bs_blocks <= kBsMaxBlocks)
+    if (TBE_BSCAN_LB && bs_blocks <= kBsMaxBlocks)
         k_bscan_lb<<<bs_blocks, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, w.bsflags,
-                                               (uint32_t)(e->nbatch + 1));
+                                               (uint32_t)(e->nbatch + 1), e->nbuckets, tb_wmin,
+                                               sparse_tb ? w.dlist : nullptr);
+    else if (sparse_tb)
+        k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, e->nbuckets, tb_wmin, w.dlist);
     else
         k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart);
     stage_end(e, ST_BOUNDS, sp);
@@ -6105,6 +6139,10 @@ tbe_status tbe_batch_format(const tbe_engine *e, uint64_t n, uint32_t *out, uint
     out[5] = (uint32_t)e->pf.pb;                   // permit-code bits
     out[6] = (uint32_t)(G.n0 ? e->pf.w0 : e->pf.wb);   // pass-0 time-offset bits (narrow records: w0)
     out[7] = (uint32_t)e->r_bits;
+    if (n_out > 8) {   // 1: a sparse token-bucket batch (k_fold_sparse + listed dense buckets, no hot runs)
+        const bool tb = e->cfg.kind == TBE_KIND_TOKEN_BUCKET;
+        out[8] = (tb && TBE_SPARSE_WAVE && fold_wide_min(e, n) > 1u) ? 1u : 0u;
+    }
     return TBE_OK;
 }
 

@@ -188,11 +188,11 @@ class TokenBucketEngine:
 
     def batch_format(self, n: int) -> dict:
         """The record layout a batch of n requests takes (tbe_batch_format)."""
-        out = (c_uint32 * 8)()
-        self._check(self._lib.tbe_batch_format(self.handle, n, out, 8))
+        out = (c_uint32 * 9)()
+        self._check(self._lib.tbe_batch_format(self.handle, n, out, 9))
         names = ("passes", "fold_records", "position_bits", "fold_time_bits", "key_bits", "permit_bits",
-                 "pass0_time_bits", "r_bits")
-        return {k: (bool(out[i]) if k == "fold_records" else out[i]) for i, k in enumerate(names)}
+                 "pass0_time_bits", "r_bits", "sparse")
+        return {k: (bool(out[i]) if k in ("fold_records", "sparse") else out[i]) for i, k in enumerate(names)}
 
     def stage_times(self) -> dict:
         out = (c_double * len(_capi.STAGES))()

@@ -374,8 +374,11 @@ tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bi
  * out[0] partition passes, out[1] 1 if the last pass writes fold records, out[2] their
  * reply-position bits (ceil_log2 n), out[3] their time-offset bits, out[4] the pass-0
  * record's key bits, out[5] permit-code bits, out[6] pass-0 time-offset bits, out[7]
- * r_bits.  n_out must be >= 8.  A request whose time offset does not fit takes the
- * escape form (its time is read from the previous record / the caller's array). */
+ * r_bits, and when n_out > 8, out[8] 1 if the batch is a sparse token-bucket batch
+ * (fewer than 64 requests per bucket on average: one wave per sparse bucket, the dense
+ * buckets listed for the wide fold, no hot-key runs).  n_out must be >= 8.  A request
+ * whose time offset does not fit takes the escape form (its time is read from the
+ * previous record / the caller's array). */
 tbe_status tbe_batch_format(const tbe_engine *engine, uint64_t n, uint32_t *out, uint32_t n_out);
 
 /* Per-stage device time (ms) accumulated since the last call, when

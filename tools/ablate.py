@@ -199,6 +199,11 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "gate": {
+        "gate5_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
+        "gate4_u": (["TBE_SPARSE_GATE_SHIFT=4"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
+        "gate3_u": (["TBE_SPARSE_GATE_SHIFT=3"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),
