@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate CPU-baseline budget (0 disables)")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--timed-stage-events", action="store_true",
+                    help="record the stage events in the timed (pipelined) engine too (A/B: each "
+                         "event record costs the stream a bubble; by default the stage times come "
+                         "from the serial replay alone)")
     ap.add_argument("--no-host-buffer", action="store_true",
                     help="skip the host-buffer (PCIe-inclusive) rate, e.g. under rocprofv3 so the "
                          "kernel statistics cover the timed batches only")
@@ -106,6 +110,8 @@ def parse():
                     help="skip the batch-size sweep (2^14 .. 2^26-request batches over config B's keys)")
     ap.add_argument("--sweep-log2", default=None,
                     help="comma-separated log2 batch sizes of the sweep (default 14,16,...,26)")
+    ap.add_argument("--sweep-zipf", action="store_true",
+                    help="the sweep's batches draw Zipf(--zipf-s) keys instead of uniform ones (A/B)")
     ap.add_argument("--no-strdir", action="store_true",
                     help="skip the string-key directory leg (config B batches as key text)")
     ap.add_argument("--unscatter-all", action="store_true",
@@ -282,9 +288,14 @@ def main():
     torch.cuda.synchronize()
     sizes = [b[0].numel() for b in bufs] or [n]
     m_max = max(sizes)
+    # Stage events in the timed engine only when no serial replay follows to take the stage
+    # times from (routed batches, or no pipeline): an event record between two kernels leaves
+    # the stream idle for several microseconds (profiles/r05n_*), ~14 of them per batch.
+    replay = not args.no_pipeline and not args.no_stage_timing and not (routed and args.route != "pre")
     eng = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                             args.period_ticks, device=dev.index,
-                            stage_timing=not args.no_stage_timing, max_batch=m_max,
+                            stage_timing=not args.no_stage_timing and (not replay or args.timed_stage_events),
+                            max_batch=m_max,
                             pack=not args.no_pack, hot=not args.no_hot, narrow=not args.no_narrow,
                             pipeline=not args.no_pipeline, fold_records=not args.unscatter_all,
                             digit_stream=not args.hist_records, rerank=args.rerank)
@@ -360,7 +371,7 @@ def main():
     # right after the timed region; its replies must equal the pipelined run's.
     stages, replay_check = stages_overlapped, None
     line_read = line_written = None
-    if layout.get("pipeline") and not args.no_stage_timing and not raw:
+    if replay and layout.get("pipeline"):
         eng.close()
         ser = TokenBucketEngine(keys_local, args.token_limit, args.tokens_per_period,
                                 args.period_ticks, device=dev.index, stage_timing=True,
@@ -598,6 +609,9 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
             assert lib.tbe_gen_batch_device(SEED_B ^ 0x5A, n_keys, s * n, n, 1, 1, T0_US + s * args.interval_us,
                                             args.interval_us, k.data_ptr(), p.data_ptr(), t.data_ptr(),
                                             gen_stream) == 0
+            if args.sweep_zipf:
+                assert lib.tbe_gen_zipf_keys_device(SEED_B ^ 0x5A, n_keys, args.zipf_s, s * n, n, k.data_ptr(),
+                                                    gen_stream) == 0
             bufs.append((k, p, t))
         g = torch.empty(n, dtype=torch.uint8, device=dev)
         r = torch.empty(n, dtype=torch.int32, device=dev)

@@ -223,11 +223,16 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
 
     n, steps, warm = args.batch, args.steps, args.warmup
     total = warm + steps
-    eng = QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, period_ticks,
-                                    args.queue_limit, 0, device=dev.index,
-                                    stage_timing=not args.no_stage_timing, max_batch=n, pack=not args.no_pack,
-                                    fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=args.rerank)
+
+    def new_engine(timing):
+        return QueueingTokenBucketEngine(kl, args.token_limit, args.tokens_per_period, period_ticks,
+                                         args.queue_limit, 0, device=dev.index, stage_timing=timing,
+                                         max_batch=n, pack=not args.no_pack, fold_records=not args.unscatter_all,
+                                         digit_stream=not args.hist_records, rerank=args.rerank)
+
+    # the timed engine records no stage events (each leaves the stream idle for a few
+    # microseconds); the stage times come from a replay of the same schedule afterwards
+    eng = new_engine(args.timed_stage_events and not args.no_stage_timing)
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int32, device=dev)
@@ -290,11 +295,29 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
     grants = cnt.cpu().numpy().astype(np.int64)
     q = queued.cpu().numpy()
     granted = float((st == 1).float().mean().item())
+    layout = eng.layout()
+    if not args.no_stage_timing and not args.timed_stage_events:
+        # the replay: a fresh engine with stage events decides the same schedule (same state
+        # batch by batch); its replies are the timed run's
+        g_timed, r_timed = st.clone(), rem.clone()
+        eng.close()
+        eng = new_engine(True)
+        cnt.zero_()
+        for s in range(warm):
+            step(s)
+        eng.synchronize()
+        eng.stage_times()
+        for s in range(warm, total):
+            step(s)
+        eng.synchronize()
+        stages = eng.stage_times()
+        torch.cuda.synchronize()
+        assert torch.equal(st, g_timed) and torch.equal(rem, r_timed), "stage replay diverged from the timed run"
     if not fused:
         stages["drain"] = drain_ms
     out = {"elapsed": elapsed, "stages": stages, "granted": granted, "q_last": int(q[-1]),
            "tick_grants_per_step": grants[warm:].tolist(), "d_last": int(grants[-1]),
-           "queued_warmup": q[:warm].tolist(), "layout": eng.layout()}
+           "queued_warmup": q[:warm].tolist(), "layout": layout}
     eng.close()
     return out
 
@@ -418,10 +441,14 @@ def run_approx(args, lib, dev, world, rank, dist):
     kshared = args.keys or 10_000_000
     n, steps, warm = args.batch, args.steps, args.warmup
     total = warm + steps
-    eng = ApproximateEngine(kshared, args.token_limit, args.tokens_per_period, args.period_ticks,
-                            0, 0, device=dev.index, stage_timing=not args.no_stage_timing, max_batch=n,
-                            pack=not args.no_pack, fold_records=not args.unscatter_all,
-                            digit_stream=not args.hist_records, rerank=args.rerank)
+    def new_engine(timing):
+        return ApproximateEngine(kshared, args.token_limit, args.tokens_per_period, args.period_ticks,
+                                 0, 0, device=dev.index, stage_timing=timing, max_batch=n,
+                                 pack=not args.no_pack, fold_records=not args.unscatter_all,
+                                 digit_stream=not args.hist_records, rerank=args.rerank)
+
+    # no stage events in the timed engine; the stage times come from a replay (below)
+    eng = new_engine(args.timed_stage_events and not args.no_stage_timing)
     seed = SEED_E + 7919 * rank
     bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -500,12 +527,26 @@ def run_approx(args, lib, dev, world, rank, dist):
     eight = approx_eight_clients(args, eng, bufs, st, av, kshared, n, total + 5, dev) if not dist else None
     # bytes each GPU receives per refresh: ring all-reduce 2 (N-1)/N * 4K, all-gather (N-1) * 4K
     xbytes = {"node": int(2 * (world - 1) * kshared * 4 // world), "clients": int((world - 1) * kshared * 4)}
+    layout = eng.layout()
+    if not args.no_stage_timing and not args.timed_stage_events:
+        # stage times from a replay of the warm-up + timed schedule on an engine that records
+        # them (the refresh epochs included, as in the timed steps)
+        eng.close()
+        eng = new_engine(True)
+        for s in range(warm):
+            step(s)
+        eng.synchronize()
+        eng.stage_times()
+        for s in range(warm, total):
+            step(s)
+        eng.synchronize()
+        stages = eng.stage_times()
 
     value = n * steps * world / elapsed
-    fp = run_fingerprint(args, world, kshared, eng.layout())
+    fp = run_fingerprint(args, world, kshared, layout)
     if rank == 0:
         write_fingerprint(fp)
-    passes = eng.layout()["passes"]
+    passes = layout["passes"]
     launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
                 "unscatter": passes, "hot": 1}
     name = max(stages, key=stages.get)

@@ -2175,7 +2175,7 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
 // is the reference's serial order (TB:202-238 per request).  Waves stride over the
 // buckets, and each wave fetches the bounds of all its buckets with one load per lane.
 // A bucket of more than 64 requests goes in chunks of 64; a key's row written back by one
-// chunk is re-read by the next after an agent-scope fence (rare in sparse batches).
+// chunk is re-read by the next after a workgroup-scope fence.
 #ifndef TBE_SPARSE_WAVE
 #define TBE_SPARSE_WAVE 1
 #endif
@@ -2217,7 +2217,11 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
             const uint32_t s = __shfl(my_s, j, 64), e = __shfl(my_e, j, 64);
             Slot *__restrict__ rows = table + ((uint64_t)b << r_bits);
             for (uint32_t c = s; c < e; c += 64) {
-                if (c != s) __threadfence();   // the previous chunk's row stores are visible
+                // the previous chunk's row stores are visible to this wave's loads below: a
+                // workgroup-scope fence (the stores complete; the CU's L1 is write-through).
+                // An agent-scope one would also write back this XCD's L2 per chunk: a 2^22
+                // batch (two chunks per bucket) took 2.4 ms in this kernel that way.
+                if (c != s) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 const uint32_t q = c + (uint32_t)lane;
                 const bool v = q < e;
                 uint32_t kl = 0, pos = q;
@@ -2878,140 +2882,99 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
     if (t == 0) next->count = nh;
 }
 
-// Cold start (TBE_HOT_SAMPLE): an engine's first two batches have no hot set yet (a key is
-// nominated by the fold of a batch and runs apart two batches later), so a key that
-// dominates them fills one ordinary bucket, whose workgroup walks its requests chunk by
-// chunk (config C's first two batches: ~27 ms folds).  Those batches are sampled instead:
-// kHotSampleN requests at a fixed stride are counted in a small hash table, every key
-// whose estimated requests reach kHotSampleMin is nominated into the batch's own hot set,
-// and k_hot_update builds it before the batch's first histogram.  Speed only: which keys
-// run apart never changes a decision.
-constexpr uint32_t kHotSampleN = 16384;
-constexpr uint32_t kHotSampleSlots = 32768;
-constexpr uint64_t kHotSampleMin = 65536;   // estimated requests of the batch
-#if TBE_HOT_SAMPLE && !TBE_HOT_CUCKOO        // (the cuckoo table's path samples every batch: k_hot_sample)
-__global__ __launch_bounds__(1024) void k_hot_sample_count(const uint64_t *__restrict__ keys, uint64_t n,
-                                                           uint64_t n_keys, uint32_t S,
-                                                           uint32_t *__restrict__ skey, uint32_t *__restrict__ scnt) {
-    const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
-    if (i >= S) return;
-    const uint64_t key = keys[(uint64_t)i * n / S];
-    if (key >= n_keys || key >= 0xFFFFFFFFull) return;   // invalid keys fail the batch anyway
-    const uint32_t k = (uint32_t)key;
-    uint32_t h = (k * 0x9E3779B1u) >> (32 - 15);
-    static_assert(kHotSampleSlots == 1u << 15, "15-bit slots");
-    for (int probe = 0; probe < 64; ++probe) {
-        const uint32_t old = atomicCAS(&skey[h], 0xFFFFFFFFu, k);
-        if (old == 0xFFFFFFFFu || old == k) {
-            atomicAdd(&scnt[h], 1u);
-            return;
-        }
-        h = (h + 1) & (kHotSampleSlots - 1);
-    }
-}
-__global__ __launch_bounds__(1024) void k_hot_sample_pick(const uint32_t *__restrict__ skey,
-                                                          const uint32_t *__restrict__ scnt, uint64_t n,
-                                                          uint32_t S, HotSet *__restrict__ hot) {
-    __shared__ uint32_t nc;
-    if (threadIdx.x == 0) nc = 0;
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < kHotSampleSlots; j += 1024) {
-        const uint32_t c = scnt[j];
-        const uint64_t est = (uint64_t)c * n / S;
-        if (c != 0 && est >= kHotSampleMin) {
-            const uint32_t at = atomicAdd(&nc, 1u);
-            const uint64_t e32 = est < 0xFFFFFFFFull ? est : 0xFFFFFFFFull;
-            if (at < kHotCandMax) hot->cand[at] = (e32 << 32) | skey[j];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) hot->n_cand = nc;
-}
-#endif
+constexpr uint64_t kHotSampleMin = 65536;   // estimated requests of a batch that make a key hot (k_hot_sample)
 
 // Every batch is sampled (rounds 3-4 sampled only an engine's first
 // two batches): a key that turns hot in a running engine would otherwise fill one ordinary
 // bucket for the two batches its fold nomination takes, and that workgroup walks its
 // millions of requests (~27 ms at config C's hottest key).  One 1024-thread workgroup, on
 // the partition stream before the batch's first histogram:
-//   1. kHotSampleN requests, one per stratum of the batch; keys already in its hot set are
-//      skipped, the others counted in an LDS hash (kHsSlots slots, bounded probing: a
-//      sample that finds no slot is dropped -- speed only);
-//   2. every key estimated at >= kHotSampleMin requests of the batch is appended to the
-//      hot set (new run index, cuckoo placement in the LDS copy of the table), up to the
-//      set's capacity -- fold nominations fill at most cap - kHotSampleReserve of it;
+//   1. S requests (hot_sample_n: n / 8192 clamped to [1024, 8192], so that a key at the
+//      threshold is expected >= 8 times), one per stratum of the batch at a hashed offset,
+//      counted in an LDS hash (key << 32 | count per slot, bounded probing: a sample that
+//      finds no slot is dropped -- speed only);
+//   2. every key estimated at >= kHotSampleMin requests of the batch that its hot set lacks
+//      is appended to the set (new run index, cuckoo placement in an LDS copy of the table,
+//      over the dead sample slots), up to the set's capacity -- fold nominations fill at
+//      most cap - kHotSampleReserve of it;
 //   3. only if a key was added, the table goes back to global memory.
-// The steady state (every dominant key already hot, or none) reads 16,384 keys and writes
-// nothing.  Which keys run apart only changes speed, never a decision.
-constexpr uint32_t kHsSlots = 8192;
+// No 64-bit division anywhere (the strata are n / S apart, offsets by multiply-high): the
+// first version's three per sample, and its 16,384 samples probing 8,192 slots, made it a
+// 54 us kernel (profiles/r05n_*).  Which keys run apart only changes speed, never a decision.
+constexpr uint32_t kHsSlots = 16384;
+constexpr uint32_t kHsSampleMax = 8192;
 constexpr int kHsProbes = 8;
 constexpr uint32_t kHsNewMax = 256;   // config C: ~71 keys above kHotSampleMin at cold start
+constexpr unsigned long long kHsEmpty = ~0ull;
+__device__ __forceinline__ uint32_t hot_sample_n(uint64_t n) {
+    return (uint32_t)min<uint64_t>(kHsSampleMax, max<uint64_t>(1024, n >> 13));
+}
 __global__ __launch_bounds__(1024) void k_hot_sample(const uint64_t *__restrict__ keys, uint64_t n,
                                                      uint64_t n_keys, HotSet *__restrict__ hot, uint32_t cap) {
-    __shared__ uint32_t skey[kHsSlots];
-    __shared__ uint32_t scnt[kHsSlots];
-    __shared__ uint64_t tab[kHotSlots];
+    __shared__ unsigned long long sl[kHsSlots];   // the sample counts, then the hot table
     __shared__ uint64_t newk[kHsNewMax];
     __shared__ uint32_t nnew, count;
+    static_assert(kHotSlots <= kHsSlots, "the hot table fits over the sample slots");
     const uint32_t t = threadIdx.x;
-    const uint32_t S = (uint32_t)min<uint64_t>(n, kHotSampleN);
+    const uint32_t S = hot_sample_n(n);
+    if (n < S) return;                        // (launched for n >= kHotSampleMin only)
     if (t == 0) {
         nnew = 0;
         count = hot->count;
     }
-    for (uint32_t j = t; j < kHsSlots; j += 1024) {
-        skey[j] = 0xFFFFFFFFu;
-        scnt[j] = 0;
-    }
-    __syncthreads();
-    const bool any = count != 0;
-    for (uint32_t j = t; j < kHotSlots; j += 1024) tab[j] = any ? hot->slot[j] : kHotSlotEmpty;
-    __syncthreads();
-    // one request from each of S equal strata, at a hashed offset inside the stratum: a
-    // fixed stride would alias with periodic traffic (a key at every 10th position is
-    // never sampled at stride 4096).  All of a thread's loads are issued before any is used.
-    constexpr int kPerThread = kHotSampleN / 1024;
+    for (uint32_t j = t; j < kHsSlots; j += 1024) sl[j] = kHsEmpty;
+    // one request from each of S strata of `step` requests, at a hashed offset inside the
+    // stratum: a fixed stride would alias with periodic traffic (a key at every 10th
+    // position is never sampled at stride 4096).  All of a thread's loads are issued before
+    // any is used.
+    const uint64_t step = n / S;             // < 2^32: the offset is a 32 x 32-bit multiply-high
+    constexpr int kPerThread = kHsSampleMax / 1024;
     uint64_t kv[kPerThread];
 #pragma unroll
     for (int j = 0; j < kPerThread; ++j) {
         const uint32_t i = t + 1024u * j;
         kv[j] = ~0ull;
         if (i < S) {
-            const uint64_t lo = (uint64_t)i * n / S, hi = (uint64_t)(i + 1) * n / S;
             uint32_t hx = (i + 0x9E3779B9u) * 0x85EBCA6Bu;
             hx ^= hx >> 13;
             hx *= 0xC2B2AE35u;
             hx ^= hx >> 16;
-            kv[j] = keys[lo + (uint64_t)hx % (hi - lo)];
+            kv[j] = keys[(uint64_t)i * step + (((uint64_t)hx * step) >> 32)];
         }
     }
+    __syncthreads();                          // slots cleared
 #pragma unroll
     for (int j = 0; j < kPerThread; ++j) {
         const uint64_t key = kv[j];
         if (key >= n_keys || key >= 0xFFFFFFFFull) continue;   // invalid keys fail the batch anyway
         const uint32_t k = (uint32_t)key;
-        if ((uint32_t)tab[hot_h1(k)] == k || (uint32_t)tab[hot_h2(k)] == k) continue;   // already hot
-        uint32_t h = (k * 0x9E3779B1u) >> (32 - 13);
-        static_assert(kHsSlots == 1u << 13, "13-bit sample slots");
+        uint32_t h = (k * 0x9E3779B1u) >> (32 - 14);
+        static_assert(kHsSlots == 1u << 14, "14-bit sample slots");
         for (int probe = 0; probe < kHsProbes; ++probe) {
-            const uint32_t old = atomicCAS(&skey[h], 0xFFFFFFFFu, k);
-            if (old == 0xFFFFFFFFu || old == k) {
-                atomicAdd(&scnt[h], 1u);
+            const unsigned long long old = atomicCAS(&sl[h], kHsEmpty, ((unsigned long long)k << 32) | 1ull);
+            if (old == kHsEmpty) break;
+            if ((uint32_t)(old >> 32) == k) {
+                atomicAdd(&sl[h], 1ull);
                 break;
             }
             h = (h + 1) & (kHsSlots - 1);
         }
     }
     __syncthreads();
+    // estimated requests c * n / S >= kHotSampleMin, and not yet in the set
     for (uint32_t j = t; j < kHsSlots; j += 1024) {
-        const uint32_t c = scnt[j];
-        if (c != 0 && (uint64_t)c * n / S >= kHotSampleMin) {
-            const uint32_t at = atomicAdd(&nnew, 1u);
-            if (at < kHsNewMax) newk[at] = skey[j];
-        }
+        const unsigned long long v = sl[j];
+        if (v == kHsEmpty || (uint64_t)(uint32_t)v * n < kHotSampleMin * S) continue;
+        const uint32_t k = (uint32_t)(v >> 32);
+        if (count && ((uint32_t)hot->slot[hot_h1(k)] == k || (uint32_t)hot->slot[hot_h2(k)] == k)) continue;
+        const uint32_t at = atomicAdd(&nnew, 1u);
+        if (at < kHsNewMax) newk[at] = k;
     }
     __syncthreads();
     if (nnew == 0) return;                    // workgroup-uniform
+    uint64_t *tab = reinterpret_cast<uint64_t *>(sl);
+    for (uint32_t j = t; j < kHotSlots; j += 1024) tab[j] = count ? hot->slot[j] : kHotSlotEmpty;
+    __syncthreads();
     if (t == 0) {
         uint32_t cnt = count;
         for (uint32_t u = 0; u < min(nnew, kHsNewMax) && cnt < cap; ++u) {
@@ -4290,7 +4253,6 @@ struct tbe_engine {
     uint32_t hot_cap = 0;
     uint32_t nb_total = 0;
     HotSet *hot[3] = {nullptr, nullptr, nullptr};
-    uint32_t *hs_key = nullptr, *hs_cnt = nullptr;   // cold-start sampling (k_hot_sample_*)
     uint64_t nbatch = 0;
     Slot *table = nullptr;
     // queueing kind
@@ -4520,7 +4482,7 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 // above 1).  Dense batches give every nonempty bucket to k_fold_wide; sparse ones only the
 // buckets of >= R/8 requests.  TBE_FOLD_NARROW_ONLY (A/B): k_fold takes every bucket.
 #ifndef TBE_SPARSE_GATE_SHIFT
-#define TBE_SPARSE_GATE_SHIFT 5              // sparse batch: fewer than R >> this requests per bucket
+#define TBE_SPARSE_GATE_SHIFT 3              // sparse batch: fewer than R >> this requests per bucket
 #endif
 uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #ifdef TBE_FOLD_NARROW_ONLY
@@ -4535,6 +4497,9 @@ uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
 #endif
 }
 
+#ifndef TBE_HOT_SPARSE_MIN_LOG2
+#define TBE_HOT_SPARSE_MIN_LOG2 20           // sparse batches below 2^this take no hot-key runs
+#endif
 // Run slots the per-batch sampler keeps free of fold nominations (k_hot_sample)
 inline uint32_t hot_reserve_host(uint32_t cap) {
 #if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
@@ -4622,27 +4587,18 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // one wave each (k_fold_sparse)
     const uint32_t tb_wmin = (!approx && !wait) ? fold_wide_min(e, n) : 1u;
     const bool sparse_tb = TBE_SPARSE_WAVE && tb_wmin > 1u;
-    // hot runs: see tbe_engine::hot.  Not in a sparse batch (the micro-batch regime): a key
-    // busy enough to matter fills one dense bucket, which k_fold_wide takes whole, and the
-    // hot machinery (its LDS tables in the first pass, four launches) costs more than it
-    // saves there.  Which keys are hot never changes a decision; the hot sets keep their
-    // contents for the next dense batch.
-    const bool hot_on = e->hot_cap && !sparse_tb;
+    // hot runs: see tbe_engine::hot.  Not in a sparse batch below 2^20 requests (the
+    // micro-batch regime): there a key busy enough to matter fills one dense bucket, which
+    // k_fold_wide takes whole, and the hot machinery (the sampler, four launches) costs more
+    // than it saves -- uniform 2^18: 0.10 ms per batch without, Zipf 2^20: 0.44 with against
+    // 0.68 without (profiles/r05q_ablate_hot_sparse.log).  Which keys are hot never changes
+    // a decision; the hot sets keep their contents for the next batch that runs them.
+    const bool hot_on = e->hot_cap && !(sparse_tb && n < (1ull << TBE_HOT_SPARSE_MIN_LOG2));
     HotSet *hot = hot_on ? e->hot[e->nbatch % 3] : nullptr;
     HotSet *hot_next = hot_on ? e->hot[(e->nbatch + 2) % 3] : nullptr;
 #if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
     // every batch: its dominant keys join its own hot set (k_hot_sample)
     if (hot && n >= kHotSampleMin) k_hot_sample<<<1, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, hot, e->hot_cap);
-#elif TBE_HOT_SAMPLE
-    if (hot && e->nbatch < 2 && e->hs_key && n >= kHotSampleMin) {
-        // cold start: nominate this batch's dominant keys into its own (still empty) hot set
-        const uint32_t S = (uint32_t)std::min<uint64_t>(n, kHotSampleN);
-        HIP_TRY(e, hipMemsetAsync(e->hs_key, 0xFF, kHotSampleSlots * sizeof(uint32_t), sp));
-        HIP_TRY(e, hipMemsetAsync(e->hs_cnt, 0, kHotSampleSlots * sizeof(uint32_t), sp));
-        k_hot_sample_count<<<(S + 1023) / 1024, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, S, e->hs_key, e->hs_cnt);
-        k_hot_sample_pick<<<1, 1024, 0, sp>>>(e->hs_key, e->hs_cnt, n, S, hot);
-        k_hot_update<<<1, 1024, 0, sp>>>(hot, e->hot_cap, w.err);
-    }
 #endif
     for (int p = 0; p < e->passes; ++p) {
         const int shift = e->r_bits + kDigitBits * p;
@@ -5099,9 +5055,6 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
             if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
             if (hipMemsetAsync(hs, 0, sizeof(HotSet), e->stream) != hipSuccess) return bail(TBE_EDEVICE);
         }
-        if (hipMalloc(&e->hs_key, kHotSampleSlots * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&e->hs_cnt, kHotSampleSlots * sizeof(uint32_t)) != hipSuccess)
-            return bail(TBE_ENOMEM);
     }
     if (hipMalloc(&e->sticky, sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     if (hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), e->stream) != hipSuccess)
@@ -5173,8 +5126,6 @@ void tbe_destroy(tbe_engine *e) {
     dfree(e->log_rem);
     dfree(e->sticky);
     for (auto &hs : e->hot) dfree(hs);
-    dfree(e->hs_key);
-    dfree(e->hs_cnt);
     for (auto &ev : e->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : {e->ev_in, e->ev_part, e->ev_out, e->ev_hot, e->ws[0].done, e->ws[1].done,

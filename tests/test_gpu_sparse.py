@@ -1,11 +1,13 @@
-"""Sparse batches: a batch far smaller than the key space (2^14 to 2^21
+"""Sparse batches: a batch far smaller than the key space (2^14 to 2^23
 requests over 1e8 keys) leaves most of the 48,829 buckets with a few requests each.  Those
 go to k_fold_sparse -- one wave per bucket, the lanes of one key ballot-matched and walked
 in arrival order by the key's first lane (TB:202-238) -- and the buckets of >= R/8 requests
-to k_fold_wide through k_bscan's dense-bucket list.  Every reply and the table against the
-C restatement (oracle/tb_ref.c): uniform batches of every sparse size, a skewed batch whose
-sparse buckets span several 64-request chunks with keys repeated across chunks, dense
-buckets inside a sparse batch, mixed permits, expiry, and the unpacked (SoA) records."""
+to k_fold_wide through the dense-bucket list the bucket scan builds.  A sparse batch runs
+no hot-key machinery: a Zipf batch's busiest keys fill dense buckets instead.  Every reply
+and the table against the C restatement (oracle/tb_ref.c): uniform batches of every sparse
+size, a skewed batch whose sparse buckets span several 64-request chunks with keys repeated
+across chunks, dense buckets inside a sparse batch, Zipf batches, mixed permits, expiry,
+and the unpacked (SoA) records."""
 import os
 
 import numpy as np
@@ -35,7 +37,7 @@ def _run(eng, ref, keys, permits, ts, tag):
     assert bad.size == 0, (tag, bad.size, bad[:5], keys[bad[:5]], g[bad[:5]], r[bad[:5]], g_ref[bad[:5]], r_ref[bad[:5]])
 
 
-@pytest.mark.parametrize("logn", [14, 17, 20, 21])
+@pytest.mark.parametrize("logn", [14, 17, 20, 21, 22, 23])
 def test_sparse_uniform_batches(engine_lib, gpu, logn):
     from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
     n_keys, n = 100_000_000, 1 << logn
@@ -94,5 +96,29 @@ def test_sparse_unpacked_records(engine_lib, gpu):
         permits = rng.integers(0, 3, n).astype(np.int32)
         ts = (T0 + b * 2_000_000 + np.sort(rng.integers(0, 1_000_000, n))).astype(np.int64)
         _run(eng, ref, keys, permits, ts, b)
+    _check_table(eng, ref)
+    eng.close()
+
+
+def test_sparse_zipf_batches(engine_lib, gpu):
+    """Zipf(1.1) batches of 2^20 requests over 1e8 keys: sparse batches (no hot-key runs),
+    whose busiest key (~11% of a batch: ~115k requests) fills one dense bucket that
+    k_fold_wide decides in ~75 chunks; between them dense 2^24 Zipf batches with hot runs,
+    whose hot sets the sparse batches leave alone."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
+    n_keys = 100_000_000
+    big, n = 1 << 24, 1 << 20
+    eng = TokenBucketEngine(n_keys, 10, 1, 10_000_000, device=0, max_batch=big)
+    assert eng.layout()["hot"]
+    assert eng.batch_format(n)["sparse"] and not eng.batch_format(big)["sparse"]
+    ref = cref.CTokenBucket(n_keys, 10, fill_rate(1, 10_000_000))
+    rng = np.random.default_rng(11)
+    perm = rng.permutation(1 << 20).astype(np.uint64) * 95 + 17   # Zipf ranks -> keys
+    for b, m in enumerate([big, n, n, big, n]):
+        ranks = np.minimum(rng.zipf(1.1, m), 1 << 20) - 1
+        keys = perm[ranks]
+        permits = rng.integers(0, 4, m).astype(np.int32)
+        ts = (T0 + b * 2_000_000 + np.sort(rng.integers(0, 1_000_000, m))).astype(np.int64)
+        _run(eng, ref, keys, permits, ts, (b, m))
     _check_table(eng, ref)
     eng.close()

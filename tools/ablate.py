@@ -199,10 +199,17 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
-    "gate": {
-        "gate5_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
-        "gate4_u": (["TBE_SPARSE_GATE_SHIFT=4"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
-        "gate3_u": (["TBE_SPARSE_GATE_SHIFT=3"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--sweep-log2", "21,22,23"]),
+    "events": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "tev_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--timed-stage-events"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "tev_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--timed-stage-events"]),
+    },
+    "hotmin": {
+        "never_u": (["TBE_HOT_SPARSE_MIN_LOG2=40"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22']),
+        "hm20_u": (["TBE_HOT_SPARSE_MIN_LOG2=20"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22']),
+        "never_z": (["TBE_HOT_SPARSE_MIN_LOG2=40"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
+        "hm20_z": (["TBE_HOT_SPARSE_MIN_LOG2=20"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
     },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
@@ -286,6 +293,9 @@ def run(rounds: int, steps: int):
             print(r, name, d["ms_per_step"], d["stage_ms_per_step"],
                   (d.get("roofline") or {}).get("avg_launch_ms"), d.get("host_buffer_decisions_per_s"),
                   d.get("host_buffer_pinned_decisions_per_s"), flush=True)
+            for b in d.get("batch_sweep") or []:
+                print("   sweep", name, b["batch"], b["ms_per_batch"], b["latency_ms"], b["fold"][:14],
+                      b["stage_ms_per_batch"], flush=True)
     print(json.dumps(results))
 
 
