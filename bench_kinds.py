@@ -230,9 +230,10 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
                                          max_batch=n, pack=not args.no_pack, fold_records=not args.unscatter_all,
                                          digit_stream=not args.hist_records, rerank=args.rerank)
 
-    # the timed engine records no stage events (each leaves the stream idle for a few
-    # microseconds); the stage times come from a replay of the same schedule afterwards
-    eng = new_engine(args.timed_stage_events and not args.no_stage_timing)
+    # the timed engine records events around the fold alone (the roofline's kernel time, two
+    # events per batch: a pair per stage would leave the stream idle ~14 times a batch); the
+    # stage breakdown comes from a replay of the same schedule afterwards
+    eng = new_engine(False if args.no_stage_timing else True if args.timed_stage_events else "fold")
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int32, device=dev)
@@ -289,6 +290,7 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
         mark(lib, 2, dev)
     eng.synchronize()
     stages = eng.stage_times()
+    fold_timed = stages.get("fold", 0.0)
     drain_ms = 0.0 if fused else sum(a.elapsed_time(b) for a, b in evs)
     outcome(total - 1)
     torch.cuda.synchronize()
@@ -317,7 +319,7 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
         stages["drain"] = drain_ms
     out = {"elapsed": elapsed, "stages": stages, "granted": granted, "q_last": int(q[-1]),
            "tick_grants_per_step": grants[warm:].tolist(), "d_last": int(grants[-1]),
-           "queued_warmup": q[:warm].tolist(), "layout": layout}
+           "queued_warmup": q[:warm].tolist(), "layout": layout, "fold_timed": fold_timed}
     eng.close()
     return out
 
@@ -340,6 +342,8 @@ def run_queue(args, lib, dev, world, rank, dist):
                 "unscatter": passes, "hot": 1, "drain": 1}
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
+    if name == "fold" and r["fold_timed"] > 0:   # the timed engine's own fold events
+        ms = r["fold_timed"] / steps
     u = _distinct(n, kl)
     packed = bool(r["layout"].get("packed"))
     if name == "fold":
@@ -447,8 +451,8 @@ def run_approx(args, lib, dev, world, rank, dist):
                                  pack=not args.no_pack, fold_records=not args.unscatter_all,
                                  digit_stream=not args.hist_records, rerank=args.rerank)
 
-    # no stage events in the timed engine; the stage times come from a replay (below)
-    eng = new_engine(args.timed_stage_events and not args.no_stage_timing)
+    # fold events alone in the timed engine; the stage breakdown comes from a replay (below)
+    eng = new_engine(False if args.no_stage_timing else True if args.timed_stage_events else "fold")
     seed = SEED_E + 7919 * rank
     bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -510,6 +514,7 @@ def run_approx(args, lib, dev, world, rank, dist):
     mark(lib, 2, dev)
     eng.synchronize()
     stages = eng.stage_times()
+    fold_timed = stages.get("fold", 0.0)
     granted = float((st == 1).float().mean().item())
     # the other exchange mode's refresh epoch, timed after the timed region on the same
     # engine (its counts are the last batch's local scores, then zeros)
@@ -551,6 +556,8 @@ def run_approx(args, lib, dev, world, rank, dist):
                 "unscatter": passes, "hot": 1}
     name = max(stages, key=stages.get)
     ms = stages[name] / (steps * launches[name])
+    if name == "fold" and fold_timed > 0:   # the timed engine's own fold events
+        ms = fold_timed / steps
     u = _distinct(n, kshared)
     if name == "fold":
         # records (key 4, permits 4, arrival index 4) + reply 4 per request; local-tier row

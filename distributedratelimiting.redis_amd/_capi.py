@@ -19,6 +19,7 @@ STATUS_NAMES = {0: "TBE_OK", 1: "TBE_EINVAL", 2: "TBE_ENOMEM", 3: "TBE_EDEVICE",
                 4: "TBE_EDISPOSED", 5: "TBE_ERANGE"}
 TBE_KIND_TOKEN_BUCKET, TBE_KIND_QUEUEING, TBE_KIND_APPROXIMATE = 0, 1, 2
 TBE_FLAG_STAGE_TIMING = 0x1
+TBE_FLAG_FOLD_TIMING = 0x100
 TBE_FLAG_NO_PACK = 0x2
 TBE_FLAG_NO_HOT = 0x4
 TBE_FLAG_NO_PIPELINE = 0x8

@@ -4312,6 +4312,7 @@ struct tbe_engine {
     // Stage timing (TBE_FLAG_STAGE_TIMING): an event pair per stage per batch, recorded
     // on the launch stream without any host synchronisation; read in tbe_stage_times.
     bool timing = false;
+    uint32_t timing_mask = 0;   // stages that record events (bit s: stage s)
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_marks;   // (stage, index of start event)
@@ -4464,7 +4465,7 @@ hipEvent_t next_event(tbe_engine *e) {
     return e->ev_pool[e->ev_used++];
 }
 inline void stage_begin(tbe_engine *e, int s, hipStream_t st) {
-    if (!e->timing) return;
+    if (!e->timing || !((e->timing_mask >> s) & 1u)) return;
     const size_t idx = e->ev_used;
     hipEvent_t a = next_event(e), b = next_event(e);
     if (!a || !b) return;
@@ -4981,7 +4982,8 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     e->nbuckets = (uint32_t)((c.n_keys + (1ull << e->r_bits) - 1) >> e->r_bits);
     const int bbits = ceil_log2(e->nbuckets);
     e->passes = std::max(1, (bbits + kDigitBits - 1) / kDigitBits);
-    e->timing = (c.flags & TBE_FLAG_STAGE_TIMING) != 0;
+    e->timing = (c.flags & (TBE_FLAG_STAGE_TIMING | TBE_FLAG_FOLD_TIMING)) != 0;
+    e->timing_mask = (c.flags & TBE_FLAG_STAGE_TIMING) ? ~0u : (1u << ST_FOLD);
     {
         // Packed records need key + permit code + a >= 32-bit time offset + escape bit.
         // Hot runs (token bucket, packed) take bucket ids past the ordinary ones that the

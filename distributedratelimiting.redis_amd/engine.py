@@ -61,7 +61,9 @@ class TokenBucketEngine:
                  pipeline: bool = True, narrow: bool = True, zero_wait_slots: int = 0,
                  fold_records: bool = True, digit_stream: bool = True, rerank: bool = False):
         self._lib = _capi.load()
-        flags = _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0
+        # stage_timing: True (every stage), "fold" (the fold alone) or False
+        flags = (_capi.TBE_FLAG_FOLD_TIMING if stage_timing == "fold"
+                 else _capi.TBE_FLAG_STAGE_TIMING if stage_timing else 0)
         if not pack:
             flags |= _capi.TBE_FLAG_NO_PACK
         if not hot:

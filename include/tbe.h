@@ -102,6 +102,11 @@ typedef struct tbe_config {
                                              of gathering through pass 0's stored permutation:
                                              0.4 GB less traffic per config-B batch, 0.06 ms
                                              slower */
+#define TBE_FLAG_FOLD_TIMING 0x100u        /* record HIP events around the fold stage only
+                                             (tbe_stage_times reports the fold alone): the
+                                             dominant kernel's time at two events per batch
+                                             instead of a pair per stage, each event record
+                                             leaving the stream idle for microseconds */
 #define TBE_FLAG_HIST_RECORDS 0x40u       /* packed records, 2 passes (A/B checks): the second
                                              pass's histogram reads the first pass's 8-byte
                                              records.  By default the first pass also writes each

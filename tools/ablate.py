@@ -199,6 +199,12 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "pipe": {
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "nopipe_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--no-pipeline"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "nopipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--no-pipeline"]),
+    },
     "events": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "tev_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--timed-stage-events"]),
