@@ -470,8 +470,9 @@ def main():
                 "line_note": (f"128 B x (lines read {line_read:.4g} + lines written {line_written:.4g}, "
                               "per-batch means of the timed batches) + records and replies")})
         if replay_check is not None:
-            roofline["overlapped_avg_launch_ms"] = round(
-                stages_overlapped.get(name, 0.0) / (args.steps * launches[name]), 4)
+            if args.timed_stage_events:   # (the timed engine records stage events only then)
+                roofline["overlapped_avg_launch_ms"] = round(
+                    stages_overlapped.get(name, 0.0) / (args.steps * launches[name]), 4)
             roofline["replay_replies_identical"] = replay_check
 
     # config A is the reference's own per-request deployment: also time the host-buffer
@@ -568,7 +569,8 @@ def main():
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "stage_ms_per_step_overlapped": ({k: round(v / args.steps, 4)
                                               for k, v in stages_overlapped.items()}
-                                             if replay_check is not None else None),
+                                             if replay_check is not None and args.timed_stage_events
+                                             else None),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

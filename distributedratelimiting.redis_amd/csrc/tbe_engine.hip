@@ -2457,7 +2457,7 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
 #define TBE_HOT_SAMPLE 1
 #endif
 constexpr int kSegBlock = kFoldBlock;
-constexpr int kSegItems = 16;
+constexpr int kSegItems = 16;   // (8: no faster, 4: slower; profiles/r05u_ablate_hot_segments.log)
 constexpr uint32_t kSeg = kSegBlock * kSegItems;  // 8192 requests per run segment
 
 struct SegSummary {

@@ -199,6 +199,10 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "seg": {
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "nostore_z": (["TBE_HOT_NO_REPLY_STORE"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "pipe": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "nopipe_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse", "--no-pipeline"]),
