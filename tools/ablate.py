@@ -199,6 +199,12 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "hs": {
+        "small_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "big_u": (["TBE_HS_SMALL=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "small_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "big_z": (["TBE_HS_SMALL=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
     "seg": {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "nostore_z": (["TBE_HOT_NO_REPLY_STORE"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
