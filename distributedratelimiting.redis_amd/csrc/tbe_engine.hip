@@ -143,25 +143,20 @@ __device__ __forceinline__ uint32_t hot_h2(uint32_t key) {
 }
 
 // Copy a hot set's hash table into LDS (every thread calls; one barrier).  Returns
-// whether any key is hot.
-// TBE_HOT_PROBE_GLOBAL (A/B): no LDS copy; the probes read the table through the caches.
-#ifndef TBE_HOT_PROBE_GLOBAL
-#define TBE_HOT_PROBE_GLOBAL 0
-#endif
-constexpr uint32_t kHotLds = TBE_HOT_PROBE_GLOBAL ? 1u : kHotSlots;   // LDS copy of the table
+// whether any key is hot.  (Probing the global table through the caches instead was
+// slower, CHANGELOG round 3.)
+constexpr uint32_t kHotLds = kHotSlots;   // LDS copy of the table
 template <int BLOCK>
 __device__ __forceinline__ bool hot_load(const HotSet *__restrict__ hot, uint64_t *slots) {
     const bool any = hot != nullptr && hot->count != 0;
-#if !TBE_HOT_PROBE_GLOBAL
     if (any)
         for (int j = threadIdx.x; j < (int)kHotSlots; j += BLOCK) slots[j] = hot->slot[j];
     __syncthreads();
-#endif
     return any;
 }
-// The table the probes read: the workgroup's LDS copy, or the global table itself.
-__device__ __forceinline__ const uint64_t *hot_table(const HotSet *__restrict__ hot, const uint64_t *lds) {
-    return TBE_HOT_PROBE_GLOBAL ? hot->slot : lds;
+// The table the probes read: the workgroup's LDS copy.
+__device__ __forceinline__ const uint64_t *hot_table(const HotSet *__restrict__, const uint64_t *lds) {
+    return lds;
 }
 
 // Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
@@ -188,12 +183,6 @@ __device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *sl
 template <int N, typename KeyT>
 __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t *slots, uint32_t nb,
                                              int r_bits, uint32_t (&sk)[N]) {
-#ifdef TBE_HOT_NOPROBE_AB
-    // A/B timing only (wrong partition): the cost of the hot-set probes
-#pragma unroll
-    for (int it = 0; it < N; ++it) sk[it] = (uint32_t)kv[it] ^ ((uint32_t)slots[it & 7] & 1u);
-    return;
-#endif
 #if TBE_HOT_CUCKOO
     // both probes of 4 requests in flight at a time (8 would spill in the hot histogram)
     constexpr int G = N < 4 ? N : 4;
@@ -1015,9 +1004,6 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 // then the caller's timestamps (for the record bases).
 // TBE_SCATTER0_WAVES (A/B): minimum waves per SIMD of the first pass (which holds the
 // caller's three columns of its 8 requests per thread in registers: 108 VGPRs, 4 waves)
-#ifndef TBE_LAST_PRESTAGE
-#define TBE_LAST_PRESTAGE 0                  // A/B: fold records formed before staging
-#endif
 #ifndef TBE_BSCAN_LB
 #define TBE_BSCAN_LB 1                       // bucket starts by decoupled look-back; 0: one workgroup (A/B)
 #endif
@@ -1045,11 +1031,7 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
-#if TBE_LAST_PRESTAGE
-    __shared__ uint8_t stage_d[LAST ? kTile : 1];    // LAST: each staged fold record's digit
-#else
     __shared__ uint16_t stage_e[LAST ? kTile : 1];   // LAST: each staged record's input element
-#endif
     __shared__ uint64_t hs[HOT ? kHotLds : 1];
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
@@ -1139,17 +1121,9 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
         if (e < nvalid) {
             const uint32_t d = (key[it] >> shift) & (kDigits - 1);
-#if TBE_LAST_PRESTAGE
-            // LAST: the fold record is formed here, where the element's index is at hand,
-            // and its digit staged beside it (the record no longer carries it)
-            stage[lpos[it]] = LAST ? fold_rec(rec[it], (uint32_t)(base + e), tbase0, tbase1, F, G) : rec[it];
-            if (LAST)
-                stage_d[lpos[it]] = (uint8_t)d;
-#else
             stage[lpos[it]] = n0 ? (rec[it] & 0x0000FFFFFFFFFFFFull) : rec[it];
             if (LAST)
                 stage_e[lpos[it]] = (uint16_t)e;
-#endif
             else if (perm)   // (null: k_unrank recomputes the positions)
                 ST_PERM(perm + base + e, goff[d] + lpos[it] - L.lstart[d]);
             if (FIRST && n0 && ((rec[it] >> 48) & 1u))   // escaped: its time beside its position
@@ -1163,11 +1137,6 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         const int j = it * kPartBlock + tid;
         if (j < nvalid) {
             const uint64_t s = stage[j];
-#if TBE_LAST_PRESTAGE
-            const uint32_t d = LAST ? (uint32_t)stage_d[j] : ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
-            gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
-            rout[gpos[it]] = s;   // runs merge in L2: keep cached
-#else
             const uint32_t d = n0 ? (uint32_t)(s >> 32) & (kDigits - 1)
                                   : ((uint32_t)(s & F.kmask) >> shift) & (kDigits - 1);
             gpos[it] = goff[d] + (uint32_t)j - L.lstart[d];
@@ -1178,7 +1147,6 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
                 rout[gpos[it]] = fold_rec32((uint32_t)s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G);
             else
                 rout[gpos[it]] = LAST ? fold_rec(s, (uint32_t)(base + stage_e[j]), tbase0, tbase1, F, G) : s;
-#endif
             // the next pass's digit, one byte beside the record (k_hist_dig reads these)
             if (!LAST && dig_next)
                 dig_next[gpos[it]] = n0 ? (uint8_t)(s >> 40)
@@ -1298,9 +1266,6 @@ __device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
 #ifndef TBE_WIDE_PER
 #define TBE_WIDE_PER 3
 #endif
-#ifndef TBE_WIDE_FT
-#define TBE_WIDE_FT 0
-#endif
 #ifndef TBE_WIDE_WAVES
 #define TBE_WIDE_WAVES 6                     // minimum waves per SIMD (register budget)
 #endif
@@ -1313,9 +1278,6 @@ constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
 #ifndef TBE_FOLD_PREFETCH
 #define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
-#endif
-#ifndef TBE_WIDE_EARLY_DMA
-#define TBE_WIDE_EARLY_DMA 0
 #endif
 #ifndef TBE_QFOLD_PREFETCH
 #define TBE_QFOLD_PREFETCH 0                 // A/B: the same for k_fold_q
@@ -1339,32 +1301,20 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 //    R/2 .. R/2048 measured, profiles/r02_ablate_wide_threshold*.log); round 3 gave it every
 //    bucket and stopped launching k_fold, whose 48828 workgroups that only read their
 //    bucket bounds and exit cost 0.03 ms per batch (profiles/r03_ablate_hot_wide_walk.log).
-//  - Sparse batches (e.g. 2^20 requests over 1e8 keys, ~21 per bucket): k_fold_wide only
-//    for buckets of at least R/8 requests, the rule k_fold's own dense test uses; the others
-//    go to k_fold, which gathers just their rows instead of the whole slice (ADVICE r03:
-//    a dense-only fold reads the whole 1.6 GB table for a batch that touches 16 MB of it).
+//  - Sparse batches (fewer than R/8 requests per bucket on average, e.g. 2^20 requests over
+//    1e8 keys, ~21 per bucket): k_fold_wide only for the buckets of at least R/8 requests
+//    (the list k_bscan_lb builds); the others go one wave each to k_fold_sparse, which
+//    gathers just their rows instead of the whole slice (a dense-only fold
+//    reads the whole 1.6 GB table for a batch that touches 16 MB of it).
 constexpr int kWideMinShift = TBE_WIDE_MIN_SHIFT;
-// Tail walk (round 3, as k_fold_q's; A/B only): the requests still pending after round 1
-// are counting-sorted by row and each row's run is decided by one thread in arrival order,
-// instead of further workgroup-wide speculative rounds; runs longer than kWideTailRun keep
-// the rounds.  Slower here (config B fold 0.77 -> 0.88 ms, Zipf 0.67 -> 0.76,
-// profiles/r03_ablate_hot_wide_walk.log): a speculative round settles most of the tail at
-// once, while the sort's barriers and the serial FP64 chains of the walkers do not pay off.
-#ifndef TBE_WIDE_TAIL_WALK
-#define TBE_WIDE_TAIL_WALK 0
-#endif
-#if TBE_WIDE_TAIL_WALK
-constexpr uint32_t kWideTailRun = 32;
-#endif
+// (A tail walk -- the requests still pending after round 1 counting-sorted by row, each
+// row's run decided by one thread -- was slower here: config B fold 0.77 -> 0.88 ms,
+// profiles/r03_ablate_hot_wide_walk.log; removed in round 5.)
 static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and tail list");
-// The rows' field t (TB:203 of the stored t_us): cached in LDS, or derived per evaluation
-#if TBE_WIDE_FT
-#define WIDE_FT_GET(j, srow) ft[j]
-#define WIDE_FT_SET(j, v) (ft[j] = (v))
-#else
+// The rows' field t (TB:203 of the stored t_us), derived per evaluation (a copy cached in
+// LDS cost occupancy and was slower, profiles/r02_ablate_wide*.log)
 #define WIDE_FT_GET(j, srow) req_time_rel((srow).t_us == kAbsent ? 0 : (srow).t_us, TB, 0).new_t
 #define WIDE_FT_SET(j, v) ((void)0)
-#endif
 
 // Buckets of >= wide_min requests (every nonempty bucket of a dense batch), shaped as above
 // (three workgroups per CU, chunks of 1536 requests).  k_fold below takes the other buckets.
@@ -1390,16 +1340,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kWideTail;
     uint32_t *t_pos = reinterpret_cast<uint32_t *>(aux + kWideTail * 2);   // reply positions
     static_assert(kWideTail * 2 * 8 >= kMaxRows * 4, "hcnt fits in aux");
-#if TBE_WIDE_FT
-    __shared__ double ft[kMaxRows];
-#endif
     __shared__ uint32_t own[kMaxRows];
     __shared__ uint32_t loaded[kMaxRows / 32];
     __shared__ uint32_t dirty[kMaxRows / 32];
-#if TBE_WIDE_TAIL_WALK
-    __shared__ uint16_t tw_sorted[kWideTail];   // tail entries by row
-    __shared__ uint32_t tw_max;
-#endif
 
     const int tid = threadIdx.x;
     // sparse batch: the dense buckets k_bscan listed (dlist); otherwise this block's bucket
@@ -1422,23 +1365,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
         }
     };
-#if TBE_WIDE_EARLY_DMA
-    // A/B: in a dense batch (every bucket here) issue the slice before the error flag and
-    // the bucket bounds are read, so its latency overlaps theirs; an early return waits for
-    // the DMA first (its LDS must not be released under it)
-    const bool early = wide_min <= 1u;
-    if (early) slice_dma();
-    if (*err || bstart[b] == bstart[b + 1]) {
-        if (early) lds_dma_wait();
-        return;
-    }
-    const uint32_t s = bstart[b], e = bstart[b + 1];
-#else
-    constexpr bool early = false;
     if (*err) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     if (s == e) return;
-#endif
     // Buckets with >= wide_min requests only (k_fold takes the others): the whole slice
     // is pulled in (LDS-DMA) and only its dirty lines are written back.
     if (e - s < wide_min) return;
@@ -1480,7 +1409,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     uint32_t pf_sink = 0;
 #endif
     load_chunk(s);   // in flight together with the dense slice
-    if (dense && !early) slice_dma();
+    if (dense) slice_dma();
     for (uint32_t j = tid; j < (R + 31) / 32; j += kWideBlock) {
         loaded[j] = 0;
         dirty[j] = 0;
@@ -1535,39 +1464,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (int r = 0; r < kWidePer; ++r)
                 if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
         }
-#if TBE_WIDE_FT
-        {
-            // First touch of a row in this bucket: claim it and derive its field t (with
-            // the field-t cache only; without it the whole slice is already in LDS and
-            // nothing needs claiming).
-            uint32_t mine = 0;
-#pragma unroll
-            for (int r = 0; r < kWidePer; ++r) {
-                if (pend & (1u << r)) {
-                    const uint32_t bit = 1u << (kl[r] & 31);
-                    if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
-                }
-            }
-            Slot tmp[kWidePer];
-#pragma unroll
-            for (int r = 0; r < kWidePer; ++r) {
-                tmp[r] = Slot{0.0, 0};                   // fully initialised: stays in VGPRs
-                if (mine & (1u << r)) tmp[r] = dense ? row[kl[r]] : rows[kl[r]];
-            }
-#pragma unroll
-            for (int r = 0; r < kWidePer; ++r) {
-                if (mine & (1u << r)) {
-                    if (!dense) row[kl[r]] = tmp[r];
-                    WIDE_FT_SET(kl[r], new_t_of(tmp[r].t_us == kAbsent ? 0 : tmp[r].t_us));
-                }
-            }
-        }
-        ReqTime rq[kWidePer];
-#pragma unroll
-        for (int r = 0; r < kWidePer; ++r) rq[r] = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms)
-                                                           : req_time(tsv[r], P.ttl_ms);
-        __syncthreads();   // claimed rows and their field t visible
-#endif
         uint32_t rep[kWidePer];
 #pragma unroll
         for (int r = 0; r < kWidePer; ++r) rep[r] = 0;
@@ -1587,12 +1483,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 if (pend & (1u << r)) {
                     nrow[r] = row[kl[r]];
                     bool m;
-#if TBE_WIDE_FT
-                    const ReqTime &rqr = rq[r];
-#else
                     // request times recomputed per evaluation (registers: three slots)
                     const ReqTime rqr = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
-#endif
                     rep[r] = tb_step_ft(nrow[r], WIDE_FT_GET(kl[r], nrow[r]), pm[r], rqr, P, m);
                     if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kWideBlock + tid)));
                 }
@@ -1645,80 +1537,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             pend = 0;
             __syncthreads();
             bool tp = (uint32_t)tid < n_tail;
-#if TBE_WIDE_TAIL_WALK
-            // counting sort of the list by row (own[] is free: round 1's tags were read
-            // before the scan above), then one walking thread per row's run
-            for (uint32_t j = tid; j < R; j += kWideBlock) own[j] = 0;
-            if (tid == 0) tw_max = 0;
-            __syncthreads();
-            uint32_t trow = 0, trk = 0;
-            if (tp) {
-                trow = t_kl_lid[tid] & 0xFFFFu;
-                trk = atomicAdd(&own[trow], 1u);
-            }
-            __syncthreads();
-            {
-                constexpr uint32_t RPT = (kMaxRows + kWideBlock - 1) / kWideBlock;
-                uint32_t cn[RPT], sum = 0, mx = 0;
-#pragma unroll
-                for (uint32_t u = 0; u < RPT; ++u) {
-                    const uint32_t j = tid * RPT + u;
-                    cn[u] = j < R ? own[j] : 0u;
-                    sum += cn[u];
-                    mx = cn[u] > mx ? cn[u] : mx;
-                }
-                uint32_t tot;
-                uint32_t st0 = block_excl_scan<kWideBlock>(sum, wsum, &tot);
-#pragma unroll
-                for (uint32_t u = 0; u < RPT; ++u) {
-                    const uint32_t j = tid * RPT + u;
-                    if (j < R) own[j] = st0;
-                    st0 += cn[u];
-                }
-                if (mx) atomicMax(&tw_max, mx);
-            }
-            __syncthreads();
-            if (tp) tw_sorted[own[trow] + trk] = (uint16_t)tid;
-            __syncthreads();
-            if (tw_max <= kWideTailRun) {
-                if (tp) {
-                    const uint32_t rw = t_kl_lid[tw_sorted[tid]] & 0xFFFFu;
-                    const uint32_t start = own[rw];
-                    if ((uint32_t)tid == start) {
-                        const uint32_t stop = (rw + 1 < R) ? own[rw + 1] : n_tail;
-                        for (uint32_t x = start + 1; x < stop; ++x) {   // arrival order
-                            const uint16_t v = tw_sorted[x];
-                            const uint32_t vl = t_kl_lid[v] >> 16;
-                            uint32_t y = x;
-                            while (y > start && (t_kl_lid[tw_sorted[y - 1]] >> 16) > vl) {
-                                tw_sorted[y] = tw_sorted[y - 1];
-                                --y;
-                            }
-                            tw_sorted[y] = v;
-                        }
-                        Slot st = row[rw];
-                        bool mod = false;
-                        for (uint32_t x = start; x < stop; ++x) {
-                            const uint32_t en = tw_sorted[x];
-                            const ReqTime rq1 = PACKED ? req_time_rel(t_ts[en], TB, P.ttl_ms) : req_time(t_ts[en], P.ttl_ms);
-                            bool m;
-                            const uint32_t rp = tb_step_ft(st, WIDE_FT_GET(rw, st), t_pm[en], rq1, P, m);
-                            mod |= m;
-                            put_reply(res, t_pos[en], rp, narrow);
-                        }
-                        if (mod) {
-                            row[rw] = st;
-                            atomicOr(&dirty[rw >> 5], 1u << (rw & 31));
-                        }
-                    }
-                }
-                // the walkers' rows, replies and their reads of own[] are done before the
-                // next chunk resets own[] and reads the rows
-                __syncthreads();
-                tp = false;
-                n_tail = 0;    // block-uniform: skip the rounds below
-            }
-#endif
             uint32_t tkl = 0, tlid = 0, trep = 0, tpos = 0;
             int32_t tpm = 0;
             int64_t tts = 0;
@@ -1737,7 +1555,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             // later rounds run on fewer waves (the fold is VALU-issue bound).
             uint32_t in_use = n_tail;
             for (uint32_t round = 2;; ++round) {
-                if (n_tail == 0) break;   // block-uniform: the tail walk settled the list
+                if (n_tail == 0) break;   // block-uniform
                 const uint32_t tag = (round << 12) | (4095u - tlid);
                 Slot nr = Slot{0.0, 0};
                 if (tp) {
@@ -3183,15 +3001,9 @@ struct QTick {
     uint32_t cap;
 };
 
-// TBE_Q_WALK=1: decide each row's requests in one thread after an LDS counting sort
-// instead of election rounds.  Parity-equal, but the config-D fold takes 3.11 ms against
-// 2.41 for the rounds (profiles/r02_ablate_qwalk.log): off by default.
-#ifndef TBE_Q_WALK
-#define TBE_Q_WALK 0
-#endif
-#if TBE_Q_WALK
-constexpr uint32_t kWalkMax = 32;   // longest per-key run a walking thread sorts
-#endif
+// (Deciding each row's requests in one thread after an LDS counting sort, instead of
+// election rounds, was parity-equal but slower: config-D fold 3.11 against 2.41 ms,
+// profiles/r02_ablate_qwalk.log; removed in round 5.)
 // Tail walk (round 3): after the first owner round, the requests still pending (a key's
 // second, third, ... request of the chunk; about a third of config D's) are sorted by row
 // in LDS and each row's run is decided by one thread in arrival order -- no further
@@ -3236,11 +3048,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     __shared__ uint16_t tw_sorted[kQTail];        // tail entries by row
     __shared__ uint32_t tw_sum[kQBlock / 64];
     __shared__ uint32_t tw_max;
-#endif
-#if TBE_Q_WALK
-    __shared__ uint16_t wsorted[kQChunk];         // the chunk's request indices by row
-    __shared__ uint32_t wsum_q[kQBlock / 64];
-    __shared__ uint32_t wtotal, wmax;
 #endif
 
     if (*err) return;
@@ -3346,9 +3153,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 kl[r] = 0; pm[r] = 0; ts[r] = 0; ai[r] = 0;
             }
         }
-#if !TBE_Q_WALK
         for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;   // election slots of this chunk
-#endif
         uint32_t mine = 0;
 #pragma unroll
         for (int r = 0; r < kQItems; ++r) {
@@ -3372,91 +3177,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 if (mine & (1u << r)) { slot[kl[r]] = tmp[r]; qh[kl[r]] = th[r]; }
         }
         __syncthreads();   // claimed rows and headers visible
-#if TBE_Q_WALK
-        // Walk: sort the chunk's requests by row (LDS counting sort; within a row the
-        // arrival order is restored by the walking thread), then one thread per row
-        // decides its requests in arrival order -- no election rounds.  A chunk whose
-        // busiest key has more than kWalkMax requests takes the rounds below.
-        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
-        if (tid == 0) wmax = 0;
-        __syncthreads();
-        uint32_t off[kQItems];
-#pragma unroll
-        for (int r = 0; r < kQItems; ++r) off[r] = (pend & (1u << r)) ? atomicAdd(&own[kl[r]], 1u) : 0u;
-        __syncthreads();
-        {
-            constexpr uint32_t RPT = (kMaxRows + kQBlock - 1) / kQBlock;
-            uint32_t cn[RPT], sum = 0, mx = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < RPT; ++u) {
-                const uint32_t j = tid * RPT + u;
-                cn[u] = j < R ? own[j] : 0u;
-                sum += cn[u];
-                mx = cn[u] > mx ? cn[u] : mx;
-            }
-            uint32_t tot;
-            uint32_t at = block_excl_scan<kQBlock>(sum, wsum_q, &tot);
-#pragma unroll
-            for (uint32_t u = 0; u < RPT; ++u) {
-                const uint32_t j = tid * RPT + u;
-                if (j < R) own[j] = at;
-                at += cn[u];
-            }
-            if (mx) atomicMax(&wmax, mx);
-            if (tid == 0) wtotal = tot;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kQItems; ++r)
-            if (pend & (1u << r)) wsorted[own[kl[r]] + off[r]] = (uint16_t)(r * kQBlock + tid);
-        __syncthreads();
-        if (wmax <= kWalkMax) {
-            for (uint32_t j = tid; j < R; j += kQBlock) {
-                const uint32_t a = own[j], z = (j + 1 < R) ? own[j + 1] : wtotal;
-                if (a == z) continue;
-                for (uint32_t x = a + 1; x < z; ++x) {           // arrival order (insertion sort)
-                    const uint16_t v = wsorted[x];
-                    uint32_t y = x;
-                    while (y > a && wsorted[y - 1] > v) {
-                        wsorted[y] = wsorted[y - 1];
-                        --y;
-                    }
-                    wsorted[y] = v;
-                }
-                Slot st = slot[j];
-                uint64_t h = qh[j];
-                bool smod = false, hmod = false;
-                uint64_t *__restrict__ kr = ring + (row0 + j) * (uint64_t)Q.cap;
-                for (uint32_t x = a; x < z; ++x) {
-                    const uint32_t q = c + wsorted[x];
-                    int32_t p;
-                    int64_t t;
-                    uint32_t qp = q;
-                    if (PACKED) {
-                        uint32_t k;
-                        fold_input(srec[q], q, G, tbase1, rec0, ts_orig, tbase, F, rmask, k, p, t, qp);
-                    } else {
-                        p = sperm[q];
-                        t = sts[q];
-                    }
-                    uint32_t status, rem;
-                    bool evaluated;
-                    const ReqTime rq1 = req_time_rel(t, TB, P.ttl_ms);
-                    q_step(st, h, smod, hmod, p, rq1, TB, sidx[q], kr, P, Q, ev_cause, ev_id, ev_count, ev_cap, status,
-                           rem, evaluated);
-                    put_wait(res, qp, status, evaluated, rem, narrow);
-                }
-                if (smod) slot[j] = st;
-                if (hmod) qh[j] = h;
-                if (smod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
-                if (hmod) atomicOr(&hdirty[j >> 5], 1u << (j & 31));
-            }
-            __syncthreads();   // the chunk's rows are settled before the next chunk reads them
-            continue;
-        }
-        for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;
-        __syncthreads();
-#endif
         // Owner rounds: each key's earliest pending request wins an election slot tagged
         // (round << 12) | (4095 - chunk index) by atomicMax, so a newer round's tag beats
         // every older one and the slots need no reset between rounds (two barriers per
