@@ -7,19 +7,22 @@
 //
 //   bucket b(key) = key >> r_bits  (2^r_bits keys per bucket; 2^11 at 1e8 keys)
 //   1. LSD stable partition of the requests by b, P = ceil(bits(b)/8) passes of 8 bits:
-//        k_hist    per-tile digit histograms (+ running in-block prefix)
-//        k_colscan digit-column scan of the per-block sums -> global digit offsets
-//        k_scatter stable local rank (wave ballot-match) -> LDS staging -> coalesced runs
+//        k_hist / k_hist_dig  per-tile digit histograms (+ running in-block prefix)
+//        k_colscan            digit-column scan of the per-block sums -> digit offsets
+//        k_scatter_rec        stable local rank (wave ballot-match) -> LDS staging ->
+//                             coalesced runs; the last pass writes fold records
 //      After the last pass the requests are grouped by bucket, arrival order kept inside.
-//   2. k_bounds: first sorted position of every bucket.
-//   3. k_fold: one workgroup per bucket.  The bucket's 2^r_bits table rows are the only
-//      state it touches; rows a request needs are pulled into LDS on first touch.
-//      Requests are taken in arrival order, 1024 at a time; within such a chunk, lanes
-//      whose keys differ decide concurrently while requests for the same key go in
-//      rounds, earliest first (LDS atomicMin "owner" election), so per-key order is the
-//      reference's serial order.  Dirty rows are written back once.
-//   4. k_unscatter: the P partitions run backwards (same local ranks recomputed from the
-//      keys) to return {granted, remaining} in arrival order with coalesced runs.
+//   2. k_bscan_lb: first sorted position of every bucket (decoupled look-back).
+//   3. k_fold_wide: one workgroup per bucket.  The bucket's 2^r_bits table rows (its
+//      slice) are the only state it touches, pulled into LDS by LDS-DMA.  Requests are
+//      taken in arrival order, 1536 at a time; every pending request evaluates the script
+//      against its key's current row and the key's earliest modifying request commits
+//      (speculative rounds, LDS atomicMax election), so per-key order is the reference's
+//      serial order.  Dirty lines are written back once.  Sparse batches: k_fold_sparse
+//      (one wave per bucket); hot keys: their own runs (k_hot_*).
+//   4. k_unscatter: {granted, remaining} back in arrival order through pass 0's
+//      permutation (the fold already put each reply at its pass-0 output position).
+// DESIGN.md §5 describes every kernel.
 //
 // Memory-bound integer/byte work plus a little FP64; no MFMA.
 #include <hip/hip_runtime.h>
@@ -50,32 +53,22 @@ namespace {
 // r01_v10_ablate.log): partition-pass input loads and permutation stores, the
 // un-partition passes, the fold's table slices.  NOT the partition passes' record runs
 // (their partial lines merge in L2: 50% slower streamed) nor the fold's replies (the
-// un-partition gather reuses their lines).  -DTBE_NO_NT turns them off for A/B runs;
-// -DTBE_SLICE_LOAD_CACHED keeps only the slice loads cached (fold 1.17 -> 1.31 ms).
+// un-partition gather reuses their lines).  -DTBE_NO_NT turns them off for A/B runs
+// (slice loads cached instead: fold 1.17 -> 1.31 ms in round 1).
 #ifndef TBE_NO_NT
 #define LD_P(p) ld_nt(p)
 #define ST_PERM(p, v) st_nt((p), (v))
 #define LD_U(p) ld_nt(p)
 #define ST_U(p, v) st_nt((p), (v))
-#ifdef TBE_SLICE_LOAD_CACHED
-#define LD_S(p) (*(p))
-#else
-#define LD_S(p) slot_load_nt(p)
-#endif
 #define ST_S(p, v) slot_store_nt((p), (v))
 #else
 #define LD_P(p) (*(p))
 #define ST_PERM(p, v) (*(p) = (v))
 #define LD_U(p) (*(p))
 #define ST_U(p, v) (*(p) = (v))
-#define LD_S(p) (*(p))
 #define ST_S(p, v) (*(p) = (v))
 #endif
-#ifdef TBE_FOLD_REC_NT
-#define LD_F(p) ld_nt(p)   // A/B: the fold's sorted records streamed
-#else
 #define LD_F(p) (*(p))
-#endif
 #define ST_F(p, v) (*(p) = (v))
 
 #ifndef TBE_PART_BLOCK
@@ -126,14 +119,11 @@ struct HotSet {
 
 __device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - TBE_HOT_SLOT_BITS); }
 constexpr uint64_t kHotSlotEmpty = 0xFFFFFFFFFFFFFFFFull;
-// TBE_HOT_CUCKOO (default on): the table is two halves of kHotSlots/2 slots and a key lives
+// The table is two halves of kHotSlots/2 slots (two-choice cuckoo) and a key lives
 // at hot_h1 in the first half or hot_h2 in the second, so a probe is two independent LDS
 // reads and never a chain.  With linear probing at load 1/4, ~10% of a Zipf batch's
 // lookups continued a chain, so nearly every wave of every tile ran the chain loop
 // (profiles/r03_ablate_hot_probe.log: the probes cost 0.13 + 0.15 ms over uniform).
-#ifndef TBE_HOT_CUCKOO
-#define TBE_HOT_CUCKOO 1
-#endif
 constexpr uint32_t kHotHalf = kHotSlots / 2;
 __device__ __forceinline__ uint32_t hot_h1(uint32_t key) { return (key * 0x9E3779B1u) >> (33 - TBE_HOT_SLOT_BITS); }
 __device__ __forceinline__ uint32_t hot_h2(uint32_t key) {
@@ -162,12 +152,10 @@ __device__ __forceinline__ const uint64_t *hot_table(const HotSet *__restrict__,
 // Partition key of a request: the key itself, or (nb + h) << r_bits for hot key h.
 __device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *slots, uint32_t nb,
                                                 int r_bits) {
-#if TBE_HOT_CUCKOO
     const uint64_t v1 = slots[hot_h1(key)], v2 = slots[hot_h2(key)];
     if ((uint32_t)v1 == key) return (nb + (uint32_t)(v1 >> 32)) << r_bits;
     if ((uint32_t)v2 == key) return (nb + (uint32_t)(v2 >> 32)) << r_bits;
     return key;
-#endif
     uint32_t h = hot_hash(key);
     for (;;) {
         const uint64_t v = slots[h];
@@ -183,7 +171,6 @@ __device__ __forceinline__ uint32_t hot_sortkey(uint32_t key, const uint64_t *sl
 template <int N, typename KeyT>
 __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t *slots, uint32_t nb,
                                              int r_bits, uint32_t (&sk)[N]) {
-#if TBE_HOT_CUCKOO
     // both probes of 4 requests in flight at a time (8 would spill in the hot histogram)
     constexpr int G = N < 4 ? N : 4;
     static_assert(N % G == 0, "groups of G requests");
@@ -204,7 +191,6 @@ __device__ __forceinline__ void hot_sortkeys(const KeyT (&kv)[N], const uint64_t
         }
     }
     return;
-#endif
     uint64_t v[N];
 #pragma unroll
     for (int it = 0; it < N; ++it) v[it] = slots[hot_hash((uint32_t)kv[it])];
@@ -1195,12 +1181,6 @@ constexpr int kFoldChunk = kFoldBlock * kFoldPer;           // 2048
 constexpr int kMaxRows = 1 << kMaxRBits;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ Slot slot_load_nt(const Slot *p) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    Slot s;
-    __builtin_memcpy(&s, &v, sizeof s);
-    return s;
-}
 __device__ __forceinline__ void slot_store_nt(Slot *p, const Slot &s) {
     u32x4 v;
     __builtin_memcpy(&v, &s, sizeof v);
@@ -1223,20 +1203,10 @@ __device__ __forceinline__ void lds_dma_wait() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-#ifndef TBE_REPLY_NT
-#define TBE_REPLY_NT 0
-#endif
 // A token-bucket reply is {granted, trunc(new_v)} with 0 <= trunc(new_v) <= TokenLimit.
 // When TokenLimit <= 127 it travels as one byte (bit 7 granted, bits 0-6 remaining)
 // through the fold and the un-partition passes instead of four.
 __device__ __forceinline__ void put_reply(uint32_t *res, uint32_t q, uint32_t rep, uint32_t narrow) {
-#if TBE_REPLY_NT   // A/B: scattered one-byte replies with the streaming hint
-    if (narrow)
-        __builtin_nontemporal_store((uint8_t)(((rep >> 24) & 0x80u) | (rep & 0x7Fu)), reinterpret_cast<uint8_t *>(res) + q);
-    else
-        __builtin_nontemporal_store(rep, res + q);
-    return;
-#endif
     if (narrow)
         reinterpret_cast<uint8_t *>(res)[q] = (uint8_t)(((rep >> 24) & 0x80u) | (rep & 0x7Fu));
     else
@@ -1293,14 +1263,14 @@ constexpr int kWideTail = TBE_WIDE_TAIL;
 #endif
 // Which buckets k_fold_wide takes is decided per launch (wide_min, fold_wide_min below):
 // the buckets of at least `wide_min` requests.  k_fold_wide pulls its whole 16*R-byte
-// slice by LDS-DMA, k_fold only the rows a bucket touches.
+// slice by LDS-DMA, k_fold_sparse only the rows a bucket touches.
 //  - Dense batches (at least R/32 requests per bucket on average: configs B and C):
 //    every nonempty bucket (wide_min = R >> kWideMinShift = 1 at R = 2048).  On a Zipf
 //    slice, whose buckets hold fewer requests once the hot keys run apart, the wide fold's
-//    24 waves per CU beat k_fold's 12 (round 2, R/32: config C fold 0.89 -> 0.69 ms;
-//    R/2 .. R/2048 measured, profiles/r02_ablate_wide_threshold*.log); round 3 gave it every
-//    bucket and stopped launching k_fold, whose 48828 workgroups that only read their
-//    bucket bounds and exit cost 0.03 ms per batch (profiles/r03_ablate_hot_wide_walk.log).
+//    24 waves per CU beat the workgroup-per-bucket gather fold's 12 (round 2, R/32: config
+//    C fold 0.89 -> 0.69 ms; R/2 .. R/2048 measured, profiles/r02_ablate_wide_threshold*.log);
+//    round 3 gave it every bucket (profiles/r03_ablate_hot_wide_walk.log), and round 5
+//    removed that gather fold (k_fold_sparse took its sparse buckets).
 //  - Sparse batches (fewer than R/8 requests per bucket on average, e.g. 2^20 requests over
 //    1e8 keys, ~21 per bucket): k_fold_wide only for the buckets of at least R/8 requests
 //    (the list k_bscan_lb builds); the others go one wave each to k_fold_sparse, which
@@ -1317,7 +1287,7 @@ static_assert(kWideChunk <= 4096 && kWideTail <= kWideBlock, "election tags and 
 #define WIDE_FT_SET(j, v) ((void)0)
 
 // Buckets of >= wide_min requests (every nonempty bucket of a dense batch), shaped as above
-// (three workgroups per CU, chunks of 1536 requests).  k_fold below takes the other buckets.
+// (three workgroups per CU, chunks of 1536 requests).  k_fold_sparse takes the other buckets.
 template <bool PACKED>
 __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
@@ -1368,7 +1338,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     if (*err) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
     if (s == e) return;
-    // Buckets with >= wide_min requests only (k_fold takes the others): the whole slice
+    // Buckets with >= wide_min requests only (k_fold_sparse takes the others): the whole slice
     // is pulled in (LDS-DMA) and only its dirty lines are written back.
     if (e - s < wide_min) return;
     const bool dense = true;
@@ -1668,319 +1638,11 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 #endif
 }
 
-// k_fold's shape: 256-thread workgroups, 4 requests per thread per chunk, 48.5 KB of
-// LDS, so three workgroups share a CU (the fold is latency-bound: one workgroup per CU
-// instead of two doubles its time, profiles/r01_v11_ablate_occupancy.log).  The row's
-// field t is derived per evaluation (field_t) instead of being cached in LDS.
-constexpr int kTbBlock = 256;
-#ifndef TBE_TB_PER
-#define TBE_TB_PER 4
-#endif
-#ifndef TBE_TB_TAIL
-#define TBE_TB_TAIL kTbBlock
-#endif
-constexpr int kTbPer = TBE_TB_PER;
-constexpr int kTbTail = TBE_TB_TAIL;                      // compact pending list after round 1
-constexpr int kTbChunk = kTbBlock * kTbPer;               // 1024 requests per chunk
-constexpr int kTailPer = kTbTail / kTbBlock;              // its entries per thread
 constexpr int64_t kRowWindow = (int64_t)1 << 31;          // field_t fast path: rows up to ~35 min older
 
 // Field t of a stored row (TB:203 applied to t_us; only used while the key is present).
 __device__ __forceinline__ double field_t(int64_t t_us, const TimeBase &B) {
     return req_time_rel(t_us == kAbsent ? 0 : t_us, B, 0).new_t;
-}
-
-template <bool PACKED>
-__global__ __launch_bounds__(kTbBlock) void k_fold(
-    const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
-    const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
-    const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
-    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
-    uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
-    uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0) {
-    __shared__ Slot row[kMaxRows];
-    // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
-    // compact list of requests still pending after round 1 (t_*)
-    __shared__ uint32_t aux[kMaxRows];
-    __shared__ uint32_t wsum[kTbBlock / 64];
-    uint32_t *hcnt = aux;
-    uint32_t *t_kl_lid = aux;
-    int32_t *t_pm = reinterpret_cast<int32_t *>(aux) + kTbTail;
-    int64_t *t_ts = reinterpret_cast<int64_t *>(aux) + kTbTail;
-    uint32_t *t_pos = aux + 4 * kTbTail;                       // reply positions
-    static_assert(kTbTail * 20 <= kMaxRows * 4, "tail list fits in aux");
-    static_assert(kTbChunk <= 4096, "election tags hold 12-bit local ids");
-    __shared__ uint32_t own[kMaxRows];
-    __shared__ uint32_t loaded[kMaxRows / 32];
-    __shared__ uint32_t dirty[kMaxRows / 32];
-
-    if (*err) return;
-    const int tid = threadIdx.x;
-    const uint32_t b = fold_bucket(G);
-    if (G.on && b >= G.nb) return;
-    const uint32_t s = bstart[b], e = bstart[b + 1];
-    if (s == e) return;
-    const uint32_t R = 1u << r_bits;
-    const uint32_t rmask = R - 1;
-    const uint64_t row0 = (uint64_t)b << r_bits;
-    const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
-    Slot *__restrict__ rows = table + row0;
-    if (e - s >= wide_min) return;   // k_fold_wide's
-    // Whole slice (dense) or touched rows only (sparse), decided below.
-    bool dense = false;
-    const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
-    const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    // one time base for request times and row field times: kRowWindow below the packed
-    // base, so rows granted up to ~35 minutes before the batch also take the fast path
-    const TimeBase TB = time_base(PACKED ? tbase - kRowWindow : -1, P.ttl_ms);
-    const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
-
-    uint32_t kl[kTbPer];
-    int32_t pm[kTbPer];
-    int64_t tsv[kTbPer];
-    uint32_t pos[kTbPer];   // where each request's reply goes (FoldFmt), or its sorted position
-    uint32_t pend = 0;
-    auto load_chunk = [&](uint32_t c) {
-        pend = 0;
-#pragma unroll
-        for (int r = 0; r < kTbPer; ++r) {
-            const uint32_t q = c + r * kTbBlock + tid;
-            kl[r] = 0;
-            pm[r] = 0;
-            tsv[r] = 0;
-            pos[r] = q;
-            if (q < e) {
-                if (PACKED) {
-                    fold_input(LD_F(srec + q), q, G, tbase1, rec0, ts_orig, tbase, F, rmask, kl[r], pm[r],
-                               tsv[r], pos[r]);
-                } else {
-                    kl[r] = skeys[q] & rmask;
-                    pm[r] = sperm[q];
-                    tsv[r] = sts[q];
-                }
-                pend |= 1u << r;
-            }
-        }
-    };
-    load_chunk(s);   // in flight together with the dense slice
-    if (!dense && (e - s) >= (R >> 3)) {
-        // Between R/8 and R/2 requests the distinct rows of the first chunk decide:
-        // uniform traffic touches nearly every 128-byte line of the slice, skewed traffic
-        // (few keys, many requests each) a fraction of them, which it gathers instead.
-        for (uint32_t j = tid; j < (R + 31) / 32; j += kTbBlock) dirty[j] = 0;
-        __syncthreads();
-        uint32_t first = 0;
-#pragma unroll
-        for (int r = 0; r < kTbPer; ++r) {
-            if (pend & (1u << r)) {
-                const uint32_t bit = 1u << (kl[r] & 31);
-                if (!(atomicOr(&dirty[kl[r] >> 5], bit) & bit)) ++first;
-            }
-        }
-        uint32_t distinct;
-        (void)block_excl_scan<kTbBlock>(first, wsum, &distinct);
-        dense = distinct >= (R >> 2);
-    }
-    if (dense) {
-        constexpr int kHalf = kMaxRows / kTbBlock / 2;   // two rounds of 4 rows per thread
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            Slot tmp[kHalf];
-#pragma unroll
-            for (int u = 0; u < kHalf; ++u) {
-                const uint32_t j = tid + (h * kHalf + u) * kTbBlock;
-                tmp[u] = LD_S(rows + (j < nrows ? j : nrows - 1));   // unconditional: keeps tmp in VGPRs
-            }
-#pragma unroll
-            for (int u = 0; u < kHalf; ++u) {
-                const uint32_t j = tid + (h * kHalf + u) * kTbBlock;
-                if (j < nrows) row[j] = tmp[u];
-            }
-        }
-    }
-    for (uint32_t j = tid; j < (R + 31) / 32; j += kTbBlock) {
-        loaded[j] = 0;
-        dirty[j] = 0;
-    }
-
-    for (uint32_t c = s; c < e; c += kTbChunk) {
-        if (c != s) load_chunk(c);
-        for (uint32_t j = tid; j < R; j += kTbBlock) own[j] = 0;
-        if (count_hot && c == s)
-            for (uint32_t j = tid; j < R; j += kTbBlock) hcnt[j] = 0;
-        lds_dma_wait();    // (first chunk) this wave's slice DMA landed
-        __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
-        if (count_hot) {
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r)
-                if (pend & (1u << r)) atomicAdd(&hcnt[kl[r]], 1u);
-        }
-        if (!dense) {
-            // First touch of a row in a sparse bucket: claim it and pull it into LDS.
-            uint32_t mine = 0;
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r) {
-                if (pend & (1u << r)) {
-                    const uint32_t bit = 1u << (kl[r] & 31);
-                    if (!(atomicOr(&loaded[kl[r] >> 5], bit) & bit)) mine |= 1u << r;
-                }
-            }
-            Slot tmp[kTbPer];
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r) {
-                tmp[r] = Slot{0.0, 0};                   // fully initialised: stays in VGPRs
-                if (mine & (1u << r)) tmp[r] = rows[kl[r]];
-            }
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r)
-                if (mine & (1u << r)) row[kl[r]] = tmp[r];
-        }
-        __syncthreads();   // claimed rows visible
-        uint32_t rep[kTbPer];
-#pragma unroll
-        for (int r = 0; r < kTbPer; ++r) rep[r] = 0;
-        // Speculative rounds.  Every pending request evaluates the script
-        // against its key's current row.  An evaluation that does not modify the row (a
-        // deny without expiry) leaves it as it found it, so the key's pending requests up
-        // to its earliest modifying one are decided by this round's evaluations; that
-        // earliest one commits the row it computed and later ones wait for the next
-        // round.  A key whose requests in the chunk all deny settles in one round.
-        // Election slot: (round << 12) | (4095 - local id); the max is the key's earliest
-        // modifier of the newest round, so no reset between rounds.  Workgroup-uniform
-        // loops: every thread runs every round and the only exits are __syncthreads_or.
-        auto eval_slots = [&](uint32_t round, Slot (&nrow)[kTbPer]) {
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r) {
-                nrow[r] = Slot{0.0, 0};
-                if (pend & (1u << r)) {
-                    nrow[r] = row[kl[r]];
-                    bool m;
-                    const ReqTime rq = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
-                    rep[r] = tb_step_ft(nrow[r], field_t(nrow[r].t_us, TB), pm[r], rq, P, m);
-                    if (m) atomicMax(&own[kl[r]], (round << 12) | (4095u - (uint32_t)(r * kTbBlock + tid)));
-                }
-            }
-        };
-        auto resolve_slots = [&](uint32_t round, const Slot (&nrow)[kTbPer]) {
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r) {
-                if (!(pend & (1u << r))) continue;
-                const uint32_t tag = (round << 12) | (4095u - (uint32_t)(r * kTbBlock + tid));
-                const uint32_t o = own[kl[r]];
-                if ((o >> 12) != round || o < tag) {
-                    pend &= ~(1u << r);             // before the key's first modifier: decided
-                } else if (o == tag) {
-                    row[kl[r]] = nrow[r];           // the row this round's evaluation produced
-                    atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
-                    pend &= ~(1u << r);
-                }
-            }
-        };
-        {
-            Slot nrow[kTbPer];
-            eval_slots(1u, nrow);
-            __syncthreads();
-            resolve_slots(1u, nrow);
-        }
-        // Round 1 settles every key's first request.  The few left pending move to a
-        // compact list (one per thread) so later rounds evaluate one request per thread
-        // instead of every slot of every lane.
-        uint32_t n_tail;
-        const uint32_t tail_at = block_excl_scan<kTbBlock>(__popc(pend), wsum, &n_tail);
-        uint32_t keep = ~0u;                     // slots whose reply this thread stores
-        if (n_tail != 0 && n_tail <= kTbTail && !count_hot) {
-            uint32_t at = tail_at;
-#pragma unroll
-            for (int r = 0; r < kTbPer; ++r) {
-                if (pend & (1u << r)) {
-                    t_kl_lid[at] = kl[r] | ((uint32_t)(r * kTbBlock + tid) << 16);
-                    t_pm[at] = pm[r];
-                    t_ts[at] = tsv[r];
-                    t_pos[at] = pos[r];
-                    ++at;
-                }
-            }
-            keep = ~pend;
-            pend = 0;
-            __syncthreads();
-            bool tp[kTailPer];
-            uint32_t tkl[kTailPer], tlid[kTailPer], trep[kTailPer];
-            int32_t tpm[kTailPer];
-            ReqTime trq[kTailPer];
-#pragma unroll
-            for (int i = 0; i < kTailPer; ++i) {
-                const uint32_t x = tid + i * kTbBlock;
-                tp[i] = x < n_tail;
-                tkl[i] = tlid[i] = trep[i] = 0;
-                tpm[i] = 0;
-                trq[i] = ReqTime{0.0, 0, 0};
-                if (tp[i]) {
-                    tkl[i] = t_kl_lid[x] & 0xFFFFu;
-                    tlid[i] = t_kl_lid[x] >> 16;
-                    tpm[i] = t_pm[x];
-                    trq[i] = PACKED ? req_time_rel(t_ts[x], TB, P.ttl_ms) : req_time(t_ts[x], P.ttl_ms);
-                }
-            }
-            for (uint32_t round = 2;; ++round) {
-                Slot nr[kTailPer];
-#pragma unroll
-                for (int i = 0; i < kTailPer; ++i) {
-                    nr[i] = Slot{0.0, 0};
-                    if (tp[i]) {
-                        nr[i] = row[tkl[i]];
-                        bool m;
-                        trep[i] = tb_step_ft(nr[i], field_t(nr[i].t_us, TB), tpm[i], trq[i], P, m);
-                        if (m) atomicMax(&own[tkl[i]], (round << 12) | (4095u - tlid[i]));
-                    }
-                }
-                __syncthreads();
-                bool any = false;
-#pragma unroll
-                for (int i = 0; i < kTailPer; ++i) {
-                    if (!tp[i]) continue;
-                    const uint32_t tag = (round << 12) | (4095u - tlid[i]);
-                    const uint32_t o = own[tkl[i]];
-                    if ((o >> 12) != round || o < tag) {
-                        tp[i] = false;
-                    } else if (o == tag) {
-                        row[tkl[i]] = nr[i];
-                        atomicOr(&dirty[tkl[i] >> 5], 1u << (tkl[i] & 31));
-                        tp[i] = false;
-                    }
-                    if (!tp[i]) put_reply(res, t_pos[tid + i * kTbBlock], trep[i], narrow);
-                    any |= tp[i];
-                }
-                if (!__syncthreads_or(any)) break;
-            }
-        } else if (n_tail != 0) {
-            for (uint32_t round = 2;; ++round) {
-                Slot nrow[kTbPer];
-                eval_slots(round, nrow);
-                __syncthreads();
-                resolve_slots(round, nrow);
-                if (!__syncthreads_or(pend != 0)) break;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < kTbPer; ++r) {
-            const uint32_t q = c + r * kTbBlock + tid;
-            if (q < e && (keep & (1u << r))) put_reply(res, pos[r], rep[r], narrow);
-        }
-    }
-    __syncthreads();
-    // modified rows (sparse) or dirty lines (dense) stream out (non-temporal: 12% faster
-    // fold, profiles/r01_v10_ablate_nt_variants.log)
-    for (uint32_t j = tid; j < nrows; j += kTbBlock)
-        if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, row[j]);
-    if (count_hot) {
-        // nominate this bucket's hot keys for their own runs in the next batch
-        for (uint32_t j = tid; j < nrows; j += kTbBlock) {
-            if (hcnt[j] >= kHotMin) {
-                const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
-                if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)hcnt[j] << 32) | (uint32_t)(row0 + j);
-            }
-        }
-    }
 }
 
 // Sparse buckets of a sparse batch (fewer than wide_min requests; 2^20 requests over 1e8
@@ -1994,9 +1656,6 @@ __global__ __launch_bounds__(kTbBlock) void k_fold(
 // buckets, and each wave fetches the bounds of all its buckets with one load per lane.
 // A bucket of more than 64 requests goes in chunks of 64; a key's row written back by one
 // chunk is re-read by the next after a workgroup-scope fence.
-#ifndef TBE_SPARSE_WAVE
-#define TBE_SPARSE_WAVE 1
-#endif
 constexpr int kSpBlock = 256;
 constexpr int kSpWaves = kSpBlock / 64;
 template <bool PACKED>
@@ -2268,12 +1927,6 @@ __global__ __launch_bounds__(kPartBlock) void k_unrank(uint64_t n, const uint8_t
 //   k_hot_replies  (parallel)  decides every request of a pass-through segment against
 //                              the S it saw.
 // Which keys are hot only changes speed, never a decision.
-#ifndef TBE_HOT_SPEC
-#define TBE_HOT_SPEC 1
-#endif
-#ifndef TBE_HOT_SAMPLE
-#define TBE_HOT_SAMPLE 1
-#endif
 constexpr int kSegBlock = kFoldBlock;
 constexpr int kSegItems = 16;   // (8: no faster, 4: slower; profiles/r05u_ablate_hot_segments.log)
 constexpr uint32_t kSeg = kSegBlock * kSegItems;  // 8192 requests per run segment
@@ -2292,23 +1945,8 @@ struct SegState {
 };
 
 
-// segbase[h] = first segment of run h; segbase[kHotKeysMax] = all segments.  One 1024-
-// thread workgroup.
-__global__ __launch_bounds__(1024) void k_hot_plan(const HotSet *__restrict__ hot,
-                                                   const uint32_t *__restrict__ bstart, uint32_t nb,
-                                                   uint32_t *__restrict__ segbase,
-                                                   const uint32_t *__restrict__ err) {
-    __shared__ uint32_t wsum[16];
-    if (*err) return;
-    const uint32_t h = threadIdx.x;
-    uint32_t ns = 0;
-    if (h < hot->count) ns = (bstart[nb + h + 1] - bstart[nb + h] + kSeg - 1) / kSeg;
-    uint32_t total;
-    const uint32_t pre = block_excl_scan<1024>(ns, wsum, &total);
-    segbase[h] = pre;
-    if (h == 0) segbase[kHotKeysMax] = total;
-}
-
+// segbase[h] = first segment of run h; segbase[kHotKeysMax] = all segments (the scan
+// k_hot_summary's workgroups do, workgroup 0 publishing it).
 // Run h of segment j: the last h with segbase[h] <= j.
 __device__ __forceinline__ uint32_t seg_run(const uint32_t *segbase, uint32_t j) {
     uint32_t lo = 0, hi = kHotKeysMax;   // segbase[lo] <= j < segbase[hi]
@@ -2320,7 +1958,7 @@ __device__ __forceinline__ uint32_t seg_run(const uint32_t *segbase, uint32_t j)
     return lo;
 }
 
-// SPEC (TBE_HOT_SPEC, the default): also decide the segment here when it passes the run's
+// SPEC (the form launched): also decide the segment here when it passes the run's
 // row as it stands before the batch (S0, table[key]) through -- the test k_hot_chain makes
 // first, on the same summary -- so in the steady state, where a run's segments all pass
 // (a hot key is mostly denied), k_hot_replies reads the run a second time only behind a
@@ -2340,7 +1978,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     if (*err) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (plan) {
-        // k_hot_plan's scan, done by every workgroup (1024 run lengths from the bucket
+        // the runs' segment scan, done by every workgroup (1024 run lengths from the bucket
         // starts); workgroup 0 publishes segbase for k_hot_chain and k_hot_replies
         static_assert(kHotKeysMax == 2 * kSegBlock, "two runs per thread");
         const uint32_t cnt = hot->count;
@@ -2635,7 +2273,6 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
         }
     }
     const uint32_t nh = min(nc, cap);
-#if TBE_HOT_CUCKOO
     // Two-choice placement in LDS (c is reused as the table once every thread holds its
     // key): a CAS into the key's first-half slot, else its second-half slot; the few keys
     // that lose both (~1% at load 1/4) are placed by thread 0 with cuckoo kicks.  A key
@@ -2682,21 +2319,6 @@ __global__ __launch_bounds__(1024) void k_hot_update(HotSet *__restrict__ next, 
     }
     __syncthreads();
     for (uint32_t j = t; j < kHotSlots; j += 1024) next->slot[j] = c[j];
-#else
-    if (t < nh) {
-        const uint32_t key = (uint32_t)c[t];
-        next->key[t] = key;
-        const unsigned long long mine = ((unsigned long long)t << 32) | key;
-        uint32_t h = hot_hash(key);
-        for (;;) {
-            const unsigned long long old = atomicCAS(
-                reinterpret_cast<unsigned long long *>(&next->slot[h]), kHotSlotEmpty, mine);
-            if (old == kHotSlotEmpty) break;
-            if ((uint32_t)old == key) break;        // nominated twice: one run is enough
-            h = (h + 1) & (kHotSlots - 1);
-        }
-    }
-#endif
     if (t == 0) next->count = nh;
 }
 
@@ -3524,11 +3146,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
     // local-tier slice with coalesced streaming loads and writes it back whole; a sparse one
     // gathers the rows it touches.  (Round 1 dropped this variant after a wrong result that
     // the rebuilt variant does not reproduce -- DESIGN.md §5 "Streaming hints".)
-#ifdef TBE_APPROX_NO_DENSE
-    constexpr bool dense = false;
-#else
     const bool dense = (e - s) >= (R >> 3);
-#endif
     if (dense) {
         // HBM -> LDS directly (LDS-DMA, streaming policy; rows past nrows get a copy of
         // the last row, which nothing reads or writes back)
@@ -4199,36 +3817,24 @@ inline void stage_end(tbe_engine *e, int s, hipStream_t st) {
 }
 
 // The token-bucket fold's density gate (see kWideMinShift): k_fold_wide takes the buckets
-// of at least the returned number of requests, k_fold the rest (launched only when this is
-// above 1).  Dense batches give every nonempty bucket to k_fold_wide; sparse ones only the
-// buckets of >= R/8 requests.  TBE_FOLD_NARROW_ONLY (A/B): k_fold takes every bucket.
+// of at least the returned number of requests, k_fold_sparse the rest (a sparse batch: the
+// returned number is above 1).  Dense batches give every nonempty bucket to k_fold_wide;
+// sparse ones only the buckets of >= R/8 requests.
 #ifndef TBE_SPARSE_GATE_SHIFT
 #define TBE_SPARSE_GATE_SHIFT 3              // sparse batch: fewer than R >> this requests per bucket
 #endif
 uint32_t fold_wide_min(const tbe_engine *e, uint64_t n) {
-#ifdef TBE_FOLD_NARROW_ONLY
-    (void)e;
-    (void)n;
-    return 0xFFFFFFFFu;
-#else
     const uint32_t R = 1u << e->r_bits;
     const uint32_t all = std::max(1u, R >> kWideMinShift);
     if (n >= (uint64_t)e->nbuckets * std::max(1u, R >> TBE_SPARSE_GATE_SHIFT)) return all;
     return std::max(all, R >> 3);
-#endif
 }
 
 #ifndef TBE_HOT_SPARSE_MIN_LOG2
 #define TBE_HOT_SPARSE_MIN_LOG2 20           // sparse batches below 2^this take no hot-key runs
 #endif
 // Run slots the per-batch sampler keeps free of fold nominations (k_hot_sample)
-inline uint32_t hot_reserve_host(uint32_t cap) {
-#if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
-    return std::min(32u, cap / 4u);
-#else
-    return 0u;
-#endif
-}
+inline uint32_t hot_reserve_host(uint32_t cap) { return std::min(32u, cap / 4u); }
 
 // Fold records for a batch of n requests: the reply position takes ceil_log2(n) bits, the
 // time offset what is left (>= 8 bits, else the plain records).  tbe_batch_format reports it.
@@ -4307,7 +3913,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     // token bucket: a sparse batch's dense buckets are listed for k_fold_wide, the rest go to
     // one wave each (k_fold_sparse)
     const uint32_t tb_wmin = (!approx && !wait) ? fold_wide_min(e, n) : 1u;
-    const bool sparse_tb = TBE_SPARSE_WAVE && tb_wmin > 1u;
+    const bool sparse_tb = tb_wmin > 1u;
     // hot runs: see tbe_engine::hot.  Not in a sparse batch below 2^20 requests (the
     // micro-batch regime): there a key busy enough to matter fills one dense bucket, which
     // k_fold_wide takes whole, and the hot machinery (the sampler, four launches) costs more
@@ -4317,10 +3923,8 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     const bool hot_on = e->hot_cap && !(sparse_tb && n < (1ull << TBE_HOT_SPARSE_MIN_LOG2));
     HotSet *hot = hot_on ? e->hot[e->nbatch % 3] : nullptr;
     HotSet *hot_next = hot_on ? e->hot[(e->nbatch + 2) % 3] : nullptr;
-#if TBE_HOT_SAMPLE && TBE_HOT_CUCKOO
     // every batch: its dominant keys join its own hot set (k_hot_sample)
     if (hot && n >= kHotSampleMin) k_hot_sample<<<1, 1024, 0, sp>>>(keys, n, e->cfg.n_keys, hot, e->hot_cap);
-#endif
     for (int p = 0; p < e->passes; ++p) {
         const int shift = e->r_bits + kDigitBits * p;
         PassBufs &out = w.pass[p];
@@ -4506,25 +4110,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
                 e->cfg.n_keys, e->table, e->params, w.res[0], w.err, 0u, tb_wmin, G, rec0, walk);
         }
-    } else if (e->packed) {
-        // dense buckets in k_fold_wide, the others in k_fold (each skips the other's)
-        const uint32_t wmin = tb_wmin;
+    } else if (e->packed) {   // a dense batch: k_fold_wide takes every bucket
         k_fold_wide<true><<<fold_grid, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
-        if (wmin > 1u)   // else k_fold_wide takes every bucket
-            k_fold<true><<<fold_grid, kTbBlock, 0, sf>>>(
-                nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, wmin, G, rec0);
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0);
     } else {
-        const uint32_t wmin = tb_wmin;
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin, G, rec0);
-        if (wmin > 1u)
-            k_fold<false><<<e->nbuckets, kTbBlock, 0, sf>>>(
-                sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart,
-                e->r_bits, e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, wmin, G, rec0);
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {
@@ -4532,19 +4125,14 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         // unchanged row as part of its bucket's slice), then the hot set of batch b+2
         stage_begin(e, ST_HOT, sf);
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
-        if (TBE_HOT_SPEC)   // (the summary kernel also does k_hot_plan's scan)
-            k_hot_summary<true><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
+        // (the summary kernel also scans the run lengths into the runs' first segments)
+        k_hot_summary<true><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                              w.segbase, w.summ, w.err, G, rec0, hot, e->table,
                                                              e->params, w.res[0], e->narrow ? 1u : 0u, 1u);
-        else
-            k_hot_plan<<<1, 1024, 0, sf>>>(hot, w.bstart, e->nbuckets, w.segbase, w.err);
-        if (!TBE_HOT_SPEC)
-            k_hot_summary<false><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                              w.segbase, w.summ, w.err, G, rec0);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
                                                       hot_next, w.segbase, w.summ, w.sst, e->table,
                                                       e->params, w.res[0], w.err, e->narrow ? 1u : 0u, G, rec0,
-                                                      TBE_HOT_SPEC ? 1u : 0u);
+                                                      1u);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
                                                    w.segbase, w.sst, e->params, w.res[0], w.err, e->narrow ? 1u : 0u,
                                                    G, rec0);
@@ -5814,7 +5402,7 @@ tbe_status tbe_batch_format(const tbe_engine *e, uint64_t n, uint32_t *out, uint
     out[7] = (uint32_t)e->r_bits;
     if (n_out > 8) {   // 1: a sparse token-bucket batch (k_fold_sparse + listed dense buckets, no hot runs)
         const bool tb = e->cfg.kind == TBE_KIND_TOKEN_BUCKET;
-        out[8] = (tb && TBE_SPARSE_WAVE && fold_wide_min(e, n) > 1u) ? 1u : 0u;
+        out[8] = (tb && fold_wide_min(e, n) > 1u) ? 1u : 0u;
     }
     return TBE_OK;
 }

@@ -36,17 +36,12 @@ VARIANT_SETS = {
         "slots4096_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "slots2048_z": (["TBE_HOT_SLOT_BITS=11"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "wideall_z": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "gprobe_z": (["TBE_HOT_PROBE_GLOBAL=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "wideall_u": (["TBE_WIDE_MIN_SHIFT=11"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
-        "rounds_u": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
-        "rounds_z": (["TBE_WIDE_TAIL_WALK=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "recnt": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
-        "recnt_u": (["TBE_FOLD_REC_NT"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "recnt_z": (["TBE_FOLD_REC_NT"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "qshape": {
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
@@ -89,7 +84,6 @@ VARIANT_SETS = {
     },
     "probe": {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "noprobe_z": (["TBE_HOT_NOPROBE_AB"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
     },
@@ -111,7 +105,6 @@ VARIANT_SETS = {
         "unall_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--unscatter-all"]),
         "s0w6_z": (["TBE_SCATTER0_WAVES=6"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "histrec_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir", "--hist-records"]),
-        "linprobe_z": (["TBE_HOT_CUCKOO=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
         "unall_q": ([], ["--workload", "queue", "--no-drain-variant", "--unscatter-all"]),
         "base_a": ([], ["--workload", "approx"]),
@@ -159,27 +152,18 @@ VARIANT_SETS = {
         "base_a": ([], ["--workload", "approx"]),
         "apf384_a": (["TBE_AFOLD_PREFETCH=384"], ["--workload", "approx"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "nospec_z": (["TBE_HOT_SPEC=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "hotw8_z": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "hotw8_u": (["TBE_HIST_HOT_WAVES=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "edma_u": (["TBE_WIDE_EARLY_DMA=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
     "r04f": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "prestage_u": (["TBE_LAST_PRESTAGE=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "replynt_u": (["TBE_REPLY_NT=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "prestage_z": (["TBE_LAST_PRESTAGE=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "replynt_z": (["TBE_REPLY_NT=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-drain-variant"]),
-        "replynt_q": (["TBE_REPLY_NT=1"], ["--workload", "queue", "--no-drain-variant"]),
     },
     "r04g": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "nosample_u": (["TBE_HOT_SAMPLE=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "nosample_z": (["TBE_HOT_SAMPLE=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "wipE": {
         "base_a": ([], ["--workload", "approx"]),
@@ -201,13 +185,10 @@ VARIANT_SETS = {
     },
     "hs": {
         "small_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "big_u": (["TBE_HS_SMALL=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "small_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "big_z": (["TBE_HS_SMALL=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "seg": {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "nostore_z": (["TBE_HOT_NO_REPLY_STORE"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
     },
     "pipe": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
