@@ -1,4 +1,4 @@
-"""The token-bucket fold (k_fold_wide / k_fold) against the C restatement, bit for bit, on
+"""The token-bucket fold (k_fold_wide / k_fold_sparse) against the C restatement, bit for bit, on
 bucket shapes chosen to land in every path: full single-chunk buckets (config B's),
 buckets with rows of many requests, multi-chunk buckets, sparse buckets, a partial last
 bucket, expiry deletions, zero and over-limit permits, one- and four-byte replies."""

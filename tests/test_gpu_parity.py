@@ -453,10 +453,10 @@ def test_fold_records_layouts(engine_lib, gpu, case, fold, digits, rerank):
     two passes; timestamps spread over hours (fold records escape to the previous pass's
     record, itself escaping to the caller's array); hot-key runs; three passes (> 2^27
     keys: 65536 reply regions); a sparse batch (the density gate sends its buckets to
-    k_fold).  rerank: the final un-partition re-ranks pass 0's tiles (k_unrank) instead of
+    k_fold_sparse).  rerank: the final un-partition re-ranks pass 0's tiles (k_unrank) instead of
     gathering through pass 0's permutation.  hist_records: the second pass's histogram
-    reads the first pass's records instead of the digit stream (k_hist_dig), whose tiles here lie inside one pass-0 digit,
-    straddle a few or (sparse) span many."""
+    reads the first pass's records instead of the digit stream (k_hist_dig), whose tiles
+    here lie inside one pass-0 digit, straddle a few or (sparse) span many."""
     rng = np.random.default_rng(zlib.crc32(case.encode()) % 1000)
     n_keys = {"three_pass": 140_000_000, "sparse": 100_000_000}.get(case, 3_000_000)
     n = {"sparse": 1 << 16, "three_pass": 300_000}.get(case, 400_000)
