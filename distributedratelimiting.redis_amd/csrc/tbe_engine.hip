@@ -2605,9 +2605,9 @@ __device__ __forceinline__ uint32_t drain_key(uint64_t key, Slot &st, uint64_t &
     }
     if (WRITE) {
         st = s;
-        smod |= m_any;
         if (seq) h = qh_pack(head, cnt, qsum);
     }
+    smod |= m_any;   // (WRITE = false: whether the writing pass would change the row)
     return seq;
 }
 
@@ -2963,7 +2963,12 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         const ReqTime rqT = req_time(T.ts, P.ttl_ms);
         const DrainLog L{T.keyseq, T.id, T.rem, T.cap};
         constexpr uint32_t kRowsPer = (kMaxRows + kQBlock - 1) / kQBlock;
+        static_assert(kRowsPer <= 32, "one bit per row of this thread");
         uint32_t mine = 0;
+        // rows whose writing pass changes something: it grants, or its one-permit probe
+        // lapsed the key (passive expiry); every other row's writing pass is a no-op, and
+        // in config D's steady state (ticks that grant nothing) that is every row
+        uint32_t need = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kRowsPer; ++u) {
             const uint32_t j = tid + u * kQBlock;
@@ -2971,7 +2976,10 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 Slot st = slot[j];
                 uint64_t h = qh[j];
                 bool sm = false;
-                mine += drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P, Q, L, 0);
+                const uint32_t g = drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P,
+                                                    Q, L, 0);
+                mine += g;
+                if (g || sm) need |= 1u << u;
             }
         }
         uint32_t total;
@@ -2984,7 +2992,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
 #pragma unroll
         for (uint32_t u = 0; u < kRowsPer; ++u) {
             const uint32_t j = tid + u * kQBlock;
-            if (j < nrows) {
+            if ((need >> u) & 1u) {
                 Slot st = slot[j];
                 uint64_t h = qh[j];
                 const uint64_t h0 = h;
@@ -3042,7 +3050,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
         const uint32_t off = block_excl_scan<kBlock>(mine, wsum, &total);
         if (threadIdx.x == 0) log_base = total ? atomicAdd(log_count, total) : 0u;
         __syncthreads();
-        if (queued) {
+        if (queued && (mine != 0 || sm)) {   // (else the writing pass is a no-op)
             bool smod = false;
             const uint64_t hb = h;
             drain_key<true>(key, st, h, smod, kr, rqT, P, Q, L, log_base + off);
@@ -4223,6 +4231,25 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
 }  // namespace
 
 // ============================================================================= C ABI
+// Resident state allocated physically contiguous where the driver can give it (else an
+// ordinary allocation): TBE_CONTIG_ALLOC bit 0 the bucket table, 1 the queue headers, 2 the
+// rings, 3 the approximate local tier.  The rings by default: every enqueue is one
+// scattered 8-byte store into 12.8 GB (config D), and contiguous memory took config D
+// from 4.17 to 3.93 ms per step (bimodal 3.8 / 4.2 ms before); the others were neutral
+// or slightly slower (profiles/r05yab_ablate_contig.log).
+#ifndef TBE_CONTIG_ALLOC
+#define TBE_CONTIG_ALLOC 4
+#endif
+template <typename T>
+hipError_t big_alloc(T **p, size_t bytes, int what) {
+    if ((TBE_CONTIG_ALLOC >> what) & 1) {
+        if (hipExtMallocWithFlags(reinterpret_cast<void **>(p), bytes, hipDeviceMallocContiguous) == hipSuccess)
+            return hipSuccess;
+        (void)hipGetLastError();
+    }
+    return hipMalloc(reinterpret_cast<void **>(p), bytes);
+}
+
 extern "C" {
 
 double tbe_fill_rate(int32_t tokens_per_period, int64_t replenishment_period_ticks) {
@@ -4359,7 +4386,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ev_hot, &e->ws[0].done, &e->ws[1].done,
                            &e->ws[0].hot_done, &e->ws[1].hot_done})
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(TBE_EDEVICE);
-    if (hipMalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (big_alloc(&e->table, c.n_keys * sizeof(Slot), 0) != hipSuccess) return bail(TBE_ENOMEM);
     if (e->hot_cap) {
         for (auto &hs : e->hot) {
             if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
@@ -4375,9 +4402,9 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->qp.queue_limit = c.queue_limit;
         e->qp.order = c.queue_order;
         e->qp.cap = (uint32_t)std::max(1, c.queue_limit);
-        if (hipMalloc(&e->qhdr, ((c.n_keys + 1) & ~1ull) * sizeof(uint64_t)) != hipSuccess)   // even: k_fold_q loads header pairs
+        if (big_alloc(&e->qhdr, ((c.n_keys + 1) & ~1ull) * sizeof(uint64_t), 1) != hipSuccess)   // even: k_fold_q loads header pairs
             return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->ring, c.n_keys * (uint64_t)e->qp.cap * sizeof(uint64_t)) != hipSuccess)
+        if (big_alloc(&e->ring, c.n_keys * (uint64_t)e->qp.cap * sizeof(uint64_t), 2) != hipSuccess)
             return bail(TBE_ENOMEM);
         if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMemsetAsync(e->qhdr, 0, c.n_keys * sizeof(uint64_t), e->stream) != hipSuccess)
@@ -4390,12 +4417,12 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->ap.cap = (uint32_t)(std::max(1, c.queue_limit) + c.zero_wait_slots);
         e->ap.decay_rate = rate;
         e->ap.period_s = (double)c.replenishment_period_ticks / 10000000.0;
-        if (hipMalloc(&e->alocal, c.n_keys * sizeof(ALocal)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (big_alloc(&e->alocal, c.n_keys * sizeof(ALocal), 3) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMalloc(&e->aclient, c.n_keys * sizeof(AClient)) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMalloc(&e->gv, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMalloc(&e->gp, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
         if (hipMalloc(&e->gt, c.n_keys * sizeof(int64_t)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->ring, c.n_keys * (uint64_t)e->ap.cap * sizeof(uint64_t)) != hipSuccess)
+        if (big_alloc(&e->ring, c.n_keys * (uint64_t)e->ap.cap * sizeof(uint64_t), 2) != hipSuccess)
             return bail(TBE_ENOMEM);
         if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
         k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,

@@ -183,6 +183,16 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "contig": {
+        "hr_q": ([], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
+        "r_q": (["TBE_CONTIG_ALLOC=4"], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
+        "none_q": (["TBE_CONTIG_ALLOC=0"], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
+        "none_a": ([], ['--workload', 'approx', '--no-host-buffer', '--no-strdir']),
+        "al_a": (["TBE_CONTIG_ALLOC=14"], ['--workload', 'approx', '--no-host-buffer', '--no-strdir']),
+    },
+    "tick": {
+        "skip_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir"]),
+    },
     "hs": {
         "small_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "small_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
