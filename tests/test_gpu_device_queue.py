@@ -219,3 +219,52 @@ def test_wait_batch_tick_device(engine_lib, gpu, order, n_keys, qlimit, n, round
     assert np.array_equal(tt, tt2)
     m = tt2 != np.iinfo(np.int64).min
     assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+@pytest.mark.parametrize("order,qlimit", [(0, 16), (1, 4)])
+def test_back_to_back_tick_batches(engine_lib, gpu, order, qlimit):
+    """Fused-tick queue batches enqueued back to back with no host synchronisation (as
+    bench.py --workload queue) at a two-pass shape whose low-digit regions are a quarter
+    tile (200,000 keys, 2^18 requests).  Every batch's statuses, remaining counts and
+    drain log, the last batch's evictions, the queues and the bucket table against the C
+    restatement (Q:67-134, Q:237-271)."""
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    n_keys, n, nb = 200_000, 1 << 18, 6
+    rng = np.random.default_rng(order * 100 + qlimit)
+    eng = QueueingTokenBucketEngine(n_keys, 4, 1, 10_000_000, qlimit, order, device=0)
+    ref = cref.CQueueingTokenBucket(n_keys, 4, fill_rate(1, 10_000_000), qlimit, order)
+    cap = n_keys * min(max(qlimit, 1), 4)
+    t, host, ins, outs, logs = S_US, [], [], [], []
+    for b in range(nb):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 1, 1, 2, 3], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        t += 1_000 + (int(rng.integers(0, 3_000_000)) if b % 2 else 0)
+        host.append((keys, permits, ts, t))
+        ins.append((_dev(keys.view(np.int64), gpu), _dev(permits, gpu), _dev(ts, gpu)))
+        outs.append((torch.empty(n, dtype=torch.uint8, device=gpu), torch.empty(n, dtype=torch.int32, device=gpu)))
+        logs.append((torch.empty(cap, dtype=torch.int64, device=gpu), torch.empty(cap, dtype=torch.int64, device=gpu),
+                     torch.empty(cap, dtype=torch.int32, device=gpu), torch.empty(1, dtype=torch.int32, device=gpu)))
+    torch.cuda.synchronize()   # NULL stream: inputs complete at the call
+    for b in range(nb):
+        eng.wait_batch_tick_device(*ins[b], *outs[b], b * n, host[b][3], *logs[b])
+    eng.synchronize()
+    cause, ids = eng.evicted()
+    for b in range(nb):
+        keys, permits, ts, tick = host[b]
+        st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, b * n)
+        assert np.array_equal(outs[b][0].cpu().numpy(), st2), f"batch {b} statuses"
+        assert np.array_equal(outs[b][1].cpu().numpy(), rem2), f"batch {b} remaining"
+        k1, i1, r1 = _sorted_log(*logs[b])
+        k2, i2, r2 = ref.refresh(tick)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2), f"batch {b} log"
+    assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2)
+    assert (st2 == 2).mean() > 0.05 and sum(int(lg[3].item()) for lg in logs) > 0
+    for k in range(0, n_keys, 997):
+        assert eng.queue_of(k) == ref.queue_of(k)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))

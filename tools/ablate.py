@@ -218,6 +218,18 @@ VARIANT_SETS = {
         "never_z": (["TBE_HOT_SPARSE_MIN_LOG2=40"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
         "hm20_z": (["TBE_HOT_SPARSE_MIN_LOG2=20"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
     },
+    "r05b": {   # one-workgroup sampler vs many small ones; the queue kind pipelined or not
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "onewg_u": (["TBE_HOT_SAMPLE_ONE_WG=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "onewg_z": (["TBE_HOT_SAMPLE_ONE_WG=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
+    },
+    "r05q": {   # the queue kind pipelined (batch b+1's partition beside batch b's fold) or not
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
+    },
     "uniform": {
         "base_u": ([], ["--workload", "uniform"]),
         "hist2_u": (["TBE_HIST_AHEAD=2"], ["--workload", "uniform"]),

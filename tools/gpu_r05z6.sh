@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u tools/diag_b2b_queue2.py > gpurun_out/r05z6_diag.log 2>&1
+rc=$?; echo "diag rc=$rc"; grep -v amdgpu.ids gpurun_out/r05z6_diag.log | cut -c1-250; exit $rc
