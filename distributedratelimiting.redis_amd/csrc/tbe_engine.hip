@@ -999,12 +999,6 @@ __device__ __forceinline__ void fold_input(uint64_t rec, uint32_t q, const FoldF
 #ifndef TBE_SCATTER0_WAVES
 #define TBE_SCATTER0_WAVES 1
 #endif
-#ifndef TBE_HS_ALIAS
-#define TBE_HS_ALIAS 0
-#endif
-#ifndef TBE_FOLD_LDS_PAD
-#define TBE_FOLD_LDS_PAD 0                   // A/B: dynamic LDS per dense k_fold_wide workgroup (4096: two per CU)
-#endif
 template <bool FIRST, bool HOT = false, bool IDX = false, bool NOTS = false, bool LAST = false>
 __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_scatter_rec(
     const uint64_t *__restrict__ kin, const int32_t *__restrict__ pin, const int64_t *__restrict__ tin,
@@ -1024,14 +1018,7 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
     __shared__ uint16_t stage_e[LAST ? kTile : 1];   // LAST: each staged record's input element
-#if TBE_HS_ALIAS
-    // A/B: the hot table's LDS copy lives in `stage` (read only while the partition keys
-    // are formed, before the ranking first writes `stage`): 37 KB of LDS instead of 70 KB
-    static_assert(kHotLds <= kTile, "the hot table fits in the staging buffer");
-    uint64_t *hs = stage;
-#else
     __shared__ uint64_t hs[HOT ? kHotLds : 1];
-#endif
     static_assert(kPartItems * (kPartBlock / 64) * kDigits * 2 <= kTile * 8, "cnt fits in stage");
 
     const int tid = threadIdx.x;
@@ -1108,7 +1095,6 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
         }
     }
     tile_offsets<kPartBlock>(tile, tiles_per_blk, tileprefix, blockprefix, digit_total, goff, L.wsum);
-    if (TBE_HS_ALIAS && HOT) __syncthreads();   // every hot-table read is done before `stage` is written
     rank_tile_wb<kPartBlock, kPartItems>(key, shift, nvalid, L, reinterpret_cast<uint32_t *>(stage), lpos);
     int64_t tbase0 = 0, tbase1 = 0;
     if (LAST && tin) {   // (the approximate kind has no timestamps: its records all escape)
@@ -4133,7 +4119,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
                 e->cfg.n_keys, e->table, e->params, w.res[0], w.err, 0u, tb_wmin, G, rec0, walk);
         }
     } else if (e->packed) {   // a dense batch: k_fold_wide takes every bucket
-        k_fold_wide<true><<<fold_grid, kWideBlock, TBE_FOLD_LDS_PAD, sf>>>(
+        k_fold_wide<true><<<fold_grid, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
             e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0);
     } else {
@@ -4251,7 +4237,7 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
 // config D from 4.17 to 3.93 ms per step (profiles/r05yab_ablate_contig.log), but with them
 // the queue and approximate kinds -- the two that have rings -- gave intermittently wrong
 // replies in engines created after other engines were freed (one key's requests out of
-// arrival order, replies no fold wrote; CHANGELOG round 5, second session), which ordinary
+// arrival order, replies no fold can produce; CHANGELOG round 5, second session), which ordinary
 // allocations never did in five rounds of the same tests.
 #ifndef TBE_CONTIG_ALLOC
 #define TBE_CONTIG_ALLOC 0

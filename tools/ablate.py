@@ -226,14 +226,6 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
     },
-    "r05s": {   # the fold at two workgroups per CU (LDS pad) so partition workgroups fit beside it
-        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "pad_u": (["TBE_FOLD_LDS_PAD=4096"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "padal_u": (["TBE_FOLD_LDS_PAD=4096", "TBE_HS_ALIAS=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "al_u": (["TBE_HS_ALIAS=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "padal_z": (["TBE_FOLD_LDS_PAD=4096", "TBE_HS_ALIAS=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-    },
     "r05q": {   # the queue kind pipelined (batch b+1's partition beside batch b's fold) or not
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
