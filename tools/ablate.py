@@ -226,6 +226,10 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
     },
+    "r05c": {   # rings physically contiguous (the session-one default) or ordinary (diagnostic builds)
+        "plain_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "contig_q": (["TBE_CONTIG_ALLOC=4"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+    },
     "r05q": {   # the queue kind pipelined (batch b+1's partition beside batch b's fold) or not
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
