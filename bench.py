@@ -591,8 +591,9 @@ def bench_batch_sweep(args, lib, n_keys: int, dev, sizes=SWEEP_LOG2):
     latency (enqueue one batch + synchronise, wall clock, median of 5), both on an engine
     without stage events, and the HIP-event stage times of the same batches on a second
     engine that records them (at small sizes the ~14 events per batch are themselves a
-    visible share of its time).  Sparse batches (below R/32 requests per bucket on average: up to 2^21 here) send
-    their sparse buckets to k_fold_sparse, one wave each; from 2^22 every bucket takes
+    visible share of its time).  Sparse batches (below R/8 requests per bucket on average,
+    R = 2048 keys per bucket: up to 2^23 here) send their sparse buckets to k_fold_sparse,
+    one wave each, and take hot-key runs only from 2^20; at 2^24 and 2^26 every bucket takes
     k_fold_wide."""
     from distributedratelimiting.redis_amd import TokenBucketEngine
     out = []

@@ -1412,7 +1412,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         // barrier before this workgroup's write-back.  384 blocks = half of the 768
         // workgroups in flight: config B fold 0.93 -> 0.85 ms; 768 -> 0.90, 1536 -> 0.93
         // (profiles/r04d_ablate_perm0_prefetch.log)
-        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN && !dlist) {
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
             const uint32_t fblk = blockIdx.x + TBE_FOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
@@ -3210,7 +3210,7 @@ __global__ __launch_bounds__(kFoldBlock, TBE_A_WAVES) void k_fold_a(
 #if TBE_AFOLD_PREFETCH
         // as k_fold_wide: touch the local-tier slice and records of the workgroup
         // TBE_AFOLD_PREFETCH blocks later (same XCD); waited for at the write-back barrier
-        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN && !dlist) {
+        if (c == s && e - s >= TBE_FOLD_PREFETCH_MIN) {
             const uint32_t fblk = blockIdx.x + TBE_AFOLD_PREFETCH;
             const uint32_t fb = fold_bucket_at(G, fblk);
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
@@ -3541,7 +3541,9 @@ struct Workspace {
     uint32_t *bstart = nullptr;
     uint32_t *bcount = nullptr;   // requests per bucket of the batch
     uint32_t *dlist = nullptr;    // sparse batches: count + ids of the dense buckets (k_bscan)
-    unsigned long long *bsflags = nullptr;   // k_bscan_lb's published totals (tagged per batch)
+    unsigned long long *bsflags = nullptr;   // k_bscan_lb's published totals (tagged per launch)
+    uint32_t bs_tag = 0;          // tag of bsflags' last k_bscan_lb launch (0: the zeroed state)
+    bool bs_fresh = false;        // bsflags just allocated: zeroed on the batch's stream first
     uint8_t *dig0 = nullptr;      // each request's pass-0 digit (k_unrank re-ranks from it)
     uint8_t *dig1 = nullptr;      // pass 1's digit of pass 0's output, in that order (k_hist_dig)
     int64_t *ts0 = nullptr;       // narrow pass-0 records: escaped requests' times at their pass-0 position
@@ -3778,9 +3780,11 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     HIP_TRY(e, hipMalloc(&w.bcount, ((uint64_t)e->nb_total + 2 + e->nbuckets) * sizeof(uint32_t)));
     w.err = w.bcount + e->nb_total;
     w.dlist = w.bcount + e->nb_total + 1;
+    // k_bscan_lb's flags are zeroed on the stream of the first batch that uses them
+    // (run_batch), not with a device-wide synchronisation here
     HIP_TRY(e, hipMalloc(&w.bsflags, kBsMaxBlocks * sizeof(unsigned long long)));
-    HIP_TRY(e, hipMemset(w.bsflags, 0, kBsMaxBlocks * sizeof(unsigned long long)));
-    HIP_TRY(e, hipDeviceSynchronize());   // (allocation time only) zeroed before any stream reads it
+    w.bs_fresh = true;
+    w.bs_tag = 0;
     if (e->unrank) HIP_TRY(e, hipMalloc(&w.dig0, cap));
     if (e->dig1) HIP_TRY(e, hipMalloc(&w.dig1, cap));
     if (e->n0) HIP_TRY(e, hipMalloc(&w.ts0, cap * sizeof(int64_t)));
@@ -3907,6 +3911,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         HIP_TRY(e, hipStreamWaitEvent(sf, in_ready, 0));
     }
     HIP_TRY(e, hipMemsetAsync(w.bcount, 0, ((uint64_t)e->nb_total + 2) * sizeof(uint32_t), sp));   // + err, dlist[0]
+    if (w.bs_fresh) {
+        HIP_TRY(e, hipMemsetAsync(w.bsflags, 0, kBsMaxBlocks * sizeof(unsigned long long), sp));
+        w.bs_fresh = false;
+    }
 
     const uint64_t kmask = e->packed ? e->pf.kmask : ~0ull;
     const FoldFmt G = batch_fold_fmt(e, n);
@@ -4050,10 +4058,16 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
     const PassBufs &sorted = w.pass[e->passes - 1];
     stage_begin(e, ST_BOUNDS, sp);
     const uint32_t bs_blocks = (e->nb_total + kBsTile - 1) / kBsTile;
-    if (TBE_BSCAN_LB && bs_blocks <= kBsMaxBlocks)
-        k_bscan_lb<<<bs_blocks, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, w.bsflags,
-                                               (uint32_t)(e->nbatch + 1), e->nbuckets, tb_wmin,
-                                               sparse_tb ? w.dlist : nullptr);
+    if (TBE_BSCAN_LB && bs_blocks <= kBsMaxBlocks) {
+        // a fresh tag per launch on these flags, taken here: a batch that
+        // failed between its launch and the end of run_batch cannot hand its tag on
+        if (++w.bs_tag == 0) {   // 2^32 launches: back to the zeroed state
+            HIP_TRY(e, hipMemsetAsync(w.bsflags, 0, kBsMaxBlocks * sizeof(unsigned long long), sp));
+            w.bs_tag = 1;
+        }
+        k_bscan_lb<<<bs_blocks, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, w.bsflags, w.bs_tag,
+                                               e->nbuckets, tb_wmin, sparse_tb ? w.dlist : nullptr);
+    }
     else if (sparse_tb)
         k_bscan<<<1, 1024, 0, sp>>>(w.bcount, e->nb_total, w.bstart, e->nbuckets, tb_wmin, w.dlist);
     else
@@ -4231,24 +4245,13 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
 }  // namespace
 
 // ============================================================================= C ABI
-// Resident state allocated physically contiguous where the driver can give it (else an
-// ordinary allocation): TBE_CONTIG_ALLOC bit 0 the bucket table, 1 the queue headers, 2 the
-// rings, 3 the approximate local tier.  A/B only, off by default: contiguous rings took
-// config D from 4.17 to 3.93 ms per step (profiles/r05yab_ablate_contig.log), but with them
-// the queue and approximate kinds -- the two that have rings -- gave intermittently wrong
-// replies in engines created after other engines were freed (one key's requests out of
-// arrival order, replies no fold can produce; CHANGELOG round 5, second session), which ordinary
-// allocations never did in five rounds of the same tests.
-#ifndef TBE_CONTIG_ALLOC
-#define TBE_CONTIG_ALLOC 0
-#endif
+// Resident state is allocated with plain hipMalloc.  (Round 5 allocated the rings with
+// hipExtMallocWithFlags(..., hipDeviceMallocContiguous) for 0.24 ms of config D, and queue
+// and approximate engines created after another engine had been freed then gave wrong
+// replies on some boxes; that flag is not among those hip_runtime_api.h documents for
+// hipExtMallocWithFlags, and the engine no longer uses it.  CHANGELOG round 6.)
 template <typename T>
-hipError_t big_alloc(T **p, size_t bytes, int what) {
-    if ((TBE_CONTIG_ALLOC >> what) & 1) {
-        if (hipExtMallocWithFlags(reinterpret_cast<void **>(p), bytes, hipDeviceMallocContiguous) == hipSuccess)
-            return hipSuccess;
-        (void)hipGetLastError();
-    }
+hipError_t dalloc(T **p, size_t bytes) {
     return hipMalloc(reinterpret_cast<void **>(p), bytes);
 }
 
@@ -4388,29 +4391,24 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     for (hipEvent_t *ev : {&e->ev_in, &e->ev_part, &e->ev_out, &e->ev_hot, &e->ws[0].done, &e->ws[1].done,
                            &e->ws[0].hot_done, &e->ws[1].hot_done})
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return bail(TBE_EDEVICE);
-    if (big_alloc(&e->table, c.n_keys * sizeof(Slot), 0) != hipSuccess) return bail(TBE_ENOMEM);
-    if (e->hot_cap) {
-        for (auto &hs : e->hot) {
-            if (hipMalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
-            if (hipMemsetAsync(hs, 0, sizeof(HotSet), e->stream) != hipSuccess) return bail(TBE_EDEVICE);
-        }
-    }
-    if (hipMalloc(&e->sticky, sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
-    if (hipMemsetAsync(e->sticky, 0, sizeof(uint32_t), e->stream) != hipSuccess)
-        return bail(TBE_EDEVICE);
-    k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
+    // Every resident buffer is allocated before any initialisation is enqueued, and every
+    // one is then initialised on e->stream -- the rings and the headers' pad entry too, though
+    // no decision reads a ring entry the engine did not write -- so a new engine never sees
+    // bytes an earlier allocation left (tests/test_gpu_recreate.py).
+    const uint64_t qhdr_n = (c.n_keys + 1) & ~1ull;   // even: k_fold_q loads header pairs
+    uint64_t ring_n = 0;
+    if (dalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (e->hot_cap)
+        for (auto &hs : e->hot)
+            if (dalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
+    if (dalloc(&e->sticky, sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     if (c.kind == TBE_KIND_QUEUEING) {
         e->qp.token_limit = c.token_limit;
         e->qp.queue_limit = c.queue_limit;
         e->qp.order = c.queue_order;
         e->qp.cap = (uint32_t)std::max(1, c.queue_limit);
-        if (big_alloc(&e->qhdr, ((c.n_keys + 1) & ~1ull) * sizeof(uint64_t), 1) != hipSuccess)   // even: k_fold_q loads header pairs
-            return bail(TBE_ENOMEM);
-        if (big_alloc(&e->ring, c.n_keys * (uint64_t)e->qp.cap * sizeof(uint64_t), 2) != hipSuccess)
-            return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMemsetAsync(e->qhdr, 0, c.n_keys * sizeof(uint64_t), e->stream) != hipSuccess)
-            return bail(TBE_EDEVICE);
+        ring_n = c.n_keys * (uint64_t)e->qp.cap;
+        if (dalloc(&e->qhdr, qhdr_n * sizeof(uint64_t)) != hipSuccess) return bail(TBE_ENOMEM);
     } else if (c.kind == TBE_KIND_APPROXIMATE) {
         e->ap.token_limit = c.token_limit;
         e->ap.queue_limit = c.queue_limit;
@@ -4419,19 +4417,40 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->ap.cap = (uint32_t)(std::max(1, c.queue_limit) + c.zero_wait_slots);
         e->ap.decay_rate = rate;
         e->ap.period_s = (double)c.replenishment_period_ticks / 10000000.0;
-        if (big_alloc(&e->alocal, c.n_keys * sizeof(ALocal), 3) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->aclient, c.n_keys * sizeof(AClient)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->gv, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->gp, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->gt, c.n_keys * sizeof(int64_t)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (big_alloc(&e->ring, c.n_keys * (uint64_t)e->ap.cap * sizeof(uint64_t), 2) != hipSuccess)
-            return bail(TBE_ENOMEM);
-        if (hipMalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
-        k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,
-                                                   c.token_limit);
+        ring_n = c.n_keys * (uint64_t)e->ap.cap;
+        if (dalloc(&e->alocal, c.n_keys * sizeof(ALocal)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (dalloc(&e->aclient, c.n_keys * sizeof(AClient)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (dalloc(&e->gv, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (dalloc(&e->gp, c.n_keys * sizeof(double)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (dalloc(&e->gt, c.n_keys * sizeof(int64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+    }
+    if (ring_n) {
+        if (dalloc(&e->ring, ring_n * sizeof(uint64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        if (dalloc(&e->counters, 2 * sizeof(uint32_t)) != hipSuccess) return bail(TBE_ENOMEM);
     }
     for (int i = 0; i < (e->pipeline ? 2 : 1); ++i)
         if (c.max_batch && ensure_workspace(e, e->ws[i], c.max_batch) != TBE_OK) return bail(TBE_ENOMEM);
+    // initialisation, in order on the engine's stream
+    hipError_t ie = hipSuccess;
+    auto zero = [&](void *p, size_t bytes) {
+        if (p && ie == hipSuccess) ie = hipMemsetAsync(p, 0, bytes, e->stream);
+    };
+    for (auto &hs : e->hot) zero(hs, sizeof(HotSet));
+    zero(e->sticky, sizeof(uint32_t));
+    zero(e->qhdr, qhdr_n * sizeof(uint64_t));
+    zero(e->ring, ring_n * sizeof(uint64_t));
+    zero(e->counters, 2 * sizeof(uint32_t));
+    for (auto &w : e->ws)
+        if (w.bsflags && w.bs_fresh) {
+            zero(w.bsflags, kBsMaxBlocks * sizeof(unsigned long long));
+            w.bs_fresh = false;
+        }
+    if (ie != hipSuccess) return bail(TBE_EDEVICE);
+    k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
+    if (c.kind == TBE_KIND_APPROXIMATE)
+        k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,
+                                                   c.token_limit);
+    if (hipGetLastError() != hipSuccess) return bail(TBE_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(TBE_EDEVICE);
     *out_engine = e;
     return TBE_OK;

@@ -380,8 +380,10 @@ tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bi
  * reply-position bits (ceil_log2 n), out[3] their time-offset bits, out[4] the pass-0
  * record's key bits, out[5] permit-code bits, out[6] pass-0 time-offset bits, out[7]
  * r_bits, and when n_out > 8, out[8] 1 if the batch is a sparse token-bucket batch
- * (fewer than 64 requests per bucket on average: one wave per sparse bucket, the dense
- * buckets listed for the wide fold, no hot-key runs).  n_out must be >= 8.  A request
+ * (fewer than R >> TBE_SPARSE_GATE_SHIFT = R/8 requests per bucket on average, R = 2^r_bits
+ * keys per bucket: one wave per sparse bucket, the dense buckets listed for the wide
+ * fold; hot-key runs only from 2^TBE_HOT_SPARSE_MIN_LOG2 = 2^20 requests, a smaller
+ * sparse batch leaves the hot sets as they are).  n_out must be >= 8.  A request
  * whose time offset does not fit takes the escape form (its time is read from the
  * previous record / the caller's array). */
 tbe_status tbe_batch_format(const tbe_engine *engine, uint64_t n, uint32_t *out, uint32_t n_out);

@@ -53,6 +53,31 @@ def test_sparse_uniform_batches(engine_lib, gpu, logn):
     eng.close()
 
 
+def test_small_sparse_batches_between_hot_batches(engine_lib, gpu):
+    """sparse batches below 2^20 requests take no hot-key runs and leave the hot
+    sets as they are (their busiest key fills one dense bucket, which k_fold_wide decides
+    chunk by chunk); placed between dense 2^24 Zipf batches whose hot sets rotate, every
+    reply and the table against the C restatement."""
+    from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
+    n_keys = 100_000_000
+    big = 1 << 24
+    eng = TokenBucketEngine(n_keys, 10, 1, 10_000_000, device=0, max_batch=big)
+    assert eng.layout()["hot"]
+    for m in (1 << 18, 1 << 19):
+        assert eng.batch_format(m)["sparse"]
+    ref = cref.CTokenBucket(n_keys, 10, fill_rate(1, 10_000_000))
+    rng = np.random.default_rng(23)
+    perm = rng.permutation(1 << 20).astype(np.uint64) * 95 + 17   # Zipf ranks -> keys
+    for b, m in enumerate([big, 1 << 19, 1 << 18, big, 1 << 19, big, big, 1 << 18]):
+        ranks = np.minimum(rng.zipf(1.1, m), 1 << 20) - 1
+        keys = perm[ranks]
+        permits = rng.integers(0, 4, m).astype(np.int32)
+        ts = (T0 + b * 2_000_000 + np.sort(rng.integers(0, 1_000_000, m))).astype(np.int64)
+        _run(eng, ref, keys, permits, ts, (b, m))
+    _check_table(eng, ref)
+    eng.close()
+
+
 def test_sparse_skewed_chunks_and_dense(engine_lib, gpu):
     """2^20 requests: 3% on 200 buckets (~157 requests each over 2048 rows: three chunks of
     64, keys repeated across them), 2% on 8 keys of one bucket (a dense bucket in a sparse
@@ -101,10 +126,10 @@ def test_sparse_unpacked_records(engine_lib, gpu):
 
 
 def test_sparse_zipf_batches(engine_lib, gpu):
-    """Zipf(1.1) batches of 2^20 requests over 1e8 keys: sparse batches (no hot-key runs),
-    whose busiest key (~11% of a batch: ~115k requests) fills one dense bucket that
-    k_fold_wide decides in ~75 chunks; between them dense 2^24 Zipf batches with hot runs,
-    whose hot sets the sparse batches leave alone."""
+    """Zipf(1.1) batches of 2^20 requests over 1e8 keys: sparse batches (fewer than R/8
+    requests per bucket) that still run hot keys apart (hot runs are on from 2^20,
+    TBE_HOT_SPARSE_MIN_LOG2: the busiest key, ~11% of a batch, ~115k requests, gets its own
+    run), between dense 2^24 Zipf batches with hot runs."""
     from distributedratelimiting.redis_amd import TokenBucketEngine, fill_rate
     n_keys = 100_000_000
     big, n = 1 << 24, 1 << 20

@@ -183,13 +183,6 @@ VARIANT_SETS = {
         "r1only_u": (["TBE_FOLD_R1_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_pf0_u": (["TBE_FOLD_COPY_ONLY", "TBE_FOLD_PREFETCH=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
-    "contig": {
-        "hr_q": ([], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
-        "r_q": (["TBE_CONTIG_ALLOC=4"], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
-        "none_q": (["TBE_CONTIG_ALLOC=0"], ['--workload', 'queue', '--no-host-buffer', '--no-strdir', '--no-drain-variant']),
-        "none_a": ([], ['--workload', 'approx', '--no-host-buffer', '--no-strdir']),
-        "al_a": (["TBE_CONTIG_ALLOC=14"], ['--workload', 'approx', '--no-host-buffer', '--no-strdir']),
-    },
     "tick": {
         "skip_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir"]),
     },
@@ -225,10 +218,6 @@ VARIANT_SETS = {
         "onewg_z": (["TBE_HOT_SAMPLE_ONE_WG=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
-    },
-    "r05c": {   # rings physically contiguous (the session-one default) or ordinary (diagnostic builds)
-        "plain_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
-        "contig_q": (["TBE_CONTIG_ALLOC=4"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
     },
     "r05q": {   # the queue kind pipelined (batch b+1's partition beside batch b's fold) or not
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
