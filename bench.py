@@ -88,6 +88,9 @@ def parse():
                          "fused into the batch's fold (A/B)")
     ap.add_argument("--no-drain-variant", action="store_true",
                     help="config D: skip the second schedule whose ticks grant (draining block)")
+    ap.add_argument("--drain-marked", action="store_true",
+                    help="config D: put the PMC window markers around the draining schedule's timed "
+                         "batches instead of the headline's (tools/pmc_passes.sh, run queue_draining)")
     ap.add_argument("--tokens-per-period", type=int, default=1)
     ap.add_argument("--period-ticks", type=int, default=None,
                     help="ReplenishmentPeriod in 100 ns ticks (default 1 s; approx: one batch interval)")
@@ -414,21 +417,24 @@ def main():
         u_meas, w_meas = int(round(u_mean)), int(round(w_mean))
         eng = ser
 
-    # ---- roofline of the dominant kernel (per launch, HIP events on the engine stream)
+    # ---- roofline: the decision kernel -- the fold,
+    # which reads and writes the table -- is the dominant kernel, and its `achieved` is the
+    # step's algorithmic bytes B_alg (25 B per request + 16 B per distinct key read + 16 B
+    # per key written) over the fold's average launch time.  The fold's own byte count
+    # (records, replies and rows) is kept beside it as kernel_own_*; the stage with the most
+    # device time is named too.
     roofline = None
-    if stages and sum(stages.values()) > 0:
+    if stages and stages.get("fold", 0) > 0:
         passes = layout["passes"]
         launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
                     "unscatter": passes - (1 if layout.get("fold_records") else 0), "hot": 5}   # per step
-        name = max(stages, key=stages.get)
+        name = "fold"
+        largest = max(stages, key=stages.get)
         per_launch_ms = stages[name] / (args.steps * launches[name])
-        # the dominant kernel's own algorithmic bytes per launch: the fold
-        # reads its sorted records and the rows of the batch's U distinct keys, writes a
-        # reply per request and the rows of the W keys it modified (U, W measured on the
-        # last timed batch)
         own_bytes = algorithmic_bytes(name, n, keys_local, passes, layout["packed"], u_meas,
                                       1 if layout.get("narrow") else 4, w_meas)
-        achieved = own_bytes / (per_launch_ms * 1e-3) / 1e9
+        achieved = step_alg / (per_launch_ms * 1e-3) / 1e9
+        own_achieved = own_bytes / (per_launch_ms * 1e-3) / 1e9
         step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
         fp = run_fingerprint(args, world, keys_local, layout)
         w_pmc, pmc_why = pmc_workload(args.workload, fp)
@@ -440,12 +446,17 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (round(pmc / launches[name], 1) if pmc is not None else None),
                     **({"traffic_null_reason": pmc_why} if pmc is None else {}),
-                    "alg_bytes_per_launch": own_bytes,
-                    "alg_bytes_note": algorithmic_note(name, layout, u_meas, w_meas),
+                    "alg_bytes_per_launch": step_alg,
+                    "alg_bytes_note": ("SURVEY.md §8(d) B_alg of the batch one fold launch decides: 25 B per "
+                                       "request + 16 B per distinct key read + 16 B per distinct key written; "
+                                       + uw_note),
+                    "kernel_own_bytes": own_bytes,
+                    "kernel_own_note": algorithmic_note(name, layout, u_meas, w_meas),
+                    "kernel_own_frac": round(own_achieved / HBM_PEAK_GBS, 4),
+                    "largest_stage": largest,
+                    "largest_stage_ms_per_step": round(stages[largest] / args.steps, 4),
                     "distinct_keys_U": u_meas, "written_keys_W": w_meas,
                     "step_alg_bytes": step_alg,
-                    "step_alg_note": "SURVEY.md §8(d) B_alg: 25 B per request + 16 B per distinct key read "
-                                     "+ 16 B per distinct key written; " + uw_note,
                     "step_achieved": round(step_achieved, 1),
                     "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
                     "step_traffic": step_pmc,

@@ -130,38 +130,40 @@ PMC_KERNELS = {
 }
 
 
-def _roofline(name, alg_bytes, ms, note, workload, fp):
-    if not ms > 0:    # --no-stage-timing: no kernel times
+def _roofline(fold_ms, step_alg, step_note, own_alg, own_note, workload, fp, ms_per_step, stages, steps,
+              pmc_key=None):
+    """SURVEY.md §8(d) roofline of one bench line: the decision kernel
+    (the fold) is the dominant kernel; `achieved` = the step's algorithmic bytes B_alg over
+    the fold's average launch time, `frac` = achieved / 8 TB/s.  The fold's own byte count
+    is kept as kernel_own_*; step_* relate B_alg to the whole timed step; `traffic` and
+    `step_traffic` are the PMC bytes (tools/pmc_summary.py) of a run with exactly this
+    fingerprint, else null with the reason."""
+    if not fold_ms > 0:    # --no-stage-timing: no kernel times
         return None
-    achieved = alg_bytes / (ms * 1e-3) / 1e9
-    w, why = pmc_workload(workload, fp)
-    traffic = _pmc_traffic(w, PMC_KERNELS[(workload, name)]) if (workload, name) in PMC_KERNELS else None
+    achieved = step_alg / (fold_ms * 1e-3) / 1e9
+    step_achieved = step_alg / (ms_per_step * 1e-3) / 1e9
+    key = pmc_key or workload
+    w, why = pmc_workload(key, fp)
+    traffic = _pmc_traffic(w, PMC_KERNELS[(workload, "fold")]) if (workload, "fold") in PMC_KERNELS else None
     if w is not None and traffic is None:
-        why = f"no PMC bytes for the {name} kernels"
-    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+        why = "no PMC bytes for the fold kernels"
+    st = w.get("step_hbm_bytes") if w is not None else None
+    largest = max(stages, key=stages.get) if stages else None
+    return {"bound": "hbm", "kernel": "fold", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             **({"traffic_null_reason": why} if traffic is None else {}),
-            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4),
-            "alg_bytes_note": note,
-            "timing": "HIP events on the engine's launch stream over the timed region",
+            "alg_bytes_per_launch": int(step_alg), "alg_bytes_note": "SURVEY.md §8(d) B_alg of the step: " + step_note,
+            "avg_launch_ms": round(fold_ms, 4),
+            "kernel_own_bytes": int(own_alg), "kernel_own_note": own_note,
+            "kernel_own_frac": round(own_alg / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            **({"largest_stage": largest, "largest_stage_ms_per_step": round(stages[largest] / steps, 4)}
+               if largest else {}),
+            "step_alg_bytes": int(step_alg), "step_achieved": round(step_achieved, 1),
+            "step_frac": round(step_achieved / HBM_PEAK_GBS, 4),
+            "step_traffic": round(st, 1) if st is not None else None,
+            **({"step_traffic_null_reason": why or "no step bytes in the PMC summary"} if st is None else {}),
+            "timing": "HIP events around the fold on the engine's launch stream over the timed region",
             "fingerprint": fp}
-
-
-def _step_roofline(line, alg, note, workload, fp):
-    """Whole-step figures beside the dominant kernel's: §8(d)'s algorithmic bytes over the
-    timed ms_per_step, and the PMC bytes of one step (tools/pmc_summary.py), if committed
-    for a run of exactly this configuration."""
-    r = line.get("roofline")
-    if r is None:
-        return
-    achieved = alg / (line["ms_per_step"] * 1e-3) / 1e9
-    r.update({"step_alg_bytes": int(alg), "step_alg_note": note, "step_achieved": round(achieved, 1),
-              "step_frac": round(achieved / HBM_PEAK_GBS, 4)})
-    w, why = pmc_workload(workload, fp)
-    st = w.get("step_hbm_bytes") if w is not None else None
-    r["step_traffic"] = round(st, 1) if st is not None else None
-    if st is None:
-        r["step_traffic_null_reason"] = why or "no step bytes in the PMC summary"
 
 
 def run(args, lib, dev, world, rank, dist):
@@ -330,43 +332,28 @@ def run_queue(args, lib, dev, world, rank, dist):
     n, steps = args.batch, args.steps
     seed = SEED_D + 7919 * rank
     fused = not args.no_fuse_tick
-    r = _queue_pass(args, lib, dev, world, dist, kl, args.period_ticks, seed, marked=True)
+    # the PMC markers go around the headline schedule's timed batches, or with --drain-marked
+    # around the draining schedule's (tools/pmc_passes.sh's "queue_draining" run)
+    r = _queue_pass(args, lib, dev, world, dist, kl, args.period_ticks, seed, marked=not args.drain_marked)
     elapsed, stages, granted, q_last, d_last = r["elapsed"], r["stages"], r["granted"], r["q_last"], r["d_last"]
     fp = run_fingerprint(args, world, kl, r["layout"])
-    if rank == 0:
+    if rank == 0 and not args.drain_marked:
         write_fingerprint(fp)
 
     value = n * steps * world / elapsed
-    passes = r["layout"]["passes"]
-    launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                "unscatter": passes, "hot": 1, "drain": 1}
-    name = max(stages, key=stages.get)
-    ms = stages[name] / (steps * launches[name])
-    if name == "fold" and r["fold_timed"] > 0:   # the timed engine's own fold events
-        ms = r["fold_timed"] / steps
     u = _distinct(n, kl)
     packed = bool(r["layout"].get("packed"))
-    if name == "fold":
-        # records (packed: u64 record 8 + arrival index 4; wide: key 4, permits 4, ts 8,
-        # index 4) + packed reply 4 per request; per distinct key: bucket row 16 + queue
-        # header 8, read and written; 8 per enqueue
-        rec = 12 if packed else 20
-        alg = n * (rec + 4) + u * 48 + q_last * 8
-        note = f"n*{rec + 4} + distinct*48 + enqueued*8 (last batch's enqueues)"
-    elif name == "drain":
-        # every key's queue header 8; per grant: ring entry 8 + log record 20 (lower bound)
-        alg = kl * 8 + d_last * 28
-        note = "n_keys*8 + grants*28 (lower bound: rows of keys with queues not counted)"
-    elif name == "scatter":
-        # per pass: read the caller's key 8 + permits 4 + ts 8 (pass 0) or one record (packed
-        # 8 + index 4, wide 20); write the record and perm 4 (averaged over the two passes)
-        if packed:
-            alg, note = n * 32, "n*32 (packed records + index, per pass: (36 + 28) / 2)"
-        else:
-            alg, note = n * 44, "n*44 (wide records, per pass)"
-    else:
-        alg = n * 20
-        note = "n*20"
+    # the fold's own bytes: records (packed: u64 record 8 + arrival index 4; wide: key 4,
+    # permits 4, ts 8, index 4) + packed reply 4 per request; per distinct key: bucket row
+    # 16 + queue header 8, read and written; 8 per enqueue
+    rec = 12 if packed else 20
+    own = n * (rec + 4) + u * 48 + q_last * 8
+    own_note = f"fold: n*{rec + 4} + distinct*48 + enqueued*8 (last batch's enqueues)"
+    # the B formula (W ~ distinct keys x grant share) + 8 B per
+    # enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
+    step_alg = n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8
+    step_note = "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)"
+    fold_ms = (r["fold_timed"] if r["fold_timed"] > 0 else stages.get("fold", 0.0)) / steps
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -383,21 +370,28 @@ def run_queue(args, lib, dev, world, rank, dist):
         "last_batch": {"granted_frac": round(granted, 4), "queued": q_last, "tick_grants": d_last},
         "tick_grants_per_step": r["tick_grants_per_step"],
         "stage_ms_per_step": {k: round(v / steps, 4) for k, v in stages.items()},
-        "roofline": _roofline(name, alg, ms, note, "queue", fp),
+        "roofline": _roofline(fold_ms, step_alg, step_note, own, own_note, "queue", fp,
+                              elapsed / steps * 1e3, stages, steps),
         "cpu_baseline": None,
     }
-    # SURVEY.md §8(d) config D, whole step: the B formula (W ~ distinct keys x grant share)
-    # + 8 B per enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
-    _step_roofline(line, n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8,
-                   "25*N + 16*U + 16*U*granted_frac + 8*enqueued + 8*dequeued (last batch)", "queue", fp)
     if not args.no_drain_variant:
         # The same schedule with ticks that grant: at 1 token/s a saturated key frees one
         # queue entry per ~1000 ticks, so config D's ticks drain nothing within a run.  With
         # ReplenishmentPeriod = 2 batch intervals every queued key gains half a token per
         # tick, and the FIFO drain (Q:237-271) completes millions of entries per tick.
         pt = 2 * args.interval_us * 10
-        d = _queue_pass(args, lib, dev, world, dist, kl, pt, seed)
+        d = _queue_pass(args, lib, dev, world, dist, kl, pt, seed, marked=args.drain_marked)
         g = np.array(d["tick_grants_per_step"], dtype=np.float64)
+        # the draining schedule's roofline, by the same rule (its PMC bytes come from
+        # tools/pmc_passes.sh's "queue_draining" run: --drain-marked puts the markers here)
+        dfp = run_fingerprint(args, world, kl, d["layout"])
+        dfp["period_ticks"] = pt
+        dfp["schedule"] = "draining"
+        if rank == 0 and args.drain_marked:
+            write_fingerprint(dfp)
+        d_step = n * 25 + u * 16 + u * d["granted"] * 16 + d["q_last"] * 8 + d["d_last"] * 8
+        d_own = n * (rec + 4) + u * 48 + d["q_last"] * 8 + d["d_last"] * 28
+        d_fold = (d["fold_timed"] if d["fold_timed"] > 0 else d["stages"].get("fold", 0.0)) / steps
         line["draining"] = {
             "period_ticks": pt, "tokens_per_period": args.tokens_per_period,
             "value": round(n * steps * world / d["elapsed"], 1),
@@ -406,6 +400,9 @@ def run_queue(args, lib, dev, world, rank, dist):
             "tick_grants_mean": round(float(g.mean()), 1) if g.size else 0.0,
             "granted_frac_last_batch": round(d["granted"], 4), "queued_last_batch": d["q_last"],
             "stage_ms_per_step": {k: round(v / steps, 4) for k, v in d["stages"].items()},
+            "roofline": _roofline(d_fold, d_step, step_note, d_own, own_note + " + dequeued*28 (ring entry + log)",
+                                  "queue", dfp, d["elapsed"] / steps * 1e3, d["stages"], steps,
+                                  pmc_key="queue_draining"),
             "note": "config D's schedule with ReplenishmentPeriod = 2 batch intervals: the fused ticks "
                     "drain queued entries every step (tick_grants = entries completed by each timed tick)"}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -551,24 +548,11 @@ def run_approx(args, lib, dev, world, rank, dist):
     fp = run_fingerprint(args, world, kshared, layout)
     if rank == 0:
         write_fingerprint(fp)
-    passes = layout["passes"]
-    launches = {"hist": passes, "colscan": passes, "scatter": passes, "bounds": 1, "fold": 1,
-                "unscatter": passes, "hot": 1}
-    name = max(stages, key=stages.get)
-    ms = stages[name] / (steps * launches[name])
-    if name == "fold" and fold_timed > 0:   # the timed engine's own fold events
-        ms = fold_timed / steps
     u = _distinct(n, kshared)
-    if name == "fold":
-        # records (key 4, permits 4, arrival index 4) + reply 4 per request; local-tier row
-        # 16 B read + written per distinct key
-        alg, note = n * 16 + u * 32, "n*16 + distinct*32"
-    elif name == "scatter":
-        # per pass: read key 8 + permits 4 (pass 0) or a record {key 4, permits 4, index 4};
-        # write the record and perm 4
-        alg, note = n * 28, "n*28 (wide records without ts, per pass)"
-    else:
-        alg, note = n * 16, "n*16"
+    # the fold's own bytes: records (key 4, permits 4, arrival index 4) + reply 4 per
+    # request; local-tier row 16 B read + written per distinct key
+    own, own_note = n * 16 + u * 32, "fold: n*16 + distinct*32"
+    fold_ms = (fold_timed if fold_timed > 0 else stages.get("fold", 0.0)) / steps
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
         "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -592,13 +576,13 @@ def run_approx(args, lib, dev, world, rank, dist):
                               "timed": "in the timed steps" if m == args.approx_mode else
                                        f"{min(steps, 5)} epochs after the timed region"}
                           for m in ("node", "clients")},
-        "roofline": _roofline(name, alg, ms, note, "approx", fp),
+        # 8+4+1 in/out + 8 local-tier state per decision,
+        # K_shared * (4 count + 24 v,p,t) per refresh
+        "roofline": _roofline(fold_ms, n * 21 + kshared * 28, "21*N + 28*K_shared (one refresh per batch)",
+                              own, own_note, "approx", fp, elapsed / steps * 1e3, stages, steps),
         **({"eight_client_refresh": eight} if eight is not None else {}),
         "cpu_baseline": None,
     }
-    # SURVEY.md §8(d) config E, whole step: 8+4+1 in/out + 8 local-tier state per decision,
-    # K_shared * (4 count + 24 v,p,t) per refresh
-    _step_roofline(line, n * 21 + kshared * 28, "21*N + 28*K_shared (one refresh per batch)", "approx", fp)
     eng.close()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_approx(args, kshared)

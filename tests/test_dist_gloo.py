@@ -27,8 +27,8 @@ def _port() -> int:
     return p
 
 
-def _spawn(fn, *args):
-    mp.start_processes(fn, args=(WORLD, _port()) + args, nprocs=WORLD, join=True,
+def _spawn(fn, *args, world: int = WORLD):
+    mp.start_processes(fn, args=(world, _port()) + args, nprocs=world, join=True,
                        start_method="spawn")
 
 
@@ -134,7 +134,8 @@ def test_owner_maps():
 
 
 def check_tb_route(res):
-    """Expected: one serial table; per step rank 0's batch, then rank 1's."""
+    """Expected: one serial table; per step rank 0's batch, then rank 1's, ..."""
+    WORLD = len(res)
     from oracle import cref
     from oracle.semantics import fill_rate_per_second
     rate = fill_rate_per_second(W.TB["tokens_per_period"], W.TB["period_ticks"])
@@ -173,6 +174,7 @@ def check_approx(res, mode):
     """Expected: the single-process multi-client reference.  clients: client r syncs at
     T + r*stagger and sees clients < r (approx_refresh_all); node: the ranks' counts
     summed into ONE sync call per key, whose reply every rank applies."""
+    WORLD = len(res)
     from oracle.semantics import ApproxClient, ApproxGlobalTable, approx_refresh_all
     A = W.AP
     clients = [ApproxClient(A["token_limit"], A["tokens_per_period"], A["period_ticks"],
@@ -221,6 +223,39 @@ def test_approx_epoch_node_mode_sums_counts(tmp_path):
     check_approx(res, "node")
 
 
+# ---- world size 8: the protocol an 8-GPU node runs, rehearsed with
+# eight gloo ranks on the CPU -- routing under the hash (§8e) and balanced owner maps, queued
+# waits with routed cancels, and both approximate exchange modes -- against the same serial
+# restatements.  Multi-GPU figures stay unmeasured on hardware; this checks the protocol.
+W8 = 8
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("map_kind", ["hash", "balanced"])
+def test_world8_route_batch_matches_serial_reference(oracle_lib, tmp_path, map_kind):
+    _spawn(W.tb_route_worker, str(tmp_path), map_kind, world=W8)
+    res = [np.load(tmp_path / f"tb_{r}.npz") for r in range(W8)]
+    check_tb_route(res)
+    assert all(res[r]["dir_keys"].size > 0 for r in range(W8))   # every owner received keys
+
+
+@pytest.mark.timeout(600)
+def test_world8_route_wait_and_cancel_matches_serial_reference(tmp_path):
+    _spawn(W.q_route_worker, str(tmp_path), world=W8)
+    check_q_route([np.load(tmp_path / f"q_{r}.npz") for r in range(W8)])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["clients", "node"])
+def test_world8_approx_epoch_matches_reference(tmp_path, mode):
+    _spawn(W.ap_epoch_worker, str(tmp_path), mode, world=W8)
+    res = [np.load(tmp_path / f"ap_{mode}_{r}.npz") for r in range(W8)]
+    if mode == "node":
+        for r in range(1, W8):
+            assert np.array_equal(res[0]["state"][:, 1:3], res[r]["state"][:, 1:3])
+    check_approx(res, mode)
+
+
 def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
     """Queued waits routed to their owners, then cancels of some of them routed the same
     way (cluster.route_cancel), then a replenish tick on every rank.  Expected = one
@@ -230,6 +265,7 @@ def test_route_wait_and_cancel_matches_serial_reference(tmp_path):
 
 
 def check_q_route(res):
+    WORLD = len(res)
     from oracle.semantics import QueueingTokenBucketTable, TokenBucketConfig
     from distributedratelimiting.redis_amd import cluster
     Q = W.Q

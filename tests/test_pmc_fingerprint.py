@@ -70,7 +70,13 @@ def test_queue_roofline_traffic_follows_the_match(tmp_path, monkeypatch):
     fp = bk.run_fingerprint(_args(workload="queue", token_limit=4, interval_us=1000), 1, 100_000_000, LAYOUT)
     monkeypatch.setattr(bk, "PMC_SUMMARY", _summary(tmp_path, fp))
     monkeypatch.setattr(bk.pmc_workload, "__defaults__", (bk.PMC_SUMMARY,))
-    r = bk._roofline("fold", 3.84e9, 2.89, "note", "queue", fp)
+    stages = {"fold": 57.8, "scatter": 20.0}
+    r = bk._roofline(2.89, 2.88e9, "B_alg", 3.84e9, "own", "queue", fp, 4.2, stages, 20)
     assert r["traffic"] == 6.5e9 and "traffic_null_reason" not in r
-    r = bk._roofline("fold", 3.84e9, 2.89, "note", "queue", dict(fp, keys_per_gpu=12_500_000))
+    # frac = the step's B_alg over the fold's launch time; the fold's own
+    # bytes are reported beside it
+    assert r["kernel"] == "fold" and r["frac"] == round(2.88e9 / 2.89e-3 / 1e9 / bk.HBM_PEAK_GBS, 4)
+    assert r["kernel_own_bytes"] == int(3.84e9) and r["largest_stage"] == "fold"
+    r = bk._roofline(2.89, 2.88e9, "B_alg", 3.84e9, "own", "queue", dict(fp, keys_per_gpu=12_500_000), 4.2,
+                     stages, 20)
     assert r["traffic"] is None and "keys_per_gpu" in r["traffic_null_reason"]

@@ -29,6 +29,11 @@ run() {   # run <name> <secs> <cmd...>
 }
 [ "${SKIP_CALIB:-0}" = 1 ] || run calib 120 python3 "$ROOT/tools/pmc_calib.py"
 for W in ${WORKLOADS:-uniform}; do
+    if [ "$W" = queue_draining ]; then   # config D's draining schedule (the markers go around it)
+        run $W 300 python3 "$ROOT/bench.py" --workload queue --steps 20 --warmup 5 --cpu-seconds 0 \
+            --no-stage-timing --no-host-buffer --no-strdir --drain-marked
+        continue
+    fi
     run $W 240 python3 "$ROOT/bench.py" --workload $W --steps 20 --warmup 5 --cpu-seconds 0 \
         --no-stage-timing --no-host-buffer --no-strdir --no-sparse --no-drain-variant
 done
