@@ -1012,8 +1012,10 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
     static_assert(!(FIRST && LAST), "fold records come from a pass after the first");
     // narrow pass-0 records (F.n0): FIRST writes u32 records (+ escaped times to ts0), LAST
     // reads them with the pass-1 digit from the digit stream `din`; the LDS stage then holds
-    // record | digit(s) << 32, since the record no longer carries the key
-    const bool n0 = F.n0 != 0 && !IDX && !NOTS;
+    // record | digit(s) << 32, since the record no longer carries the key.  The queueing
+    // kind (IDX) keeps its arrival index beside them; the approximate kind (NOTS) has no
+    // time: its narrow record is row | permit code (round 6)
+    const bool n0 = F.n0 != 0;
     __shared__ RankLds<kPartBlock> L;
     __shared__ uint32_t goff[kDigits];
     __shared__ uint64_t stage[kTile];
@@ -1058,8 +1060,11 @@ __global__ __launch_bounds__(kPartBlock, FIRST ? TBE_SCATTER0_WAVES : 1) void k_
             const int e = wb_elem<kPartBlock, kPartItems>(it);   // wave-blocked tile order
             bad |= (e < nvalid) && (pv[it] < 0 || (!NOTS && tv[it] < 0));
             if (n0) {
-                bool esc;
-                const uint32_t r32 = pack_rec32(skv[it], pv[it], tv[it], tbase, F, esc);
+                bool esc = false;
+                const uint32_t r32 =
+                    NOTS ? (skv[it] & ((1u << F.rb) - 1u)) |
+                               ((uint32_t)(pv[it] < 0 ? 0 : (pv[it] > F.pc_max ? F.pc_max : pv[it])) << F.rb)
+                         : pack_rec32(skv[it], pv[it], tv[it], tbase, F, esc);
                 // stage: record | pass-0 digit << 32 | pass-1 digit << 40; escape flag in bit 48
                 rec[it] = (uint64_t)r32 | ((uint64_t)((skv[it] >> shift) & (kDigits - 1)) << 32) |
                           ((uint64_t)((skv[it] >> (shift + kDigitBits)) & (kDigits - 1)) << 40) |
@@ -1331,6 +1336,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     auto slice_dma = [&]() {
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
+#if defined(TBE_FOLD_COPY_ONLY) && defined(TBE_COPY_ROWS)
+            if (u * kWideBlock >= (TBE_COPY_ROWS)) break;   // A/B: a 3/4 slice
+#endif
             const uint32_t j = tid + u * kWideBlock;
             lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
         }
@@ -1394,7 +1402,10 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         for (int r = 0; r < kWidePer; ++r)
             if (pend & (1u << r)) put_reply(res, pos[r], kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
     }
-    for (uint32_t j = tid; j < nrows; j += kWideBlock) ST_S(rows + j, row[j]);
+#ifndef TBE_COPY_ROWS
+#define TBE_COPY_ROWS kMaxRows   // A/B: rows per slice written back (3/4: the bytes of 12-byte rows)
+#endif
+    for (uint32_t j = tid; j < nrows && j < (uint32_t)(TBE_COPY_ROWS); j += kWideBlock) ST_S(rows + j, row[j]);
     return;
 #endif
 
@@ -3787,7 +3798,7 @@ tbe_status ensure_workspace(tbe_engine *e, Workspace &w, uint64_t n) {
     w.bs_tag = 0;
     if (e->unrank) HIP_TRY(e, hipMalloc(&w.dig0, cap));
     if (e->dig1) HIP_TRY(e, hipMalloc(&w.dig1, cap));
-    if (e->n0) HIP_TRY(e, hipMalloc(&w.ts0, cap * sizeof(int64_t)));
+    if (e->n0 && e->cfg.kind != TBE_KIND_APPROXIMATE) HIP_TRY(e, hipMalloc(&w.ts0, cap * sizeof(int64_t)));
     w.cap_n = cap;
     return TBE_OK;
 }
@@ -3858,7 +3869,9 @@ FoldFmt batch_fold_fmt(const tbe_engine *e, uint64_t n) {
     const int tw = 64 - e->r_bits - e->pf.pb - 1 - pw;
     if (tw >= (approx ? 1 : 8)) {   // (the approximate kind's records carry no time)
         G.on = 1;
-        G.n0 = e->n0 ? 1 : 0;
+        // approximate kind: narrow pass-0 records only in batches that cannot queue, whose
+        // fold never reads an arrival index (k_fold_a's arrival())
+        G.n0 = (e->n0 && !(approx && e->wait_mode)) ? 1 : 0;
         G.rb = e->r_bits;
         G.pb = e->pf.pb;
         G.pw = pw;
@@ -3980,28 +3993,28 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         stage_begin(e, ST_SCATTER, sp);
         if (e->packed && approx && p == 0)
             k_scatter_rec<true, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
-                keys, permits, nullptr, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                keys, permits, nullptr, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr,
                 nullptr, FoldFmt{}, dnext);
         else if (e->packed && approx && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
-                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, pf, out.tileprefix,
                 out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0, nullptr,
-                nullptr, G);
+                nullptr, G, nullptr, w.dig1);
         else if (e->packed && approx)
             k_scatter_rec<false><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
                 out.blockprefix, out.digit_total, tpb, out.rec, out.perm, w.err);
         else if (e->packed && wait && p == 0)
             k_scatter_rec<true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
-                keys, permits, ts, nullptr, n, shift, e->pf, out.tileprefix, out.blockprefix,
+                keys, permits, ts, nullptr, n, shift, pf, out.tileprefix, out.blockprefix,
                 out.digit_total, tpb, out.rec, unrank ? nullptr : out.perm, w.err, nullptr, 0, 0, nullptr, out.idx,
-                FoldFmt{}, dnext);
+                FoldFmt{}, dnext, nullptr, w.ts0);
         else if (e->packed && wait && G.on && p == e->passes - 1)
             k_scatter_rec<false, false, true, false, true><<<ntiles, kPartBlock, 0, sp>>>(
-                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
+                nullptr, nullptr, ts, w.pass[p - 1].rec, n, shift, pf, out.tileprefix,
                 out.blockprefix, out.digit_total, tpb, out.rec, nullptr, w.err, nullptr, 0, 0,
-                w.pass[p - 1].idx, out.idx, G);
+                w.pass[p - 1].idx, out.idx, G, nullptr, w.dig1);
         else if (e->packed && wait)
             k_scatter_rec<false, false, true><<<ntiles, kPartBlock, 0, sp>>>(
                 nullptr, nullptr, nullptr, w.pass[p - 1].rec, n, shift, e->pf, out.tileprefix,
@@ -4358,7 +4371,11 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->dig1 = e->packed && e->passes == 2 && (c.flags & TBE_FLAG_HIST_RECORDS) == 0;
         {
             const int w0 = 32 - e->r_bits - pbits - 1;
-            e->n0 = TBE_NARROW0 && e->dig1 && e->foldrec && c.kind == TBE_KIND_TOKEN_BUCKET && w0 >= 8;
+            // token bucket and queueing kinds: the time offset needs >= 8 bits; the approximate
+            // kind's narrow record is row | permit code (no time), used by batches that cannot
+            // queue (AcquireCore: no arrival index is ever read, batch_fold_fmt)
+            e->n0 = TBE_NARROW0 && e->dig1 && e->foldrec &&
+                    (c.kind == TBE_KIND_APPROXIMATE ? e->r_bits + pbits + 1 <= 32 : w0 >= 8);
             e->pf.n0 = 0;                  // per batch (run_batch): only with this batch's fold records
             e->pf.rb = e->r_bits;
             e->pf.w0 = w0;

@@ -177,6 +177,11 @@ VARIANT_SETS = {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "hotpipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_hot_summary_pipelined.patch"),
     },
+    "rows12": {   # round 6: the fold's copy-only floor with 16-byte rows and with 3/4 of the bytes
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "copy34_u": (["TBE_FOLD_COPY_ONLY", "TBE_COPY_ROWS=1536"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
