@@ -268,3 +268,94 @@ def test_back_to_back_tick_batches(engine_lib, gpu, order, qlimit):
     assert np.array_equal(tt, tt2)
     m = tt2 != np.iinfo(np.int64).min
     assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_queue_narrow_pass0_with_escapes(engine_lib, gpu, order):
+    """Round 6: the queueing kind's pass 0 writes 4-byte records (row | permit code | escape
+    | time offset) beside the arrival index.  1e6 keys (r_bits 10) at TokenLimit 62 leave a
+    15-bit time window (+-16 ms): batches spread over 4 s mostly escape (their times go to
+    the side array), tight ones fit; fused ticks between them.  Statuses, remaining counts,
+    evictions, drain logs, queues and the table against the C restatement (Q:67-134,
+    Q:237-271)."""
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+    n_keys, n, tl, ql = 1_000_000, 1 << 20, 62, 16
+    eng = QueueingTokenBucketEngine(n_keys, tl, 5, 10_000_000, ql, order, device=0)
+    assert eng.layout()["narrow_pass0"]
+    assert eng.batch_format(n)["pass0_time_bits"] == 15
+    ref = cref.CQueueingTokenBucket(n_keys, tl, fill_rate(5, 10_000_000), ql, order)
+    rng = np.random.default_rng(17 + order)
+    cap = n_keys * min(ql, tl)
+    t = S_US
+    for b, spread in enumerate([4_000_000, 1_000, 4_000_000, 20_000, 1_000]):
+        keys = rng.integers(0, n_keys // 8, n).astype(np.uint64)     # ~8 requests per key
+        permits = rng.choice([0, 1, 2, 7, 20, 63], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, spread, n))).astype(np.int64)
+        if b == 2:
+            ts = ts[::-1].copy()                                    # out of order
+        t += spread + 500_000
+        d = [_dev(keys.view(np.int64), gpu), _dev(permits, gpu), _dev(ts, gpu)]
+        st = torch.empty(n, dtype=torch.uint8, device=gpu)
+        rem = torch.empty(n, dtype=torch.int32, device=gpu)
+        lg = (torch.empty(cap, dtype=torch.int64, device=gpu), torch.empty(cap, dtype=torch.int64, device=gpu),
+              torch.empty(cap, dtype=torch.int32, device=gpu), torch.empty(1, dtype=torch.int32, device=gpu))
+        torch.cuda.synchronize()
+        eng.wait_batch_tick_device(*d, st, rem, b * n, t, *lg)
+        eng.synchronize()
+        st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, b * n, threads=8)
+        bad = np.flatnonzero((st.cpu().numpy() != st2) | (rem.cpu().numpy() != rem2))
+        assert bad.size == 0, (b, bad.size, bad[:5])
+        cause, ids = eng.evicted()
+        assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2)
+        k1, i1, r1 = _sorted_log(*lg)
+        k2, i2, r2 = ref.refresh(t, threads=8)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2), b
+    for k in range(0, n_keys // 8, 1231):
+        assert eng.queue_of(k) == ref.queue_of(k)
+    v, tt = eng.export_state()
+    v2, tt2 = ref.bucket_state()
+    assert np.array_equal(tt, tt2)
+    m = tt2 != np.iinfo(np.int64).min
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+def test_approx_narrow_pass0_acquire_then_wait(engine_lib, gpu):
+    """Round 6: the approximate kind's AcquireCore batches take 4-byte pass-0 records (row |
+    permit code; nothing reads an arrival index), its WaitAsync batches the 8-byte ones that
+    carry it.  Both alternate on one engine at 1e6 keys; statuses, availability, evictions
+    and sampled local tiers against the C restatement (A:84-214)."""
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    n_keys, n, tl = 1_000_000, 1 << 20, 40
+    eng = ApproximateEngine(n_keys, tl, 10, 10_000_000, 6, 1, device=0)
+    assert eng.layout()["narrow_pass0"]
+    ref = cref.CApprox(n_keys, tl, 10, 10_000_000, 6, 1, 4)
+    rng = np.random.default_rng(5)
+    counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    d_st = torch.empty(n, dtype=torch.uint8, device=gpu)
+    d_av = torch.empty(n, dtype=torch.int32, device=gpu)
+    for e, wait in enumerate([False, True, False, True, False]):
+        keys = rng.integers(0, n_keys // 16, n).astype(np.uint64)
+        permits = rng.choice([0, 1, 2, 5, 41], n).astype(np.int32)
+        torch.cuda.synchronize()
+        eng.acquire_batch_device(_dev(keys.view(np.int64), gpu), _dev(permits, gpu), d_st, d_av,
+                                 wait=wait, id_base=e * n)
+        eng.synchronize()
+        s2, a2, c2, i2 = ref.acquire_batch(keys, permits, wait=wait, id_base=e * n, threads=8)
+        bad = np.flatnonzero((d_st.cpu().numpy() != s2) | (d_av.cpu().numpy() != a2))
+        assert bad.size == 0, (e, wait, bad.size, bad[:5])
+        cause, ids = eng.evicted()
+        assert np.array_equal(cause, c2) and np.array_equal(ids, i2)
+        ts = S_US + (e + 1) * 1_000_000
+        eng.collect(counts)
+        torch.cuda.synchronize()
+        got = eng.sync(counts, 1, 0, ts, 0)
+        exp = ref.sync(ref.collect(), 1, 0, ts, 0, threads=8)
+        for a, b in zip(got, exp):
+            assert np.array_equal(a, b)
+    x = ref.export()
+    for k in range(0, n_keys // 16, 997):
+        lo, gl, est, av, q = eng.local_state(k)
+        assert (lo, gl, est, av, q) == (x["local"][k], x["global"][k], x["est"][k], x["available"][k],
+                                        x["queued"][k])

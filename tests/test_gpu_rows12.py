@@ -1,0 +1,129 @@
+"""The token-bucket table's 12-byte rows (round 6): v exactly, the grant
+time as a 32-bit offset from the row's bucket epoch, times that do not fit in the side
+array (csrc/tbe_engine.hip "token-bucket rows, 12 B").  Every decision must stay the
+reference script's (TB:202-238) whatever the timestamps do, so these traces move time by
+hours -- forward, backward, out of order inside a batch -- under a 10-hour TTL (rows stay
+present across the jumps), through dense folds (which move the epochs and take rows back
+from the side array), sparse folds, hot-key runs, and export -> import.  Every reply and the
+whole table against the C restatement."""
+import numpy as np
+import pytest
+
+from oracle import cref
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_760_572_800 * 1_000_000
+H = 3_600_000_000                 # one hour in us
+ABSENT = np.iinfo(np.int64).min
+THREADS = 8
+
+
+def _rate():
+    from distributedratelimiting.redis_amd import fill_rate
+    return fill_rate(1, 36_000_000_000)   # 1 token per hour: TTL ceil(10 / rate) = 10 h
+
+
+def _engine(n_keys, max_batch, **kw):
+    from distributedratelimiting.redis_amd import TokenBucketEngine
+    return TokenBucketEngine(n_keys, 10, 1, 36_000_000_000, device=0, max_batch=max_batch, **kw)
+
+
+def _check(eng, ref, keys, permits, ts, tag):
+    g, r = eng.acquire_batch(keys, permits, ts)
+    g2, r2 = ref.acquire_batch(keys, permits, ts, threads=THREADS)
+    bad = np.flatnonzero((g != g2) | (r != r2))
+    assert bad.size == 0, (tag, bad.size, bad[:5], keys[bad[:5]], ts[bad[:5]])
+
+
+def _check_table(eng, ref):
+    v, t = eng.export_state()
+    v2, t2 = ref.export_state()
+    assert np.array_equal(t, t2), np.flatnonzero(t != t2)[:10]
+    m = t2 != ABSENT
+    assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+# (offset from T0 in us, spread of the batch in us, batch size, out of order)
+SCHEDULE = [
+    (0, 1_000, 1 << 20, False),             # dense: every bucket's epoch set
+    (10_000, 5_000, 1 << 12, False),        # sparse
+    (3 * H, 1_000, 1 << 20, False),         # +3 h: epochs move, the rows of 0 go to the side array
+    (3 * H + 50_000, 2_000, 1 << 12, False),
+    (H, 10_000, 1 << 20, True),             # back to +1 h, out of order: writes below the epochs
+    (5 * H, 7 * H, 1 << 20, False),         # one batch spanning 7 hours
+    (5 * H + 1, 1_000, 1 << 14, False),     # sparse again
+    (20 * H, 1_000, 1 << 20, False),        # +20 h: every row has lapsed (TTL 10 h)
+]
+
+
+def test_rows12_time_jumps_dense_and_sparse(engine_lib, gpu):
+    n_keys = 1_000_000                         # r_bits 10: dense batches of 2^20, sparse below
+    eng = _engine(n_keys, 1 << 20)
+    ref = cref.CTokenBucket(n_keys, 10, _rate())
+    rng = np.random.default_rng(606)
+    assert eng.batch_format(1 << 12)["sparse"] and not eng.batch_format(1 << 20)["sparse"]
+    for i, (off, spread, n, ooo) in enumerate(SCHEDULE):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.integers(0, 4, n).astype(np.int32)
+        ts = (T0 + off + np.sort(rng.integers(0, spread, n))).astype(np.int64)
+        if ooo:
+            rng.shuffle(ts)
+        _check(eng, ref, keys, permits, ts, i)
+        _check_table(eng, ref)
+    eng.close()
+
+
+def test_rows12_hot_keys_across_jumps(engine_lib, gpu):
+    """Zipf batches whose hot keys run apart (k_hot_chain reads and writes their rows
+    through the bucket epochs), with time jumping hours between them."""
+    n_keys, n = 4_000_000, 1 << 22
+    eng = _engine(n_keys, n)
+    assert eng.layout()["hot"]
+    ref = cref.CTokenBucket(n_keys, 10, _rate())
+    rng = np.random.default_rng(77)
+    perm = rng.permutation(1 << 20).astype(np.uint64) * 3 + 1
+    for i, off in enumerate([0, 2 * H, 2 * H + 1_000, -H, 4 * H, 4 * H + 10]):
+        ranks = np.minimum(rng.zipf(1.1, n), 1 << 20) - 1
+        keys = perm[ranks]
+        permits = rng.integers(0, 3, n).astype(np.int32)
+        ts = (T0 + 2 * H + off + np.sort(rng.integers(0, 20_000, n))).astype(np.int64)
+        _check(eng, ref, keys, permits, ts, i)
+    _check_table(eng, ref)
+    eng.close()
+
+
+def test_rows12_export_import_with_side_rows(engine_lib, gpu):
+    """A table whose rows span hours (some in the side array) exported and imported into a
+    fresh engine -- whose buckets have no epoch yet, so every imported time starts in the
+    side array -- then both engines decide the same batches as the restatement."""
+    n_keys = 300_000
+    a = _engine(n_keys, 1 << 19)
+    ref = cref.CTokenBucket(n_keys, 10, _rate())
+    rng = np.random.default_rng(5)
+    for off in (0, 4 * H, 2 * H):
+        keys = rng.integers(0, n_keys, 1 << 19).astype(np.uint64)
+        permits = rng.integers(0, 4, 1 << 19).astype(np.int32)
+        ts = (T0 + off + np.sort(rng.integers(0, 1_000, 1 << 19))).astype(np.int64)
+        _check(a, ref, keys, permits, ts, off)
+    v, t = a.export_state()
+    b = _engine(n_keys, 1 << 19)
+    b.import_state(v[:100_000], t[:100_000])
+    b.import_state(v[100_000:], t[100_000:], first=100_000)
+    v2, t2 = b.export_state()
+    assert np.array_equal(t, t2) and np.array_equal(v[t != ABSENT].view(np.uint64), v2[t != ABSENT].view(np.uint64))
+    for off in (4 * H + 5_000, 6 * H, 6 * H + 10):
+        keys = rng.integers(0, n_keys, 1 << 19).astype(np.uint64)
+        permits = rng.integers(0, 4, 1 << 19).astype(np.int32)
+        ts = (T0 + off + np.sort(rng.integers(0, 1_000, 1 << 19))).astype(np.int64)
+        ga, ra = a.acquire_batch(keys, permits, ts)
+        gb, rb = b.acquire_batch(keys, permits, ts)
+        g2, r2 = ref.acquire_batch(keys, permits, ts, threads=THREADS)
+        assert np.array_equal(gb, g2) and np.array_equal(rb, r2), off
+        assert np.array_equal(ga, g2) and np.array_equal(ra, r2), off
+    _check_table(b, ref)
+    va, ta = a.export_state()
+    vb, tb = b.export_state()
+    assert np.array_equal(ta, tb) and np.array_equal(va[ta != ABSENT].view(np.uint64), vb[tb != ABSENT].view(np.uint64))
+    a.close()
+    b.close()
