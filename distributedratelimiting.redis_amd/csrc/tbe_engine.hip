@@ -1386,8 +1386,10 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
     uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0,
     const uint32_t *__restrict__ dlist = nullptr) {
-    // the bucket's slice as stored: 3 words per row (12-byte rows), 16-byte chunks by LDS-DMA
-    __shared__ __attribute__((aligned(16))) uint32_t sw[3 * kMaxRows];
+    // The bucket's rows as Slot {v, t_us} (16 B) while the rounds run.  The slice arrives as
+    // stored, 3 words per row (12-byte rows), by LDS-DMA into the top 3/4 of this array and
+    // is expanded in place (expand_rows); the write-back encodes the dirty lines again.
+    __shared__ __attribute__((aligned(16))) Slot row[kMaxRows];
     __shared__ uint32_t side_any;   // a row of this bucket has its time in the side array
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
@@ -1421,28 +1423,38 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     // so none of the loop invariants spill at this peak.  The table is padded to whole
     // buckets (and 16 KB), so every chunk a wave loads exists; chunks past the slice land
     // in sw past its 3R words and are never written back.
+    uint32_t *const raw = reinterpret_cast<uint32_t *>(row) + kMaxRows;   // words [R, 4R): the stored slice
     auto slice_dma = [&]() {
 #pragma unroll
         for (int u = 0; u < kChunksPerThread; ++u) {
             if ((uint32_t)(u * kWideBlock) < nchunks)   // wave-uniform
                 lds_dma16(reinterpret_cast<const uint4 *>(wrows) + u * kWideBlock + tid,
-                          &sw[4 * (u * kWideBlock + (tid & ~63))]);
+                          &raw[4 * (u * kWideBlock + (tid & ~63))]);
         }
     };
-    // rows j of the slice, decoded against the bucket's epoch E (set below) / encoded back
-    int64_t E = kEpochUnset;
+    int64_t E = kEpochUnset;                        // the bucket's epoch for the write-back (below)
     int64_t *__restrict__ sideb = T.side + row0;   // (uniform: the side entries of this slice)
-    auto rd = [&](uint32_t j) -> Slot {
-        return row_decode(sw[3 * j], sw[3 * j + 1], sw[3 * j + 2], E, sideb, j);
-    };
-    auto wrow = [&](uint32_t j, const Slot &v) {
-        bool esc = false;
-        const uint32_t t32 = t32_encode(v.t_us, E, sideb, j, esc);
-        if (esc) side_any = 1u;
-        const uint64_t bits = (uint64_t)__double_as_longlong(v.v);
-        sw[3 * j] = (uint32_t)bits;
-        sw[3 * j + 1] = (uint32_t)(bits >> 32);
-        sw[3 * j + 2] = t32;
+    // Expand the landed slice into Slot rows, decoding times against the bucket's stored
+    // epoch: every thread first reads all its rows' words (they lie above every Slot it
+    // writes only once all are read), then writes the Slots.
+    auto expand_rows = [&](int64_t E0) {
+        constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
+        uint32_t w0[kRowsPerThread], w1[kRowsPerThread], w2[kRowsPerThread];
+#pragma unroll
+        for (int u = 0; u < kRowsPerThread; ++u) {
+            const uint32_t j = tid + u * kWideBlock;
+            if (j < R) {
+                w0[u] = raw[3 * j];
+                w1[u] = raw[3 * j + 1];
+                w2[u] = raw[3 * j + 2];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kRowsPerThread; ++u) {
+            const uint32_t j = tid + u * kWideBlock;
+            if (j < R) row[j] = row_decode(w0[u], w1[u], w2[u], E0, sideb, j);
+        }
     };
     if (*err) return;
     const uint32_t s = bstart[b], e = bstart[b + 1];
@@ -1515,7 +1527,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             if (pend & (1u << r)) put_reply(res, pos[r], kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
     }
     for (uint32_t c = tid; c < nchunks; c += kWideBlock)
-        chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, *reinterpret_cast<const uint4 *>(&sw[4 * c]));
+        chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, *reinterpret_cast<const uint4 *>(&raw[4 * c]));
     return;
 #endif
 
@@ -1526,20 +1538,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (uint32_t j = tid; j < R; j += kWideBlock) hcnt[j] = 0;
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
-        if (c == s && conv) {
-            // re-encode the slice against the new epoch (and take times back from the side
-            // array where they now fit); only rows whose words change become dirty
-            for (uint32_t j = tid; j < R; j += kWideBlock) {
-                const uint32_t t32 = sw[3 * j + 2];
-                if (t32 == kT32Absent) continue;
-                bool esc = false;
-                const uint32_t n32 = t32_encode(t32_decode(t32, be0.e, sideb, j), E, sideb, j, esc);
-                if (esc) side_any = 1u;
-                if (n32 != t32) {
-                    sw[3 * j + 2] = n32;
-                    atomicOr(&dirty[j >> 5], 1u << (j & 31));
-                }
-            }
+        if (c == s) {
+            expand_rows(be0.e);
             __syncthreads();
         }
 #if TBE_FOLD_PREFETCH
@@ -1589,7 +1589,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (int r = 0; r < kWidePer; ++r) {
                 nrow[r] = Slot{0.0, 0};
                 if (pend & (1u << r)) {
-                    nrow[r] = rd(kl[r]);
+                    nrow[r] = row[kl[r]];
                     bool m;
                     // request times recomputed per evaluation (registers: three slots)
                     const ReqTime rqr = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
@@ -1607,7 +1607,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 if ((o >> 12) != round || o < tag) {
                     pend &= ~(1u << r);             // before the key's first modifier: decided
                 } else if (o == tag) {
-                    wrow(kl[r], nrow[r]);           // the row this round's evaluation produced
+                    row[kl[r]] = nrow[r];           // the row this round's evaluation produced
                     WIDE_FT_SET(kl[r], rq[r].new_t);        // its field t (unused while absent)
                     atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                     pend &= ~(1u << r);
@@ -1667,7 +1667,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                 const uint32_t tag = (round << 12) | (4095u - tlid);
                 Slot nr = Slot{0.0, 0};
                 if (tp) {
-                    nr = rd(tkl);
+                    nr = row[tkl];
                     bool m;
                     trep = tb_step_ft(nr, WIDE_FT_GET(tkl, nr), tpm, trq, P, m);
                     if (m) atomicMax(&own[tkl], tag);
@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     if ((o >> 12) != round || o < tag) {
                         tp = false;
                     } else if (o == tag) {
-                        wrow(tkl, nr);
+                        row[tkl] = nr;
                         WIDE_FT_SET(tkl, trq.new_t);
                         atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
                         tp = false;
@@ -1727,7 +1727,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     const uint32_t tag = (round << 12) | tag_lo;
                     Slot nr = Slot{0.0, 0};
                     if (pend & bit) {
-                        nr = rd(kl[r]);
+                        nr = row[kl[r]];
                         bool m;
                         const ReqTime rqr = PACKED ? req_time_rel(tsv[r], TB, P.ttl_ms) : req_time(tsv[r], P.ttl_ms);
                         rep[r] = tb_step_ft(nr, WIDE_FT_GET(kl[r], nr), pm[r], rqr, P, m);
@@ -1739,7 +1739,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                         if ((o >> 12) != round || o < tag) {
                             pend &= ~bit;
                         } else if (o == tag) {
-                            wrow(kl[r], nr);
+                            row[kl[r]] = nr;
                             WIDE_FT_SET(kl[r], rq[r].new_t);
                             atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                             pend &= ~bit;
@@ -1761,12 +1761,36 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     __syncthreads();
     // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log):
     // the 16-byte chunks of every 128-byte line of the slice that holds a modified row
+    // Encoded against the bucket's epoch E: when E moved (or rows sat in the side array) every
+    // line goes back, re-encoded; a row's time that does not fit E goes to the side array.
     for (uint32_t c = tid; c < nchunks; c += kWideBlock) {
         const uint32_t g = c >> 3;
         const uint32_t lo = (128u * g) / 12u, hi = min((128u * g + 127u) / 12u, R - 1u);
-        if (rows_dirty(dirty, lo, hi))
-            chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, *reinterpret_cast<const uint4 *>(&sw[4 * c]));
+        if (!conv && !rows_dirty(dirty, lo, hi)) continue;
+        // chunk c = words 4c .. 4c+3 of the stored slice: rows 4c/3 and (4c+3)/3
+        const uint32_t ra = (4u * c) / 3u, rb = (4u * c + 3u) / 3u;
+        auto enc = [&](uint32_t j, uint32_t &x0, uint32_t &x1, uint32_t &x2) {
+            const Slot sj = row[j];
+            bool esc = false;
+            x2 = t32_encode(sj.t_us, E, sideb, j, esc);
+            if (esc) side_any = 1u;
+            const uint64_t bits = (uint64_t)__double_as_longlong(sj.v);
+            x0 = (uint32_t)bits;
+            x1 = (uint32_t)(bits >> 32);
+        };
+        uint32_t a0, a1, a2, b0, b1, b2;
+        enc(ra, a0, a1, a2);
+        enc(rb, b0, b1, b2);
+        // word 4c + k is field (4c + k) % 3 of row (4c + k) / 3 (register selects, no arrays)
+        auto pick = [&](uint32_t k) -> uint32_t {
+            const uint32_t wi = 4u * c + k, rj = wi / 3u, f = wi - 3u * rj;
+            const bool A = rj == ra;
+            const uint32_t x0 = A ? a0 : b0, x1 = A ? a1 : b1, x2 = A ? a2 : b2;
+            return f == 0u ? x0 : (f == 1u ? x1 : x2);
+        };
+        chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, uint4{pick(0), pick(1), pick(2), pick(3)});
     }
+    __syncthreads();   // side_any complete
     if (tid == 0 && (E != be0.e || side_any != be0.side)) T.be[b] = BucketEpoch{E, side_any, 0u};
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
@@ -2682,6 +2706,8 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
         const uint64_t v = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
         *reinterpret_cast<u64x4 *>(kr + (tail & ~3u)) = u64x4{v, v, v, v};
     }
+#elif defined(TBE_Q_RING_NT)   // A/B: the ring entry as a non-temporal store
+    __builtin_nontemporal_store(((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p, kr + tail);
 #elif !defined(TBE_Q_NO_RING_WRITE)
     kr[tail] = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
 #else
