@@ -1432,8 +1432,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                           &raw[4 * (u * kWideBlock + (tid & ~63))]);
         }
     };
-    int64_t E = kEpochUnset;                        // the bucket's epoch for the write-back (below)
-    int64_t *__restrict__ sideb = T.side + row0;   // (uniform: the side entries of this slice)
     // Expand the landed slice into Slot rows, decoding times against the bucket's stored
     // epoch: every thread first reads all its rows' words (they lie above every Slot it
     // writes only once all are read), then writes the Slots.
@@ -1453,7 +1451,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 #pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
             const uint32_t j = tid + u * kWideBlock;
-            if (j < R) row[j] = row_decode(w0[u], w1[u], w2[u], E0, sideb, j);
+            if (j < R) row[j] = row_decode(w0[u], w1[u], w2[u], E0, T.side + row0, j);
         }
     };
     if (*err) return;
@@ -1463,16 +1461,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     // is pulled in (LDS-DMA) and only its dirty lines are written back.
     if (e - s < wide_min) return;
     const bool dense = true;
-    // The bucket's epoch: kept while the batch's first time lies in [E + 2^29, E + 3 * 2^30],
-    // else moved to ts[0] - 2^31; moving it (or taking rows back from the side array)
-    // re-encodes the slice once it has landed (`conv`, block-uniform)
-    const BucketEpoch be0 = T.be[b];
-    {
-        const int64_t tref = PACKED ? ts_orig[0] : sts[s];
-        E = be0.e;
-        if (E == kEpochUnset || tref - E < kEpochLo || tref - E > kEpochHi) E = tref - kEpochLead;
-    }
-    const bool conv = E != be0.e || be0.side != 0u;
     if (tid == 0) side_any = 0u;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
@@ -1539,8 +1527,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
         if (c == s) {
-            expand_rows(be0.e);
-            __syncthreads();
+            expand_rows(T.be[b].e);   // (the epoch is read again at the write-back: nothing of it
+            __syncthreads();          // stays live through the rounds)
         }
 #if TBE_FOLD_PREFETCH
         // Touch one word per 128-B line of the slice and of the records of the workgroup
@@ -1761,8 +1749,18 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     __syncthreads();
     // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log):
     // the 16-byte chunks of every 128-byte line of the slice that holds a modified row
-    // Encoded against the bucket's epoch E: when E moved (or rows sat in the side array) every
-    // line goes back, re-encoded; a row's time that does not fit E goes to the side array.
+    // Encoded against the bucket's epoch E, kept while the batch's first time lies in
+    // [E + 2^29, E + 3 * 2^30], else moved to ts[0] - 2^31.  When E moved (or rows sat in the
+    // side array: `conv`, block-uniform) every line goes back, re-encoded; a row's time that
+    // does not fit E goes to the side array.
+    const BucketEpoch be0 = T.be[b];
+    int64_t E = be0.e;
+    {
+        const int64_t tref = PACKED ? ts_orig[0] : sts[s];
+        if (E == kEpochUnset || tref - E < kEpochLo || tref - E > kEpochHi) E = tref - kEpochLead;
+    }
+    const bool conv = E != be0.e || be0.side != 0u;
+    int64_t *__restrict__ sideb = T.side + row0;
     for (uint32_t c = tid; c < nchunks; c += kWideBlock) {
         const uint32_t g = c >> 3;
         const uint32_t lo = (128u * g) / 12u, hi = min((128u * g + 127u) / 12u, R - 1u);

@@ -34,7 +34,7 @@ def run(lib, dev, bufs, settle):
         time.sleep(settle)
     st = torch.empty(N, dtype=torch.uint8, device=dev)
     rem = torch.empty(N, dtype=torch.int32, device=dev)
-    cap = 1 << 27
+    cap = N_KEYS * 4          # tbe_refresh_bound: min(QueueLimit, TokenLimit) grants per key
     lk = torch.empty(cap, dtype=torch.int64, device=dev)
     li = torch.empty(cap, dtype=torch.int64, device=dev)
     lr = torch.empty(cap, dtype=torch.int32, device=dev)
