@@ -405,12 +405,7 @@ def main():
             k = bufs[s][0]
             kw = k[g_all[i].bool()]
             uw.append((int(torch.unique(k).numel()), int(torch.unique(kw).numel())))
-            if layout.get("rows12"):   # 12-byte rows: a row may straddle two 128-byte lines
-                lr = torch.unique(torch.cat([k * 12 // 128, (k * 12 + 11) // 128]))
-                lw = torch.unique(torch.cat([kw * 12 // 128, (kw * 12 + 11) // 128]))
-                lines.append((int(lr.numel()), int(lw.numel())))
-            else:
-                lines.append((int(torch.unique(k // 8).numel()), int(torch.unique(kw // 8).numel())))
+            lines.append((int(torch.unique(k // 8).numel()), int(torch.unique(kw // 8).numel())))
         del g_all
         line_read = float(np.mean([a for a, _ in lines]))
         line_written = float(np.mean([b for _, b in lines]))

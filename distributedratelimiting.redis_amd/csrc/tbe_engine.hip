@@ -1228,90 +1228,6 @@ __device__ __forceinline__ bool row_line_dirty(const uint32_t *dirty, uint32_t j
 __device__ __forceinline__ bool row_dirty(const uint32_t *dirty, uint32_t j) {
     return (dirty[j >> 5] >> (j & 31u)) & 1u;
 }
-// any of rows lo..hi (hi - lo < 32) modified
-__device__ __forceinline__ bool rows_dirty(const uint32_t *dirty, uint32_t lo, uint32_t hi) {
-    const uint32_t w0 = lo >> 5, w1 = hi >> 5;
-    const uint32_t m0 = dirty[w0] >> (lo & 31u);
-    if (w0 == w1) return (m0 & ((2u << (hi - lo)) - 1u)) != 0u;
-    return m0 != 0u || (dirty[w1] & ((2u << (hi & 31u)) - 1u)) != 0u;
-}
-__device__ __forceinline__ void chunk_store_nt(uint4 *p, const uint4 &v) {
-    u32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
-}
-
-// ----------------------------------------------------------------- token-bucket rows, 12 B
-// (round 6).  The fold moves the table at 128-byte line granularity, so
-// the bytes per row set its cost.  A token-bucket row is stored as three
-// words, {v lo, v hi, t32}, 12 bytes instead of the 16 of Slot: field v exactly (f64), and
-// the grant time as a 32-bit offset from its BUCKET's epoch E (one i64 per bucket):
-//   t32 = 0                 absent (never granted, or deleted by passive expiry)
-//   t32 = 0xFFFFFFFF        the time did not fit: it is in side[key] (i64)
-//   t32 = t_us - E + 1      otherwise (t_us - E in [0, 2^32 - 3]: a 71-minute window)
-// Every time stays exact -- the side array takes whatever does not fit -- so no input
-// (timestamps out of order, hours apart, a clock stepped back) changes a decision; only
-// the speed.  The dense fold (k_fold_wide), which holds a bucket's whole slice, moves the
-// bucket's epoch along with the batch's time (E = ts[0] - 2^31 whenever ts[0] leaves
-// [E + 2^29, E + 3*2^30]) and re-encodes the slice, taking escaped times back from the side
-// array where they now fit; the sparse fold and the hot-key runs encode against the
-// epoch as it stands.  `side` in BucketEpoch flags a bucket that has rows in the side array.
-constexpr int64_t kEpochUnset = INT64_MIN;
-constexpr uint32_t kT32Absent = 0u;
-constexpr uint32_t kT32Side = 0xFFFFFFFFu;
-constexpr int64_t kT32Max = 0xFFFFFFFDll;             // t_us - E in [0, kT32Max]
-constexpr int64_t kEpochLead = (int64_t)1 << 31;      // a new epoch: the batch's ts[0] - 2^31
-constexpr int64_t kEpochLo = (int64_t)1 << 29;        // keep E while ts[0] - E in [kEpochLo, kEpochHi]
-constexpr int64_t kEpochHi = (int64_t)3 << 30;
-struct BucketEpoch {
-    int64_t e;        // the bucket's epoch (kEpochUnset until its first dense fold)
-    uint32_t side;    // nonzero: some row of the bucket has its time in the side array
-    uint32_t pad;
-};
-struct RowsTB {       // the token-bucket table
-    uint32_t *w;      // 3 words per key
-    BucketEpoch *be;  // per bucket
-    int64_t *side;    // per key; read only where t32 == kT32Side
-};
-__device__ __forceinline__ bool t32_fits(int64_t t, int64_t E) {
-    return E != kEpochUnset && t >= E && t - E <= kT32Max;
-}
-__device__ __forceinline__ int64_t t32_decode(uint32_t t32, int64_t E, const int64_t *__restrict__ side, uint64_t key) {
-    if (t32 == kT32Absent) return kAbsent;
-    if (t32 == kT32Side) return side[key];
-    return E + (int64_t)(t32 - 1u);
-}
-// encode t against E; a time that does not fit goes to side[key] (*escaped set)
-__device__ __forceinline__ uint32_t t32_encode(int64_t t, int64_t E, int64_t *__restrict__ side, uint64_t key,
-                                               bool &escaped) {
-    if (t == kAbsent) return kT32Absent;
-    if (t32_fits(t, E)) return (uint32_t)(t - E) + 1u;
-    side[key] = t;
-    escaped = true;
-    return kT32Side;
-}
-__device__ __forceinline__ Slot row_decode(uint32_t lo, uint32_t hi, uint32_t t32, int64_t E,
-                                           const int64_t *__restrict__ side, uint64_t key) {
-    Slot s;
-    s.v = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-    s.t_us = t32_decode(t32, E, side, key);
-    return s;
-}
-// one row from / to global memory (sparse fold, hot runs): three dwords at 12 * key
-__device__ __forceinline__ Slot row12_load(const RowsTB &T, uint64_t key, int64_t E) {
-    const uint32_t *p = T.w + 3 * key;
-    return row_decode(p[0], p[1], p[2], E, T.side, key);
-}
-// returns true when the time went to the side array (the caller flags the bucket)
-__device__ __forceinline__ bool row12_store(const RowsTB &T, uint64_t key, int64_t E, const Slot &s) {
-    bool esc = false;
-    const uint32_t t32 = t32_encode(s.t_us, E, T.side, key, esc);
-    const uint64_t bits = (uint64_t)__double_as_longlong(s.v);
-    uint32_t *p = T.w + 3 * key;
-    p[0] = (uint32_t)bits;
-    p[1] = (uint32_t)(bits >> 32);
-    p[2] = t32;
-    return esc;
-}
 
 // Shape of k_fold_wide (profiles/r02_ablate_wide*.log): 512 threads x 2 requests per
 // chunk, the rows' field t derived per evaluation instead of cached, a 256-entry pending
@@ -1382,15 +1298,11 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
-    int r_bits, uint64_t n_keys, RowsTB T, TbParams P,
+    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, HotSet *__restrict__ hot_next,
     uint32_t narrow, uint32_t wide_min, FoldFmt G, const uint64_t *__restrict__ rec0,
     const uint32_t *__restrict__ dlist = nullptr) {
-    // The bucket's rows as Slot {v, t_us} (16 B) while the rounds run.  The slice arrives as
-    // stored, 3 words per row (12-byte rows), by LDS-DMA into the top 3/4 of this array and
-    // is expanded in place (expand_rows); the write-back encodes the dirty lines again.
-    __shared__ __attribute__((aligned(16))) Slot row[kMaxRows];
-    __shared__ uint32_t side_any;   // a row of this bucket has its time in the side array
+    __shared__ Slot row[kMaxRows];
     // aux: requests per row in buckets that may hold a hot key (hcnt), otherwise the
     // compact list of requests still pending after round 1 (t_*)
     // A pending entry is 16 bytes (row | local id << 16, permits, timestamp); its request
@@ -1416,42 +1328,19 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const uint32_t rmask = R - 1;
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
-    uint32_t *__restrict__ wrows = T.w + 3 * row0;
-    const uint32_t nchunks = (3u * R) >> 2;                     // 16-byte chunks of the slice
-    constexpr int kChunksPerThread = (3 * kMaxRows / 4 + kWideBlock - 1) / kWideBlock;
+    Slot *__restrict__ rows = table + row0;
+    constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
     // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held for it,
-    // so none of the loop invariants spill at this peak.  The table is padded to whole
-    // buckets (and 16 KB), so every chunk a wave loads exists; chunks past the slice land
-    // in sw past its 3R words and are never written back.
-    uint32_t *const raw = reinterpret_cast<uint32_t *>(row) + kMaxRows;   // words [R, 4R): the stored slice
+    // so none of the loop invariants spill at this peak.  Rows past nrows get a copy of the
+    // last row; no request reaches them and they are never written.
     auto slice_dma = [&]() {
 #pragma unroll
-        for (int u = 0; u < kChunksPerThread; ++u) {
-            if ((uint32_t)(u * kWideBlock) < nchunks)   // wave-uniform
-                lds_dma16(reinterpret_cast<const uint4 *>(wrows) + u * kWideBlock + tid,
-                          &raw[4 * (u * kWideBlock + (tid & ~63))]);
-        }
-    };
-    // Expand the landed slice into Slot rows, decoding times against the bucket's stored
-    // epoch: every thread first reads all its rows' words (they lie above every Slot it
-    // writes only once all are read), then writes the Slots.
-    auto expand_rows = [&](int64_t E0) {
-        constexpr int kRowsPerThread = (kMaxRows + kWideBlock - 1) / kWideBlock;
-        uint32_t w0[kRowsPerThread], w1[kRowsPerThread], w2[kRowsPerThread];
-#pragma unroll
         for (int u = 0; u < kRowsPerThread; ++u) {
+#if defined(TBE_FOLD_COPY_ONLY) && defined(TBE_COPY_ROWS)
+            if (u * kWideBlock >= (TBE_COPY_ROWS)) break;   // A/B: a 3/4 slice
+#endif
             const uint32_t j = tid + u * kWideBlock;
-            if (j < R) {
-                w0[u] = raw[3 * j];
-                w1[u] = raw[3 * j + 1];
-                w2[u] = raw[3 * j + 2];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kRowsPerThread; ++u) {
-            const uint32_t j = tid + u * kWideBlock;
-            if (j < R) row[j] = row_decode(w0[u], w1[u], w2[u], E0, T.side + row0, j);
+            lds_dma16(rows + (j < nrows ? j : nrows - 1), &row[u * kWideBlock + (tid & ~63)]);
         }
     };
     if (*err) return;
@@ -1461,7 +1350,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     // is pulled in (LDS-DMA) and only its dirty lines are written back.
     if (e - s < wide_min) return;
     const bool dense = true;
-    if (tid == 0) side_any = 0u;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
@@ -1514,8 +1402,10 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         for (int r = 0; r < kWidePer; ++r)
             if (pend & (1u << r)) put_reply(res, pos[r], kl[r] ^ (uint32_t)pm[r] ^ (uint32_t)tsv[r], narrow);
     }
-    for (uint32_t c = tid; c < nchunks; c += kWideBlock)
-        chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, *reinterpret_cast<const uint4 *>(&raw[4 * c]));
+#ifndef TBE_COPY_ROWS
+#define TBE_COPY_ROWS kMaxRows   // A/B: rows per slice written back (3/4: the bytes of 12-byte rows)
+#endif
+    for (uint32_t j = tid; j < nrows && j < (uint32_t)(TBE_COPY_ROWS); j += kWideBlock) ST_S(rows + j, row[j]);
     return;
 #endif
 
@@ -1526,10 +1416,6 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             for (uint32_t j = tid; j < R; j += kWideBlock) hcnt[j] = 0;
         lds_dma_wait();    // (first chunk) this wave's slice DMA landed
         __syncthreads();   // own[] reset, bitmaps and (first chunk) dense slice visible
-        if (c == s) {
-            expand_rows(T.be[b].e);   // (the epoch is read again at the write-back: nothing of it
-            __syncthreads();          // stays live through the rounds)
-        }
 #if TBE_FOLD_PREFETCH
         // Touch one word per 128-B line of the slice and of the records of the workgroup
         // TBE_FOLD_PREFETCH blocks later (the same XCD), so that its loads find them in L2 or
@@ -1543,12 +1429,11 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             if (fblk < gridDim.x && (!G.on || fb < G.nb)) {
                 const uint32_t fs = bstart[fb], fe = bstart[fb + 1];
                 if (fe - fs >= wide_min && fe > fs) {
-                    constexpr int kLines = 3 * kMaxRows / 32;   // 128-byte lines of a slice
-                    if (tid < kLines) {
-                        if ((uint32_t)tid * 32u < 3u * R)
-                            pf_sink = T.w[3 * ((uint64_t)fb << r_bits) + (uint64_t)tid * 32u];
+                    if (tid < (int)(kMaxRows / 8)) {
+                        const uint64_t fr = ((uint64_t)fb << r_bits) + (uint64_t)tid * 8u;
+                        if (fr < n_keys) pf_sink = reinterpret_cast<const uint32_t *>(table + fr)[0];
                     } else if (PACKED) {
-                        const uint32_t q = fs + (uint32_t)(tid - kLines) * 16u;
+                        const uint32_t q = fs + (uint32_t)(tid - kMaxRows / 8) * 16u;
                         if (q < fe) pf_sink = (uint32_t)srec[q];
                     }
                 }
@@ -1747,49 +1632,9 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
         }
     }
     __syncthreads();
-    // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log):
-    // the 16-byte chunks of every 128-byte line of the slice that holds a modified row
-    // Encoded against the bucket's epoch E, kept while the batch's first time lies in
-    // [E + 2^29, E + 3 * 2^30], else moved to ts[0] - 2^31.  When E moved (or rows sat in the
-    // side array: `conv`, block-uniform) every line goes back, re-encoded; a row's time that
-    // does not fit E goes to the side array.
-    const BucketEpoch be0 = T.be[b];
-    int64_t E = be0.e;
-    {
-        const int64_t tref = PACKED ? ts_orig[0] : sts[s];
-        if (E == kEpochUnset || tref - E < kEpochLo || tref - E > kEpochHi) E = tref - kEpochLead;
-    }
-    const bool conv = E != be0.e || be0.side != 0u;
-    int64_t *__restrict__ sideb = T.side + row0;
-    for (uint32_t c = tid; c < nchunks; c += kWideBlock) {
-        const uint32_t g = c >> 3;
-        const uint32_t lo = (128u * g) / 12u, hi = min((128u * g + 127u) / 12u, R - 1u);
-        if (!conv && !rows_dirty(dirty, lo, hi)) continue;
-        // chunk c = words 4c .. 4c+3 of the stored slice: rows 4c/3 and (4c+3)/3
-        const uint32_t ra = (4u * c) / 3u, rb = (4u * c + 3u) / 3u;
-        auto enc = [&](uint32_t j, uint32_t &x0, uint32_t &x1, uint32_t &x2) {
-            const Slot sj = row[j];
-            bool esc = false;
-            x2 = t32_encode(sj.t_us, E, sideb, j, esc);
-            if (esc) side_any = 1u;
-            const uint64_t bits = (uint64_t)__double_as_longlong(sj.v);
-            x0 = (uint32_t)bits;
-            x1 = (uint32_t)(bits >> 32);
-        };
-        uint32_t a0, a1, a2, b0, b1, b2;
-        enc(ra, a0, a1, a2);
-        enc(rb, b0, b1, b2);
-        // word 4c + k is field (4c + k) % 3 of row (4c + k) / 3 (register selects, no arrays)
-        auto pick = [&](uint32_t k) -> uint32_t {
-            const uint32_t wi = 4u * c + k, rj = wi / 3u, f = wi - 3u * rj;
-            const bool A = rj == ra;
-            const uint32_t x0 = A ? a0 : b0, x1 = A ? a1 : b1, x2 = A ? a2 : b2;
-            return f == 0u ? x0 : (f == 1u ? x1 : x2);
-        };
-        chunk_store_nt(reinterpret_cast<uint4 *>(wrows) + c, uint4{pick(0), pick(1), pick(2), pick(3)});
-    }
-    __syncthreads();   // side_any complete
-    if (tid == 0 && (E != be0.e || side_any != be0.side)) T.be[b] = BucketEpoch{E, side_any, 0u};
+    // dirty lines stream out (non-temporal: 12% faster fold, profiles/r01_v10_ablate.log)
+    for (uint32_t j = tid; j < nrows; j += kWideBlock)
+        if (row_line_dirty(dirty, j)) ST_S(rows + j, row[j]);
     if (count_hot) {
         // nominate this bucket's hot keys for their own runs in the next batch
         for (uint32_t j = tid; j < nrows; j += kWideBlock) {
@@ -1829,7 +1674,7 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint64_t *__restrict__ srec,
     const int64_t *__restrict__ ts_orig, PackFmt F, const uint32_t *__restrict__ bstart,
-    int r_bits, uint64_t n_keys, RowsTB T, TbParams P,
+    int r_bits, uint64_t n_keys, Slot *__restrict__ table, TbParams P,
     uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow, uint32_t wide_min,
     FoldFmt G, const uint64_t *__restrict__ rec0, uint32_t n_walk) {
     if (*err) return;
@@ -1858,9 +1703,7 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
             work &= work - 1;
             const uint32_t b = __shfl(my_b, j, 64);
             const uint32_t s = __shfl(my_s, j, 64), e = __shfl(my_e, j, 64);
-            const uint64_t row0 = (uint64_t)b << r_bits;
-            const int64_t E = T.be[b].e;   // (only k_fold_wide moves an epoch)
-            bool esc_any = false;
+            Slot *__restrict__ rows = table + ((uint64_t)b << r_bits);
             for (uint32_t c = s; c < e; c += 64) {
                 // the previous chunk's row stores are visible to this wave's loads below: a
                 // workgroup-scope fence (the stores complete; the CU's L1 is write-through).
@@ -1890,7 +1733,7 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
                 }
                 const bool leader = v && (peers & lt) == 0;   // the key's earliest request here
                 Slot st = Slot{0.0, 0};
-                if (leader) st = row12_load(T, row0 + kl, E);
+                if (leader) st = rows[kl];
                 uint64_t todo = leader ? peers : 0ull;
                 bool mod = false;
                 while (__any(todo != 0ull)) {
@@ -1907,9 +1750,8 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
                         todo &= todo - 1;
                     }
                 }
-                if (leader && mod) esc_any |= row12_store(T, row0 + kl, E, st);
+                if (leader && mod) rows[kl] = st;
             }
-            if (__any(esc_any) && lane == 0) atomicOr(&T.be[b].side, 1u);
         }
     }
 }
@@ -2137,7 +1979,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, uint32_t *segbase,
     SegSummary *__restrict__ summ, const uint32_t *__restrict__ err, FoldFmt G, const uint64_t *__restrict__ rec0,
-    const HotSet *__restrict__ hot = nullptr, RowsTB T = RowsTB{}, int r_bits = 0, TbParams P = TbParams{},
+    const HotSet *__restrict__ hot = nullptr, const Slot *__restrict__ table = nullptr, TbParams P = TbParams{},
     uint32_t *__restrict__ res = nullptr, uint32_t narrow = 0, uint32_t plan = 0) {
     __shared__ int64_t wts[kSegBlock / 64];
     __shared__ int32_t wp[kSegBlock / 64];
@@ -2179,8 +2021,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
         int64_t mx = INT64_MIN;
         int32_t mn = INT32_MAX;
         // the run's row before the batch, in flight with the records (SPEC)
-        const uint32_t hk = SPEC ? hot->key[h] : 0u;
-        const Slot s0 = SPEC ? row12_load(T, hk, T.be[hk >> r_bits].e) : Slot{0.0, 0};
+        const Slot s0 = SPEC ? table[hot->key[h]] : Slot{0.0, 0};
         uint64_t rv[kSegItems];   // every record of the segment in flight at once
 #pragma unroll
         for (int it = 0; it < kSegItems; ++it) {
@@ -2248,7 +2089,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, uint32_t nb, const HotSet *__restrict__ hot,
     HotSet *__restrict__ hot_next, const uint32_t *__restrict__ segbase,
-    const SegSummary *__restrict__ summ, SegState *__restrict__ sst, RowsTB T, int r_bits,
+    const SegSummary *__restrict__ summ, SegState *__restrict__ sst, Slot *__restrict__ table,
     TbParams P, uint32_t *__restrict__ res, const uint32_t *__restrict__ err, uint32_t narrow, FoldFmt G,
     const uint64_t *__restrict__ rec0, uint32_t spec) {
     __shared__ Slot S;
@@ -2265,9 +2106,8 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
     const TimeBase TB = time_base(tbase, P.ttl_ms);
-    const int64_t Ek = T.be[key >> r_bits].e;   // the row's bucket epoch (k_fold_wide ran before)
     if (tid == 0) {
-        S = row12_load(T, key, Ek);
+        S = table[key];
         ftS = new_t_of(S.t_us == kAbsent ? 0 : S.t_us);
     }
     __syncthreads();
@@ -2362,7 +2202,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
         cur = f + 1;
     }
     if (tid == 0) {
-        if (touched && row12_store(T, key, Ek, S)) atomicOr(&T.be[key >> r_bits].side, 1u);
+        if (touched) table[key] = S;
         if (e0 - s0 >= kHotMin / 2) {                 // still hot: nominate again
             const uint32_t at = atomicAdd(&hot_next->n_cand, 1u);
             if (at < kHotCandMax) hot_next->cand[at] = ((uint64_t)(e0 - s0) << 32) | key;
@@ -3663,20 +3503,6 @@ __global__ void k_init_table(Slot *__restrict__ table, uint64_t n_keys, double c
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = i; k < n_keys; k += stride) table[k] = Slot{cap, kAbsent};
 }
-// token-bucket rows: every row absent with v = cap (the padding past them was zeroed), every
-// bucket without an epoch
-__global__ void k_init_rows12(uint32_t *__restrict__ w, uint64_t rows, double cap, BucketEpoch *__restrict__ be,
-                              uint64_t nb) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t bits = (uint64_t)__double_as_longlong(cap);
-    for (uint64_t k = i; k < rows; k += stride) {
-        w[3 * k] = (uint32_t)bits;
-        w[3 * k + 1] = (uint32_t)(bits >> 32);
-        w[3 * k + 2] = kT32Absent;
-    }
-    for (uint64_t b = i; b < nb; b += stride) be[b] = BucketEpoch{kEpochUnset, 0u, 0u};
-}
 
 __global__ void k_sticky(const uint32_t *__restrict__ err, uint32_t *__restrict__ sticky) {
     if (threadIdx.x == 0 && *err) *sticky = 1u;
@@ -3789,13 +3615,7 @@ struct tbe_engine {
     uint32_t nb_total = 0;
     HotSet *hot[3] = {nullptr, nullptr, nullptr};
     uint64_t nbatch = 0;
-    Slot *table = nullptr;         // queueing kind: 16-byte rows
-    // token-bucket kind: 12-byte rows, per-bucket epochs and the side array (RowsTB)
-    uint32_t *tw = nullptr;
-    BucketEpoch *bep = nullptr;
-    int64_t *tside = nullptr;
-    uint64_t tw_rows = 0;          // rows allocated: whole buckets
-    RowsTB rows() const { return RowsTB{tw, bep, tside}; }
+    Slot *table = nullptr;
     // queueing kind
     QParams qp{};
     uint64_t *qhdr = nullptr;      // per-key queue header
@@ -4315,26 +4135,26 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         if (e->packed) {
             k_fold_wide<true><<<dgrid, kWideBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-                e->rows(), e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0, w.dlist);
+                e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0, w.dlist);
             k_fold_sparse<true><<<sgrid, kSpBlock, 0, sf>>>(
                 nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-                e->rows(), e->params, w.res[0], w.err, e->narrow ? 1u : 0u, tb_wmin, G, rec0, walk);
+                e->table, e->params, w.res[0], w.err, e->narrow ? 1u : 0u, tb_wmin, G, rec0, walk);
         } else {
             k_fold_wide<false><<<dgrid, kWideBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-                e->cfg.n_keys, e->rows(), e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0, w.dlist);
+                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0, w.dlist);
             k_fold_sparse<false><<<sgrid, kSpBlock, 0, sf>>>(
                 sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-                e->cfg.n_keys, e->rows(), e->params, w.res[0], w.err, 0u, tb_wmin, G, rec0, walk);
+                e->cfg.n_keys, e->table, e->params, w.res[0], w.err, 0u, tb_wmin, G, rec0, walk);
         }
     } else if (e->packed) {   // a dense batch: k_fold_wide takes every bucket
         k_fold_wide<true><<<fold_grid, kWideBlock, 0, sf>>>(
             nullptr, nullptr, nullptr, sorted.rec, ts, e->pf, w.bstart, e->r_bits, e->cfg.n_keys,
-            e->rows(), e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0);
+            e->table, e->params, w.res[0], w.err, hot_next, e->narrow ? 1u : 0u, tb_wmin, G, rec0);
     } else {
         k_fold_wide<false><<<e->nbuckets, kWideBlock, 0, sf>>>(
             sorted.keys, sorted.permits, sorted.ts, nullptr, nullptr, e->pf, w.bstart, e->r_bits,
-            e->cfg.n_keys, e->rows(), e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0);
+            e->cfg.n_keys, e->table, e->params, w.res[0], w.err, nullptr, 0u, tb_wmin, G, rec0);
     }
     stage_end(e, ST_FOLD, sf);
     if (hot) {
@@ -4344,10 +4164,10 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         const unsigned sgrid = (unsigned)std::min<uint64_t>(1024, n / kSeg + e->hot_cap);
         // (the summary kernel also scans the run lengths into the runs' first segments)
         k_hot_summary<true><<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
-                                                             w.segbase, w.summ, w.err, G, rec0, hot, e->rows(),
-                                                             e->r_bits, e->params, w.res[0], e->narrow ? 1u : 0u, 1u);
+                                                             w.segbase, w.summ, w.err, G, rec0, hot, e->table,
+                                                             e->params, w.res[0], e->narrow ? 1u : 0u, 1u);
         k_hot_chain<<<e->hot_cap, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets, hot,
-                                                      hot_next, w.segbase, w.summ, w.sst, e->rows(), e->r_bits,
+                                                      hot_next, w.segbase, w.summ, w.sst, e->table,
                                                       e->params, w.res[0], w.err, e->narrow ? 1u : 0u, G, rec0,
                                                       1u);
         k_hot_replies<<<sgrid, kSegBlock, 0, sf>>>(sorted.rec, ts, e->pf, w.bstart, e->nbuckets,
@@ -4596,15 +4416,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     // bytes an earlier allocation left (tests/test_gpu_recreate.py).
     const uint64_t qhdr_n = (c.n_keys + 1) & ~1ull;   // even: k_fold_q loads header pairs
     uint64_t ring_n = 0;
-    constexpr uint64_t kRowsPad = 16384;   // bytes past the last bucket (LDS-DMA chunks of small buckets)
-    if (c.kind == TBE_KIND_TOKEN_BUCKET) {
-        e->tw_rows = (uint64_t)e->nbuckets << e->r_bits;
-        if (dalloc(&e->tw, e->tw_rows * 12 + kRowsPad) != hipSuccess) return bail(TBE_ENOMEM);
-        if (dalloc(&e->bep, (uint64_t)e->nbuckets * sizeof(BucketEpoch)) != hipSuccess) return bail(TBE_ENOMEM);
-        if (dalloc(&e->tside, c.n_keys * sizeof(int64_t)) != hipSuccess) return bail(TBE_ENOMEM);
-    } else if (c.kind == TBE_KIND_QUEUEING) {
-        if (dalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
-    }
+    if (dalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
     if (e->hot_cap)
         for (auto &hs : e->hot)
             if (dalloc(&hs, sizeof(HotSet)) != hipSuccess) return bail(TBE_ENOMEM);
@@ -4647,15 +4459,13 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     zero(e->qhdr, qhdr_n * sizeof(uint64_t));
     zero(e->ring, ring_n * sizeof(uint64_t));
     zero(e->counters, 2 * sizeof(uint32_t));
-    zero(e->tw, e->tw ? e->tw_rows * 12 + kRowsPad : 0);
     for (auto &w : e->ws)
         if (w.bsflags && w.bs_fresh) {
             zero(w.bsflags, kBsMaxBlocks * sizeof(unsigned long long));
             w.bs_fresh = false;
         }
     if (ie != hipSuccess) return bail(TBE_EDEVICE);
-    if (e->table) k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
-    if (e->tw) k_init_rows12<<<2048, 256, 0, e->stream>>>(e->tw, e->tw_rows, e->params.cap, e->bep, e->nbuckets);
+    k_init_table<<<2048, 256, 0, e->stream>>>(e->table, c.n_keys, e->params.cap);
     if (c.kind == TBE_KIND_APPROXIMATE)
         k_init_approx<<<2048, 256, 0, e->stream>>>(c.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt,
                                                    c.token_limit);
@@ -4676,9 +4486,6 @@ void tbe_destroy(tbe_engine *e) {
     free_workspace(e->ws[1]);
     free_staging(e);
     dfree(e->table);
-    dfree(e->tw);
-    dfree(e->bep);
-    dfree(e->tside);
     dfree(e->alocal);
     dfree(e->aclient);
     dfree(e->gv);
@@ -4894,50 +4701,14 @@ tbe_status tbe_synchronize(tbe_engine *e) {
     return TBE_OK;
 }
 
-// Rows [first, first + count) of the table as {v, t_us} (absent: t_us = INT64_MIN), through
-// the token-bucket kind's 12-byte rows, bucket epochs and side array, or the queueing
-// kind's 16-byte ones.  The copies are ordered on the engine's stream.
-static tbe_status read_rows(tbe_engine *e, uint64_t first, uint64_t count, Slot *out) {
-    hipStream_t st = e->stream;
-    if (e->cfg.kind == TBE_KIND_QUEUEING) {
-        HIP_TRY(e, hipMemcpyAsync(out, e->table + first, count * sizeof(Slot), hipMemcpyDeviceToHost, st));
-        HIP_TRY(e, hipStreamSynchronize(st));
-        return TBE_OK;
-    }
-    std::vector<uint32_t> w(3 * count);
-    const uint64_t b0 = first >> e->r_bits, b1 = (first + count - 1) >> e->r_bits;
-    std::vector<BucketEpoch> be(b1 - b0 + 1);
-    HIP_TRY(e, hipMemcpyAsync(w.data(), e->tw + 3 * first, 12 * count, hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipMemcpyAsync(be.data(), e->bep + b0, be.size() * sizeof(BucketEpoch), hipMemcpyDeviceToHost, st));
-    HIP_TRY(e, hipStreamSynchronize(st));
-    bool any_side = false;
-    for (uint64_t i = 0; i < count && !any_side; ++i) any_side = w[3 * i + 2] == kT32Side;
-    std::vector<int64_t> side;
-    if (any_side) {
-        side.resize(count);
-        HIP_TRY(e, hipMemcpyAsync(side.data(), e->tside + first, 8 * count, hipMemcpyDeviceToHost, st));
-        HIP_TRY(e, hipStreamSynchronize(st));
-    }
-    for (uint64_t i = 0; i < count; ++i) {
-        const uint64_t bits = (uint64_t)w[3 * i] | ((uint64_t)w[3 * i + 1] << 32);
-        std::memcpy(&out[i].v, &bits, 8);
-        const uint32_t t32 = w[3 * i + 2];
-        out[i].t_us = t32 == kT32Absent ? kAbsent
-                    : t32 == kT32Side   ? side[i]
-                                        : be[((first + i) >> e->r_bits) - b0].e + (int64_t)(t32 - 1u);
-    }
-    return TBE_OK;
-}
-
 tbe_status tbe_query(tbe_engine *e, uint64_t key, int64_t ts_us, double *v, double *t,
                      int32_t *present) {
     if (!e || !v || !t || !present) return TBE_EINVAL;
-    if (e->cfg.kind == TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not a token-bucket engine");
     if (key >= e->cfg.n_keys) return fail(e, TBE_EINVAL, "key out of range");
     HIP_TRY(e, hipSetDevice(e->device));
     Slot s;
-    const tbe_status rs = read_rows(e, key, 1, &s);
-    if (rs != TBE_OK) return rs;
+    HIP_TRY(e, hipMemcpyAsync(&s, e->table + key, sizeof(Slot), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
     *present = 0;
     *v = 0.0;
     *t = 0.0;
@@ -4952,14 +4723,14 @@ tbe_status tbe_query(tbe_engine *e, uint64_t key, int64_t ts_us, double *v, doub
 
 tbe_status tbe_export_state(tbe_engine *e, uint64_t first, uint64_t count, double *v, int64_t *t_us) {
     if (!e || !v || !t_us) return TBE_EINVAL;
-    if (e->cfg.kind == TBE_KIND_APPROXIMATE) return fail(e, TBE_EINVAL, "not a token-bucket engine");
     if (first > e->cfg.n_keys || count > e->cfg.n_keys - first)
         return fail(e, TBE_EINVAL, "range out of bounds");
     if (count == 0) return TBE_OK;
     HIP_TRY(e, hipSetDevice(e->device));
     std::vector<Slot> tmp(count);
-    const tbe_status rs = read_rows(e, first, count, tmp.data());
-    if (rs != TBE_OK) return rs;
+    HIP_TRY(e, hipMemcpyAsync(tmp.data(), e->table + first, count * sizeof(Slot),
+                              hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
     for (uint64_t i = 0; i < count; ++i) {
         v[i] = tmp[i].v;
         t_us[i] = tmp[i].t_us;
@@ -5048,42 +4819,7 @@ tbe_status tbe_import_state(tbe_engine *e, uint64_t first, uint64_t count, const
     }
     HIP_TRY(e, hipSetDevice(e->device));
     HIP_TRY(e, hipDeviceSynchronize());   // after every enqueued batch, whatever its stream
-    if (e->cfg.kind == TBE_KIND_QUEUEING) {
-        HIP_TRY(e, hipMemcpy(e->table + first, tmp.data(), count * sizeof(Slot), hipMemcpyHostToDevice));
-        return TBE_OK;
-    }
-    // token-bucket rows: times encoded against their bucket's epoch; those that do not fit
-    // (or whose bucket has none yet) go to the side array and flag their bucket
-    const uint64_t b0 = first >> e->r_bits, b1 = (first + count - 1) >> e->r_bits;
-    std::vector<BucketEpoch> be(b1 - b0 + 1);
-    HIP_TRY(e, hipMemcpy(be.data(), e->bep + b0, be.size() * sizeof(BucketEpoch), hipMemcpyDeviceToHost));
-    std::vector<uint32_t> w(3 * count);
-    std::vector<int64_t> side(count, 0);
-    bool any_side = false;
-    for (uint64_t i = 0; i < count; ++i) {
-        uint64_t bits;
-        std::memcpy(&bits, &tmp[i].v, 8);
-        w[3 * i] = (uint32_t)bits;
-        w[3 * i + 1] = (uint32_t)(bits >> 32);
-        const int64_t t = tmp[i].t_us;
-        BucketEpoch &ep = be[((first + i) >> e->r_bits) - b0];
-        if (t == kAbsent) {
-            w[3 * i + 2] = kT32Absent;
-        } else if (ep.e != kEpochUnset && t >= ep.e && t - ep.e <= kT32Max) {
-            w[3 * i + 2] = (uint32_t)(t - ep.e) + 1u;
-        } else {
-            w[3 * i + 2] = kT32Side;
-            side[i] = t;
-            ep.side = 1u;
-            any_side = true;
-        }
-    }
-    HIP_TRY(e, hipMemcpy(e->tw + 3 * first, w.data(), 12 * count, hipMemcpyHostToDevice));
-    if (any_side) {
-        // rows outside [first, first + count) keep their side entries: write only the range
-        HIP_TRY(e, hipMemcpy(e->tside + first, side.data(), 8 * count, hipMemcpyHostToDevice));
-        HIP_TRY(e, hipMemcpy(e->bep + b0, be.data(), be.size() * sizeof(BucketEpoch), hipMemcpyHostToDevice));
-    }
+    HIP_TRY(e, hipMemcpy(e->table + first, tmp.data(), count * sizeof(Slot), hipMemcpyHostToDevice));
     return TBE_OK;
 }
 
@@ -5716,8 +5452,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
               (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
-              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u) | (e->n0 ? 256u : 0u) |
-              (e->tw ? 512u : 0u);
+              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u) | (e->n0 ? 256u : 0u);
     return TBE_OK;
 }
 

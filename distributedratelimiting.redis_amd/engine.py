@@ -186,7 +186,7 @@ class TokenBucketEngine:
                 "hot": bool(c.value & 2), "pipeline": bool(c.value & 4), "narrow": bool(c.value & 8),
                 "medium": bool(c.value & 16), "fold_records": bool(c.value & 32),
                 "digit_stream": bool(c.value & 64), "rerank": bool(c.value & 128),
-                "narrow_pass0": bool(c.value & 256), "rows12": bool(c.value & 512)}
+                "narrow_pass0": bool(c.value & 256)}
 
     def batch_format(self, n: int) -> dict:
         """The record layout a batch of n requests takes (tbe_batch_format)."""

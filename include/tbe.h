@@ -373,9 +373,7 @@ tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t 
  * bit 7 set when the final un-partition re-ranks pass 0's tiles (TBE_FLAG_RERANK sets
  * it), bit 8 set when pass 0 writes narrow 4-byte records (token bucket and queueing kinds
  * with fold records and the digit stream, and the approximate kind's AcquireCore batches; a
- * batch uses them when it uses fold records), bit 9 set when the bucket table keeps 12-byte
- * rows (token-bucket kind: v, and the grant time as a 32-bit offset from its bucket's epoch,
- * exact for any timestamps through a side array). */
+ * batch uses them when it uses fold records). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* The record layout a batch of n requests takes (diagnostics and tests):

@@ -1,11 +1,11 @@
-"""The token-bucket table's 12-byte rows (round 6): v exactly, the grant
-time as a 32-bit offset from the row's bucket epoch, times that do not fit in the side
-array (csrc/tbe_engine.hip "token-bucket rows, 12 B").  Every decision must stay the
-reference script's (TB:202-238) whatever the timestamps do, so these traces move time by
-hours -- forward, backward, out of order inside a batch -- under a 10-hour TTL (rows stay
-present across the jumps), through dense folds (which move the epochs and take rows back
-from the side array), sparse folds, hot-key runs, and export -> import.  Every reply and the
-whole table against the C restatement."""
+"""Timestamps hours apart (round 6).  The decision of the reference script (TB:202-238)
+depends on the stored grant time exactly (refill and passive expiry), so these traces move
+time by hours -- forward, backward, out of order inside a batch, one batch spanning seven
+hours -- under a 10-hour TTL (rows stay present across the jumps), through dense folds,
+sparse folds, hot-key runs and export -> import (the escaped-record paths: times outside a
+batch's record window are read from the caller's array).  Every reply and the whole table
+against the C restatement.  (Written for the 12-byte-row table that round 6 measured and
+dropped, CHANGELOG round 6; they hold for any table layout.)"""
 import numpy as np
 import pytest
 
@@ -57,7 +57,7 @@ SCHEDULE = [
 ]
 
 
-def test_rows12_time_jumps_dense_and_sparse(engine_lib, gpu):
+def test_time_jumps_dense_and_sparse(engine_lib, gpu):
     n_keys = 1_000_000                         # r_bits 10: dense batches of 2^20, sparse below
     eng = _engine(n_keys, 1 << 20)
     ref = cref.CTokenBucket(n_keys, 10, _rate())
@@ -74,7 +74,7 @@ def test_rows12_time_jumps_dense_and_sparse(engine_lib, gpu):
     eng.close()
 
 
-def test_rows12_hot_keys_across_jumps(engine_lib, gpu):
+def test_hot_keys_across_jumps(engine_lib, gpu):
     """Zipf batches whose hot keys run apart (k_hot_chain reads and writes their rows
     through the bucket epochs), with time jumping hours between them."""
     n_keys, n = 4_000_000, 1 << 22
@@ -93,7 +93,7 @@ def test_rows12_hot_keys_across_jumps(engine_lib, gpu):
     eng.close()
 
 
-def test_rows12_export_import_with_side_rows(engine_lib, gpu):
+def test_export_import_with_side_rows(engine_lib, gpu):
     """A table whose rows span hours (some in the side array) exported and imported into a
     fresh engine -- whose buckets have no epoch yet, so every imported time starts in the
     side array -- then both engines decide the same batches as the restatement."""
