@@ -88,6 +88,9 @@ def parse():
                          "fused into the batch's fold (A/B)")
     ap.add_argument("--no-drain-variant", action="store_true",
                     help="config D: skip the second schedule whose ticks grant (draining block)")
+    ap.add_argument("--settle-s", type=float, default=0.0,
+                    help="seconds to wait before the first allocation (lets background device-memory "
+                         "work left by an earlier process finish; reported in the line)")
     ap.add_argument("--drain-marked", action="store_true",
                     help="config D: put the PMC window markers around the draining schedule's timed "
                          "batches instead of the headline's (tools/pmc_passes.sh, run queue_draining)")
@@ -203,6 +206,8 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
+    if args.settle_s > 0:
+        time.sleep(args.settle_s)
     world, rank, local_rank, dist, dev = dist_setup(args)
     if dist:
         import torch.distributed as td
