@@ -91,6 +91,8 @@ def parse():
     ap.add_argument("--settle-s", type=float, default=0.0,
                     help="seconds to wait before the first allocation (lets background device-memory "
                          "work left by an earlier process finish; reported in the line)")
+    ap.add_argument("--engine-first", action="store_true",
+                    help="config D: create the engine before generating the inputs (A/B; round 5's order)")
     ap.add_argument("--drain-marked", action="store_true",
                     help="config D: put the PMC window markers around the draining schedule's timed "
                          "batches instead of the headline's (tools/pmc_passes.sh, run queue_draining)")

@@ -235,8 +235,15 @@ def _queue_pass(args, lib, dev, world, dist, kl, period_ticks, seed, marked=Fals
     # the timed engine records events around the fold alone (the roofline's kernel time, two
     # events per batch: a pair per stage would leave the stream idle ~14 times a batch); the
     # stage breakdown comes from a replay of the same schedule afterwards
-    eng = new_engine(False if args.no_stage_timing else True if args.timed_stage_events else "fold")
+    # inputs first, then the engine -- the order bench.py uses for configs B and C (an engine
+    # created before 33 GB of inputs ran its fold 20-25% slower than the same engine created
+    # after them: profiles/r06h_settle_ab.log, r06i_*; CHANGELOG round 6)
+    timing = False if args.no_stage_timing else True if args.timed_stage_events else "fold"
+    eng = new_engine(timing) if args.engine_first else None   # (A/B: round 5's order)
     bufs = [_gen(lib, seed, kl, s, n, args.interval_us, dev) for s in range(total)]
+    torch.cuda.synchronize()
+    if eng is None:
+        eng = new_engine(timing)
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int32, device=dev)
     # drain log: a tick grants at most min(QueueLimit, TokenLimit) entries per key

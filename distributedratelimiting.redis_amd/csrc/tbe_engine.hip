@@ -2544,8 +2544,6 @@ __device__ __forceinline__ void q_step(Slot &st, uint64_t &hdr, bool &smod, bool
         const uint64_t v = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
         *reinterpret_cast<u64x4 *>(kr + (tail & ~3u)) = u64x4{v, v, v, v};
     }
-#elif defined(TBE_Q_RING_NT)   // A/B: the ring entry as a non-temporal store
-    __builtin_nontemporal_store(((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p, kr + tail);
 #elif !defined(TBE_Q_NO_RING_WRITE)
     kr[tail] = ((uint64_t)(Q.id_base + ai) << 16) | (uint32_t)p;
 #else

@@ -177,10 +177,6 @@ VARIANT_SETS = {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "hotpipe_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"], "wip_hot_summary_pipelined.patch"),
     },
-    "qring": {   # round 6: config D's ring entry stores, plain or non-temporal
-        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
-        "ringnt_q": (["TBE_Q_RING_NT"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
-    },
     "rows12": {   # round 6: the fold's copy-only floor with 16-byte rows and with 3/4 of the bytes
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
