@@ -455,10 +455,12 @@ def run_approx(args, lib, dev, world, rank, dist):
                                  pack=not args.no_pack, fold_records=not args.unscatter_all,
                                  digit_stream=not args.hist_records, rerank=args.rerank)
 
-    # fold events alone in the timed engine; the stage breakdown comes from a replay (below)
-    eng = new_engine(False if args.no_stage_timing else True if args.timed_stage_events else "fold")
+    # fold events alone in the timed engine; the stage breakdown comes from a replay (below).
+    # Inputs first, then the engine, as for configs B, C and D
     seed = SEED_E + 7919 * rank
     bufs = [_gen(lib, seed, kshared, s, n, args.interval_us, dev)[:2] for s in range(total)]
+    torch.cuda.synchronize()
+    eng = new_engine(False if args.no_stage_timing else True if args.timed_stage_events else "fold")
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     av = torch.empty(n, dtype=torch.int32, device=dev)
     counts = torch.empty(kshared, dtype=torch.int32, device=dev)
