@@ -45,6 +45,10 @@ prof() {   # rocprofv3 with the program itself after -- (no launcher hop)
     echo "[prof:$w] rc=$rc"
     tail -n 2 "$OUT/${TAG}_prof_$w.log" | cut -c1-300
     [ $rc -eq 0 ] || exit $rc
+    # kernel statistics and the timed / replay marker windows, for profiles/
+    cp "$OUT/${TAG}_prof_$w/run_kernel_stats.csv" "$OUT/${TAG}_${w}_kernel_stats.csv" 2>/dev/null
+    python3 tools/prof_window.py "$OUT/${TAG}_prof_$w/run_kernel_trace.csv" \
+        --out "$OUT/${TAG}_${w}_kernel_windows.json" > "$OUT/${TAG}_${w}_kernel_windows.txt" 2>&1 || true
 }
 
 for s in "$@"; do
