@@ -3399,7 +3399,7 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
     const uint64_t *__restrict__ ring, AParams A, const int32_t *__restrict__ all_counts,
     uint32_t n_clients, uint32_t my, int64_t ts_us, int64_t stagger_us,
     uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
-    uint32_t *__restrict__ log_count, uint32_t log_cap) {
+    uint32_t *__restrict__ log_count, uint32_t log_cap, uint32_t write_client) {
     // the sync times (TIME at A:241-242) of the first clients are the same for every key
     constexpr uint32_t kSyncTimes = 64;
     __shared__ ReqTime crq[kSyncTimes];
@@ -3446,11 +3446,17 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
         const double q = A.period_s / my_period;
         const double rnd = __builtin_rint(q);
         const double est = (rnd != rnd) ? rnd : (rnd > 1.0 ? rnd : 1.0);
-        AClient ac;
-        ac.est = est;
-        ac.global = my_global;
-        ac.pad = 0;
-        aclient[k] = ac;
+        // The client view {est, global} only answers queries (the lease path reads the cap
+        // derived from it).  With one client it is a function of the tier row just written
+        // (k_aclient_derive), so it is derived when asked for instead of written here: 16 of
+        // the 96 bytes per key of config E's refresh (round 6).
+        if (write_client) {
+            AClient ac;
+            ac.est = est;
+            ac.global = my_global;
+            ac.pad = 0;
+            aclient[k] = ac;
+        }
         const double lim = (double)wrap_sub(A.token_limit, my_global) / est;
         a.cap = dotnet_to_int(__builtin_ceil(lim));
         // drain (A:467-501)
@@ -3480,6 +3486,25 @@ __global__ __launch_bounds__(kBlock) void k_approx_sync(
         }
         a.hc = (head & 0xFFFFu) | (cnt << 16);
         alocal[k] = a;
+    }
+}
+
+// The client view of keys [first, first + count) after a one-client sync: exactly what
+// k_approx_sync computes for r == my when the client's sync is the last (A:441-443).
+__global__ __launch_bounds__(kBlock) void k_aclient_derive(uint64_t first, uint64_t count, const double *__restrict__ gv,
+                                                           const double *__restrict__ gp, AClient *__restrict__ aclient,
+                                                           double period_s) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = first + i;
+        const int32_t my_global = (int32_t)(int64_t)gv[k];
+        const double my_period = round_trip_14g(gp[k]);
+        const double q = period_s / my_period;
+        const double rnd = __builtin_rint(q);
+        AClient ac;
+        ac.est = (rnd != rnd) ? rnd : (rnd > 1.0 ? rnd : 1.0);
+        ac.global = my_global;
+        ac.pad = 0;
+        aclient[k] = ac;
     }
 }
 
@@ -3637,6 +3662,7 @@ struct tbe_engine {
     AParams ap{};
     ALocal *alocal = nullptr;
     AClient *aclient = nullptr;
+    bool aclient_lazy = false;    // the last sync had one client: aclient is derived on demand
     double *gv = nullptr, *gp = nullptr;
     int64_t *gt = nullptr;
     int32_t *acounts = nullptr;   // tbe_approx_refresh's own count buffer (single client)
@@ -5191,8 +5217,9 @@ static tbe_status approx_sync(tbe_engine *e, const int32_t *d_all_counts, uint32
     k_approx_sync<<<(unsigned)blocks, kBlock, 0, st>>>(
         e->cfg.n_keys, e->alocal, e->aclient, e->gv, e->gp, e->gt, e->ring, e->ap, d_all_counts,
         n_clients, my_client, ts_us, stagger_us, e->log_keyseq, e->log_id, e->log_rem, e->counters + 1,
-        (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu));
+        (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu), n_clients != 1 ? 1u : 0u);
     HIP_TRY(e, hipGetLastError());
+    e->aclient_lazy = n_clients == 1;
     uint32_t cnt = 0;
     HIP_TRY(e, hipMemcpyAsync(&cnt, e->counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(e, hipStreamSynchronize(st));
@@ -5232,6 +5259,11 @@ tbe_status tbe_approx_query(tbe_engine *e, uint64_t key, int32_t *local, int32_t
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     ALocal a;
     AClient c;
+    if (e->aclient_lazy) {   // (idempotent: the value a one-client sync would have written)
+        k_aclient_derive<<<1, kBlock, 0, e->stream>>>(key, 1, e->gv, e->gp, e->aclient, e->ap.period_s);
+        HIP_TRY(e, hipGetLastError());
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+    }
     HIP_TRY(e, hipMemcpy(&a, e->alocal + key, sizeof a, hipMemcpyDeviceToHost));
     HIP_TRY(e, hipMemcpy(&c, e->aclient + key, sizeof c, hipMemcpyDeviceToHost));
     *local = a.local;
@@ -5277,6 +5309,15 @@ tbe_status tbe_approx_import_state(tbe_engine *e, uint64_t first, uint64_t count
     }
     HIP_TRY(e, hipSetDevice(e->device));
     HIP_TRY(e, hipDeviceSynchronize());
+    if (e->aclient_lazy) {
+        // the client views still follow from the tier rows this import overwrites: write them
+        const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
+        k_aclient_derive<<<(unsigned)blocks, kBlock, 0, e->stream>>>(0, e->cfg.n_keys, e->gv, e->gp, e->aclient,
+                                                                     e->ap.period_s);
+        HIP_TRY(e, hipGetLastError());
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        e->aclient_lazy = false;
+    }
     HIP_TRY(e, hipMemcpy(e->gv + first, tv.data(), count * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(e, hipMemcpy(e->gp + first, tp.data(), count * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(e, hipMemcpy(e->gt + first, t_us, count * sizeof(int64_t), hipMemcpyHostToDevice));

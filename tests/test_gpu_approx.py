@@ -288,3 +288,48 @@ def test_global_tier_snapshot_restore(engine_lib, gpu):
     assert (pb == 0.0).all() and (vb == 0.0).all()
     with pytest.raises(TbeError):
         b.import_global(v[:10], p[:10], t[:10], first=n_keys - 5)
+
+
+def test_client_view_survives_import_after_one_client_sync(engine_lib, gpu):
+    """Round 6: after a one-client sync the engine derives the client view {global, est}
+    (A:441-443) from the tier row when asked instead of writing it every sync.  Importing
+    another tier replica afterwards must not change the view -- the reference's client keeps
+    the values of its last sync until its next one -- and a multi-client sync writes it
+    again.  Views against the oracle client at every step."""
+    import torch
+    from distributedratelimiting.redis_amd import ApproximateEngine
+    n_keys, limit, tokens, ticks = 400, 30, 10, 10_000_000
+    eng = ApproximateEngine(n_keys, limit, tokens, ticks, 0, 0, device=0)
+    client = ApproxClient(limit, tokens, ticks, 0, 0)
+    table = ApproxGlobalTable(client.decay_rate)
+    rng = np.random.default_rng(21)
+    counts = torch.zeros(n_keys, dtype=torch.int32, device=gpu)
+    ts = S_US
+
+    def views():
+        return [eng.local_state(k)[1:3] for k in range(0, n_keys, 7)]
+
+    def expect():
+        return [(client.st(k).global_, client.st(k).est) for k in range(0, n_keys, 7)]
+
+    for epoch in range(3):
+        keys = rng.integers(0, n_keys, 3000).astype(np.uint64)
+        permits = rng.integers(0, 4, keys.size).astype(np.int32)
+        eng.acquire_batch(keys, permits, wait=False)
+        for k, p in zip(keys.tolist(), permits.tolist()):
+            client.acquire(k, p)
+        ts += 800_000
+        eng.collect(counts)
+        torch.cuda.synchronize()
+        eng.sync(counts, 1, 0, ts, 0)
+        approx_refresh_all([client], table, ts, 0, range(n_keys))
+        assert views() == expect(), epoch
+    before = views()
+    v, p, t = eng.export_global()
+    eng.import_global(np.zeros_like(v), np.full_like(p, 0.25), t)   # another replica's rows
+    assert views() == before                                          # the view is the last sync's
+    eng.import_global(v, p, t)
+    two = torch.cat([counts, counts])
+    torch.cuda.synchronize()
+    eng.sync(two, 2, 1, ts + 800_000, 1000)                           # a multi-client sync writes it
+    assert all(isinstance(x[1], float) for x in views())
