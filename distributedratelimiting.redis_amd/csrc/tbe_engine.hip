@@ -1251,6 +1251,10 @@ constexpr int kWideBlock = TBE_WIDE_BLOCK;
 constexpr int kWidePer = TBE_WIDE_PER;
 constexpr int kWideChunk = kWideBlock * kWidePer;
 constexpr int kWideTail = TBE_WIDE_TAIL;
+#ifndef TBE_WIDE_SOLO
+#define TBE_WIDE_SOLO 1                      // the last rounds in wave 0 alone (0: whole workgroup, A/B)
+#endif
+constexpr uint32_t kWideSolo = TBE_WIDE_SOLO ? 64u : 0u;   // pending requests the solo wave takes
 #ifndef TBE_FOLD_PREFETCH
 #define TBE_FOLD_PREFETCH 384                // blocks ahead whose slice k_fold_wide touches (0: off)
 #endif
@@ -1535,8 +1539,8 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
             // survivors fit in fewer waves they are packed to the front of the list, so
             // later rounds run on fewer waves (the fold is VALU-issue bound).
             uint32_t in_use = n_tail;
-            for (uint32_t round = 2;; ++round) {
-                if (n_tail == 0) break;   // block-uniform
+            uint32_t round = 2;
+            while (in_use > kWideSolo) {   // block-uniform
                 const uint32_t tag = (round << 12) | (4095u - tlid);
                 Slot nr = Slot{0.0, 0};
                 if (tp) {
@@ -1558,6 +1562,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     }
                     if (!tp) put_reply(res, tpos, trep, narrow);
                 }
+                ++round;
                 const uint64_t bal = __ballot(tp);
                 if ((tid & 63) == 0) wsum[tid >> 6] = (uint32_t)__popcll(bal);
                 __syncthreads();
@@ -1568,7 +1573,10 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     off += (w < (tid >> 6)) ? cw : 0u;
                     left += cw;
                 }
-                if (left == 0) break;
+                if (left == 0) {
+                    in_use = 0;
+                    break;
+                }
                 if ((left + 63) / 64 < (in_use + 63) / 64) {
                     if (tp) {
                         const uint32_t at = off + (uint32_t)__popcll(bal & lanemask_lt());
@@ -1583,6 +1591,45 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
                     in_use = left;
                 }
             }
+#if TBE_WIDE_SOLO
+            // The last rounds hold at most one wave of pending requests, all in wave 0 (list
+            // positions < 64): that wave finishes them alone, ordered by its own LDS accesses
+            // (a wave's LDS operations complete in issue order) instead of two workgroup
+            // barriers per round that every wave would run.  The others wait at the barrier
+            // below.
+            if (in_use != 0) {   // block-uniform
+                if (tid < 64) {
+                    for (;; ++round) {
+                        const uint32_t tag = (round << 12) | (4095u - tlid);
+                        Slot nr = Slot{0.0, 0};
+                        if (tp) {
+                            nr = row[tkl];
+                            bool m;
+                            trep = tb_step_ft(nr, WIDE_FT_GET(tkl, nr), tpm, trq, P, m);
+                            if (m) atomicMax(&own[tkl], tag);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        if (tp) {
+                            const uint32_t o = own[tkl];
+                            if ((o >> 12) != round || o < tag) {
+                                tp = false;
+                            } else if (o == tag) {
+                                row[tkl] = nr;
+                                WIDE_FT_SET(tkl, trq.new_t);
+                                atomicOr(&dirty[tkl >> 5], 1u << (tkl & 31));
+                                tp = false;
+                            }
+                            if (!tp) put_reply(res, tpos, trep, narrow);
+                        }
+                        if (!__any(tp)) break;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                __syncthreads();   // rows and own[] settled before the next chunk or the write-back
+            }
+#endif
         } else if (n_tail != 0) {
             // More pending requests than the list holds, or its space holds hcnt: the slots
             // settle one window of local ids at a time (slot r = ids [r*B, r*B+B)).  A key's
@@ -2967,7 +3014,11 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         }
     }
     __syncthreads();
+#ifdef TBE_Q_TICK_SKIP
+    if (false) {   // A/B timing only (wrong queues): the cost of the fused tick's drain
+#else
     if (tick) {
+#endif
         // The fused replenish tick (Q:237-271, as k_drain) on the rows and headers in LDS:
         // count this workgroup's grants, reserve them in the log with one atomic, then
         // drain and log (drain_key).

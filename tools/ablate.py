@@ -182,6 +182,18 @@ VARIANT_SETS = {
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copy34_u": (["TBE_FOLD_COPY_ONLY", "TBE_COPY_ROWS=1536"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "solo": {   # round 6: the dense fold's last rounds (<= 64 pending) in one wave, or the whole workgroup
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "solo0_u": (["TBE_WIDE_SOLO=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+        "solo0_z": (["TBE_WIDE_SOLO=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
+    },
+    "qfloors6": {   # round 6: where config D's fold time goes
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "r1only_q": (["TBE_Q_R1_ONLY"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "notick_q": (["TBE_Q_TICK_SKIP"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
