@@ -862,6 +862,23 @@ __device__ __forceinline__ uint32_t pack_rec32(uint32_t pkey, int32_t p, int64_t
 __device__ __forceinline__ int64_t pack_base(const int64_t *__restrict__ ts, const PackFmt &F) {
     return ts[0] - ((int64_t)1 << (F.wb - 1));
 }
+// req_time_rel's base for a batch (TimeBase): 2^31 us (~35 min) below its first
+// timestamp, so that request times up to ~35 min above it and stored row times up to ~35
+// min below it take the 32-bit path.  Not pack_base: with wb > 32 (few keys or a small
+// TokenLimit, e.g. config D's wb = 33) that sits 2^32 us below, every request lies beyond
+// req_time_rel's window and the whole fold took req_time's 64-bit path.
+#ifndef TBE_REL_BASE
+#define TBE_REL_BASE 1                       // 0: pack_base, as before round 6 (A/B)
+#endif
+__device__ __forceinline__ int64_t rel_base(const int64_t *__restrict__ ts, const PackFmt &F) {
+#if TBE_REL_BASE
+    (void)F;
+    const int64_t b = ts[0] - ((int64_t)1 << 31);
+    return b > 0 ? b : 0;
+#else
+    return pack_base(ts, F);
+#endif
+}
 __device__ __forceinline__ uint64_t pack_rec(uint64_t key, int32_t p, int64_t ts, uint64_t idx,
                                              int64_t tbase, const PackFmt &F) {
     const uint64_t pc = (uint64_t)(p < 0 ? 0 : (p > F.pc_max ? F.pc_max : p));
@@ -1356,7 +1373,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
     const bool dense = true;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request times (req_time_rel)
+    const TimeBase TB = time_base(PACKED ? rel_base(ts_orig, F) : 0, P.ttl_ms);   // fast request times (req_time_rel)
     const bool count_hot = hot_next != nullptr && (e - s) >= kHotMin;
 
     uint32_t kl[kWidePer];
@@ -1696,7 +1713,7 @@ __global__ __launch_bounds__(kWideBlock, TBE_WIDE_WAVES) void k_fold_wide(
 #endif
 }
 
-constexpr int64_t kRowWindow = (int64_t)1 << 31;          // field_t fast path: rows up to ~35 min older
+constexpr int64_t kRowWindow = (int64_t)1 << 31;          // k_drain's time base: rows up to ~35 min older
 
 // Field t of a stored row (TB:203 applied to t_us; only used while the key is present).
 __device__ __forceinline__ double field_t(int64_t t_us, const TimeBase &B) {
@@ -1731,7 +1748,7 @@ __global__ __launch_bounds__(kSpBlock) void k_fold_sparse(
     const uint32_t rmask = (1u << r_bits) - 1u;
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(PACKED ? tbase - kRowWindow : -1, P.ttl_ms);
+    const TimeBase TB = time_base(PACKED ? rel_base(ts_orig, F) : -1, P.ttl_ms);
     const uint64_t lt = lanemask_lt();
     for (uint32_t bb0 = wave; bb0 < n_walk; bb0 += nwaves * 64u) {
         // the bounds of this wave's next 64 buckets: lane j holds bucket bb0 + j * nwaves
@@ -2060,7 +2077,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_summary(
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(tbase, P.ttl_ms);
+    const TimeBase TB = time_base(rel_base(ts_orig, F), P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const uint32_t h = seg_run(segbase, j);
         const uint32_t a = bstart[nb + h] + (j - segbase[h]) * kSeg;
@@ -2152,7 +2169,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_chain(
     const uint32_t j0 = segbase[h], nseg = segbase[h + 1] - j0;
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(tbase, P.ttl_ms);
+    const TimeBase TB = time_base(rel_base(ts_orig, F), P.ttl_ms);
     if (tid == 0) {
         S = table[key];
         ftS = new_t_of(S.t_us == kAbsent ? 0 : S.t_us);
@@ -2268,7 +2285,7 @@ __global__ __launch_bounds__(kSegBlock) void k_hot_replies(
     const uint32_t total = segbase[kHotKeysMax];
     const int64_t tbase = pack_base(ts_orig, F);
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(tbase, P.ttl_ms);
+    const TimeBase TB = time_base(rel_base(ts_orig, F), P.ttl_ms);
     for (uint32_t j = blockIdx.x; j < total; j += gridDim.x) {
         const SegState st = sst[j];
         if (st.pass != 1u) continue;
@@ -2619,10 +2636,24 @@ struct DrainLog {
     int32_t *rem;
     uint32_t cap;
 };
+// The row's field t as tb_step derives it, by req_time_rel against the batch's time base
+// (rows of recent grants take its 32-bit path; any other falls back to req_time).
+#ifndef TBE_TICK_FT
+#define TBE_TICK_FT 1                        // 0: tb_step's own 64-bit derivation (A/B)
+#endif
+__device__ __forceinline__ uint32_t tick_step(Slot &row, int32_t permits, const ReqTime &rq, const TimeBase &TB,
+                                              const TbParams &P, bool &modified) {
+#if TBE_TICK_FT
+    return tb_step_ft(row, req_time_rel(row.t_us == kAbsent ? 0 : row.t_us, TB, 0).new_t, permits, rq, P, modified);
+#else
+    (void)TB;
+    return tb_step(row, permits, rq, P, modified);
+#endif
+}
 template <bool WRITE>
 __device__ __forceinline__ uint32_t drain_key(uint64_t key, Slot &st, uint64_t &h, bool &smod,
-                                              const uint64_t *__restrict__ kr, const ReqTime &rqT, const TbParams &P,
-                                              const QParams &Q, const DrainLog &L, uint32_t at) {
+                                              const uint64_t *__restrict__ kr, const ReqTime &rqT, const TimeBase &TB,
+                                              const TbParams &P, const QParams &Q, const DrainLog &L, uint32_t at) {
     uint32_t cnt = (uint32_t)((h >> 16) & 0xFFFFu);
     if (cnt == 0) return 0;
     uint32_t head = (uint32_t)(h & 0xFFFFu);
@@ -2634,7 +2665,7 @@ __device__ __forceinline__ uint32_t drain_key(uint64_t key, Slot &st, uint64_t &
         {
             Slot probe = s;
             bool pm;
-            if (!(tb_step(probe, 1, rqT, P, pm) >> 31)) {
+            if (!(tick_step(probe, 1, rqT, TB, P, pm) >> 31)) {
                 s = probe;
                 m_any |= pm;
                 break;
@@ -2648,7 +2679,7 @@ __device__ __forceinline__ uint32_t drain_key(uint64_t key, Slot &st, uint64_t &
         const uint64_t ent = kr[idx];
         const int32_t p = (int32_t)(ent & 0xFFFFu);
         bool m;
-        const uint32_t reply = tb_step(s, p, rqT, P, m);
+        const uint32_t reply = tick_step(s, p, rqT, TB, P, m);
         m_any |= m;
         if (!(reply >> 31)) break;
         if (WRITE && at + seq < L.cap) {
@@ -2750,7 +2781,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const bool dense = tick || (e - s) >= (R >> 3);   // a tick drains every row
     const int64_t tbase = PACKED ? pack_base(ts_orig, F) : 0;
     const int64_t tbase1 = G.on ? fold_base(ts_orig, G) : 0;
-    const TimeBase TB = time_base(tbase, P.ttl_ms);   // fast request / row times (req_time_rel)
+    const TimeBase TB = time_base(PACKED ? rel_base(ts_orig, F) : 0, P.ttl_ms);   // fast request / row times (req_time_rel)
     if (dense) {
         // The slice goes HBM -> LDS directly (LDS-DMA, streaming policy): no VGPRs held for
         // it.  Rows one per lane; headers two per lane (16 B), the header array being padded
@@ -2834,16 +2865,18 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             }
         }
         for (uint32_t j = tid; j < R; j += kQBlock) own[j] = 0;   // election slots of this chunk
-        uint32_t mine = 0;
+        uint32_t mine = 0;   // rows this thread gathers (a sparse bucket's first touch)
+        if (!dense) {        // (a dense slice is all loaded)
 #pragma unroll
-        for (int r = 0; r < kQItems; ++r) {
-            if (pend & (1u << r)) {
-                const uint32_t bit = 1u << (kl[r] & 31);
-                const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
-                if (!(old & bit)) mine |= 1u << r;
+            for (int r = 0; r < kQItems; ++r) {
+                if (pend & (1u << r)) {
+                    const uint32_t bit = 1u << (kl[r] & 31);
+                    const uint32_t old = atomicOr(&loaded[kl[r] >> 5], bit);
+                    if (!(old & bit)) mine |= 1u << r;
+                }
             }
         }
-        {
+        if (mine) {
             Slot tmp[kQItems];
             uint64_t th[kQItems];
 #pragma unroll
@@ -3038,7 +3071,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 Slot st = slot[j];
                 uint64_t h = qh[j];
                 bool sm = false;
-                const uint32_t g = drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P,
+                const uint32_t g = drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, TB, P,
                                                     Q, L, 0);
                 mine += g;
                 if (g || sm) need |= 1u << u;
@@ -3059,7 +3092,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 uint64_t h = qh[j];
                 const uint64_t h0 = h;
                 bool smod = false;
-                const uint32_t g = drain_key<true>(row0 + j, st, h, smod, ring + (row0 + j) * (uint64_t)Q.cap, rqT, P,
+                const uint32_t g = drain_key<true>(row0 + j, st, h, smod, ring + (row0 + j) * (uint64_t)Q.cap, rqT, TB, P,
                                                    Q, L, at);
                 at += g;
                 if (smod) slot[j] = st;
@@ -3095,6 +3128,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
     __shared__ uint32_t log_base;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const ReqTime rqT = req_time(ts_us, P.ttl_ms);
+    const TimeBase TB = time_base(ts_us > kRowWindow ? ts_us - kRowWindow : 0, 0);   // rows' field t (tick_step)
     const DrainLog L{log_keyseq, log_id, log_rem, log_cap};
     // block-uniform trip count (the log reservation below is a block-wide scan)
     for (uint64_t k0 = (uint64_t)blockIdx.x * kBlock; k0 < n_keys; k0 += stride) {
@@ -3107,7 +3141,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
         bool sm = false;
         Slot st0 = st;
         uint64_t h0 = h;
-        const uint32_t mine = queued ? drain_key<false>(key, st0, h0, sm, kr, rqT, P, Q, L, 0) : 0u;
+        const uint32_t mine = queued ? drain_key<false>(key, st0, h0, sm, kr, rqT, TB, P, Q, L, 0) : 0u;
         uint32_t total;
         const uint32_t off = block_excl_scan<kBlock>(mine, wsum, &total);
         if (threadIdx.x == 0) log_base = total ? atomicAdd(log_count, total) : 0u;
@@ -3115,7 +3149,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
         if (queued && (mine != 0 || sm)) {   // (else the writing pass is a no-op)
             bool smod = false;
             const uint64_t hb = h;
-            drain_key<true>(key, st, h, smod, kr, rqT, P, Q, L, log_base + off);
+            drain_key<true>(key, st, h, smod, kr, rqT, TB, P, Q, L, log_base + off);
             if (smod) table[key] = st;
             if (h != hb) qhdr[key] = h;
         }

@@ -194,6 +194,16 @@ VARIANT_SETS = {
         "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "notick_q": (["TBE_Q_TICK_SKIP"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
     },
+    "tickft": {   # round 6: the fused tick's row times by req_time_rel, or tb_step's 64-bit path
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir"]),
+        "tickft0_q": (["TBE_TICK_FT=0"], ["--workload", "queue", "--no-host-buffer", "--no-strdir"]),
+    },
+    "relbase": {   # round 6: req_time_rel's base 2^31 us below the batch's first time, or pack_base (wb = 33 in D)
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "rb0_q": (["TBE_REL_BASE=0", "TBE_TICK_FT=0"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "rb0_u": (["TBE_REL_BASE=0", "TBE_TICK_FT=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
