@@ -127,3 +127,60 @@ def test_export_import_with_side_rows(engine_lib, gpu):
     assert np.array_equal(ta, tb) and np.array_equal(va[ta != ABSENT].view(np.uint64), vb[tb != ABSENT].view(np.uint64))
     a.close()
     b.close()
+
+
+def test_queue_time_jumps_with_fused_ticks(engine_lib, gpu):
+    """The queueing kind (Q:67-134) with a replenish tick fused into every batch (Q:237-271)
+    while time jumps by hours.  The folds derive request and row times on a 32-bit path
+    relative to a base 2^31 us below each batch's first time, and fall back to the 64-bit
+    derivation outside it (rows granted hours before, a batch spanning seven hours):
+    statuses, remaining counts, evictions, drain logs, queues and the table against the C
+    restatement.  1e6 keys at TokenLimit 4 give 40-bit record times (no escapes), so every
+    fallback here is the time derivation's own."""
+    import torch
+    from distributedratelimiting.redis_amd import QueueingTokenBucketEngine, fill_rate
+
+    def dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+    n_keys, n, tl, ql = 1_000_000, 1 << 18, 4, 16
+    for order in (0, 1):
+        eng = QueueingTokenBucketEngine(n_keys, tl, 1, 36_000_000_000, ql, order, device=0, max_batch=n)
+        ref = cref.CQueueingTokenBucket(n_keys, tl, fill_rate(1, 36_000_000_000), ql, order)
+        rng = np.random.default_rng(91 + order)
+        cap = n_keys * min(ql, tl)
+        lg = (torch.empty(cap, dtype=torch.int64, device=gpu), torch.empty(cap, dtype=torch.int64, device=gpu),
+              torch.empty(cap, dtype=torch.int32, device=gpu), torch.empty(1, dtype=torch.int32, device=gpu))
+        for b, (off, spread, n_b, ooo) in enumerate(SCHEDULE):
+            n_b = min(n_b, n)
+            keys = rng.integers(0, n_keys // 4, n_b).astype(np.uint64)
+            permits = rng.choice([0, 1, 1, 2, 3, 5], n_b).astype(np.int32)
+            ts = (T0 + off + np.sort(rng.integers(0, spread, n_b))).astype(np.int64)
+            if ooo:
+                rng.shuffle(ts)
+            t_tick = int(ts.max()) + 500_000
+            st = torch.empty(n_b, dtype=torch.uint8, device=gpu)
+            rem = torch.empty(n_b, dtype=torch.int32, device=gpu)
+            d = [dev(keys.view(np.int64)), dev(permits), dev(ts)]
+            torch.cuda.synchronize()
+            eng.wait_batch_tick_device(*d, st, rem, b * n, t_tick, *lg)
+            eng.synchronize()
+            st2, rem2, cause2, ids2 = ref.acquire_batch(keys, permits, ts, b * n, threads=THREADS)
+            bad = np.flatnonzero((st.cpu().numpy() != st2) | (rem.cpu().numpy() != rem2))
+            assert bad.size == 0, (order, b, bad.size, bad[:5])
+            cause, ids = eng.evicted()
+            assert np.array_equal(cause, cause2) and np.array_equal(ids, ids2), (order, b)
+            m = int(lg[3].item())
+            ks = lg[0][:m].cpu().numpy().view(np.uint64)
+            o = np.argsort(ks, kind="stable")
+            k2, i2, r2 = ref.refresh(t_tick, threads=THREADS)
+            assert np.array_equal(ks[o] >> np.uint64(16), k2), (order, b)
+            assert np.array_equal(lg[1][:m].cpu().numpy()[o], i2) and np.array_equal(lg[2][:m].cpu().numpy()[o], r2)
+        for k in range(0, n_keys // 4, 4099):
+            assert eng.queue_of(k) == ref.queue_of(k)
+        v, tt = eng.export_state()
+        v2, tt2 = ref.bucket_state()
+        assert np.array_equal(tt, tt2)
+        m = tt2 != ABSENT
+        assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+        eng.close()
