@@ -2803,14 +2803,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             const uint32_t wbase = u * kQBlock + (tid & ~63);   // pair index of lane 0
             if (2 * wbase < R) {
                 const uint32_t pj = tid + u * kQBlock;
-#ifdef TBE_Q_HDR_HALF
-                // A/B timing only (wrong queues): half the header bytes moved (the lanes of
-                // the upper half of each wave skip their load and store; their headers read 0)
-                if ((tid & 63) >= 32) {
-                    qh[2 * wbase + 2 * (tid & 63)] = 0;
-                    qh[2 * wbase + 2 * (tid & 63) + 1] = 0;
-                } else
-#endif
                 lds_dma16(hrows + 2 * (pj < npair ? pj : npair - 1), &qh[2 * wbase]);
             }
         }
@@ -3117,9 +3109,6 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     // the whole 1.6 GB row table back every batch.
     for (uint32_t j = tid; j < nrows; j += kQBlock) {
         if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
-#ifdef TBE_Q_HDR_HALF
-        if ((j & 127u) < 64u)
-#endif
         if (dense ? ((hdirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(hdirty, j)) ST_U(hrows + j, qh[j]);
     }
 #if TBE_QFOLD_PREFETCH

@@ -204,10 +204,6 @@ VARIANT_SETS = {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "rb0_u": (["TBE_REL_BASE=0", "TBE_TICK_FT=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
-    "qhdr": {   # round 6: the queue fold's time with half its header bytes (timing only): what a 32-bit header could save
-        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
-        "hdrhalf_q": (["TBE_Q_HDR_HALF"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
-    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
