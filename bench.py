@@ -50,8 +50,10 @@ T0_US = 1_760_000_000_000_000
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: the schedule tools/pmc_passes.sh measures, so that a run without flags
+    # matches profiles/pmc_summary.json's fingerprint and carries its PMC traffic
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=("uniform", "zipf", "queue", "approx", "testapp"),
                     default="uniform",
                     help="uniform: config B (the headline); zipf: config C's per-GPU slice; "
