@@ -2531,6 +2531,28 @@ struct QParams {
 __device__ __forceinline__ uint64_t qh_pack(uint32_t head, uint32_t cnt, int64_t qsum) {
     return (uint64_t)(head & 0xFFFFu) | ((uint64_t)(cnt & 0xFFFFu) << 16) | ((uint64_t)qsum << 32);
 }
+// Stored width of a queue header (round 6).  With QueueLimit <= kQh32MaxLimit the header is
+// kept in 32 bits -- head 10 bits, count 11, queued permits 11: every queued entry holds >= 1
+// permit (a zero-permit wait is granted at once, Q:153) and the queued permits never exceed
+// QueueLimit (Q:92), so head, count and permits are all <= QueueLimit -- which halves the
+// header bytes the fold reads and writes back.  Kernels work on the 64-bit form (qh_pack):
+// qh_widen on every load, qh_store<HW> on every store.
+#ifndef TBE_QH32
+#define TBE_QH32 1                           // 0: 64-bit headers always (A/B)
+#endif
+constexpr uint32_t kQh32MaxLimit = 1024;
+__host__ __device__ inline uint64_t qh_widen(uint64_t h) { return h; }
+__host__ __device__ inline uint64_t qh_widen(uint32_t h) {
+    return (uint64_t)(h & 0x3FFu) | ((uint64_t)((h >> 10) & 0x7FFu) << 16) | ((uint64_t)(h >> 21) << 32);
+}
+template <typename HW>
+__host__ __device__ inline HW qh_store(uint64_t h);
+template <>
+__host__ __device__ inline uint64_t qh_store<uint64_t>(uint64_t h) { return h; }
+template <>
+__host__ __device__ inline uint32_t qh_store<uint32_t>(uint64_t h) {
+    return (uint32_t)(h & 0x3FFu) | ((uint32_t)((h >> 16) & 0x7FFu) << 10) | ((uint32_t)(h >> 32) << 21);
+}
 
 // k_fold_q's shape: 768 threads x 2 requests (79 VGPRs, 56.8 KB of LDS), two workgroups
 // (24 waves) per CU; against 512 x 4 (128 VGPRs, 16 waves) the config-D fold takes 1.91
@@ -2734,18 +2756,18 @@ constexpr uint32_t kQTailRun = 32;       // longest run a walking thread sorts a
 // (workgroup-scope fence; one CU, one vector L1).
 // PACKED: requests arrive as packed records (PackFmt; permit code min(p, TokenLimit + 1),
 // which leaves REJECTED exactly where p > TokenLimit) beside their arrival indices.
-template <bool PACKED>
+template <bool PACKED, typename HW>
 __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const uint32_t *__restrict__ skeys, const int32_t *__restrict__ sperm,
     const int64_t *__restrict__ sts, const uint32_t *__restrict__ sidx,
     const uint64_t *__restrict__ srec, const int64_t *__restrict__ ts_orig, PackFmt F,
     const uint32_t *__restrict__ bstart, int r_bits, uint64_t n_keys, Slot *__restrict__ table,
-    uint64_t *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
+    HW *__restrict__ qhdr, uint64_t *__restrict__ ring, TbParams P, QParams Q,
     uint32_t *__restrict__ res, uint32_t *__restrict__ ev_cause, int64_t *__restrict__ ev_id,
     uint32_t *__restrict__ ev_count, uint32_t ev_cap, const uint32_t *__restrict__ err, uint32_t narrow,
     QTick T, FoldFmt G, const uint64_t *__restrict__ rec0) {
     __shared__ __attribute__((aligned(16))) Slot slot[1 << kMaxRBits];   // LDS-DMA destinations
-    __shared__ __attribute__((aligned(16))) uint64_t qh[1 << kMaxRBits];
+    __shared__ __attribute__((aligned(16))) HW qh[1 << kMaxRBits];
     __shared__ uint32_t own[1 << kMaxRBits];      // election slots, or the walk's row counts / starts
     __shared__ uint32_t loaded[(1 << kMaxRBits) / 32];
     __shared__ uint32_t dirty[(1 << kMaxRBits) / 32];    // rows modified (smod)
@@ -2773,7 +2795,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     const uint64_t row0 = (uint64_t)b << r_bits;
     const uint32_t nrows = (uint32_t)min<uint64_t>(R, n_keys - row0);
     Slot *__restrict__ rows = table + row0;
-    uint64_t *__restrict__ hrows = qhdr + row0;
+    HW *__restrict__ hrows = qhdr + row0;
 
     // A dense bucket (>= R/8 requests: nearly every 128-byte line of its slice is touched)
     // pulls its whole slice of rows and queue headers with coalesced loads and writes it
@@ -2796,14 +2818,15 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                 lds_dma16(rows + (j < nrows ? j : nrows - 1), &slot[wbase]);
             }
         }
-        constexpr int kHPT = (kMaxRows / 2 + kQBlock - 1) / kQBlock;
-        const uint32_t npair = (nrows + 1) >> 1;
+        constexpr uint32_t kHPL = 16 / sizeof(HW);   // headers per 16-byte lane load
+        constexpr int kHPT = (kMaxRows / kHPL + kQBlock - 1) / kQBlock;
+        const uint32_t ngrp = (nrows + kHPL - 1) / kHPL;   // (the header array is padded to kHPL)
 #pragma unroll
         for (int u = 0; u < kHPT; ++u) {
-            const uint32_t wbase = u * kQBlock + (tid & ~63);   // pair index of lane 0
-            if (2 * wbase < R) {
+            const uint32_t wbase = u * kQBlock + (tid & ~63);   // group index of lane 0
+            if (kHPL * wbase < R) {
                 const uint32_t pj = tid + u * kQBlock;
-                lds_dma16(hrows + 2 * (pj < npair ? pj : npair - 1), &qh[2 * wbase]);
+                lds_dma16(hrows + kHPL * (pj < ngrp ? pj : ngrp - 1), &qh[kHPL * wbase]);
             }
         }
     }
@@ -2878,7 +2901,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
         }
         if (mine) {
             Slot tmp[kQItems];
-            uint64_t th[kQItems];
+            HW th[kQItems];
 #pragma unroll
             for (int r = 0; r < kQItems; ++r) {
                 tmp[r] = Slot{0.0, 0};
@@ -2907,7 +2930,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                     continue;
                 won |= 1u << r;
                 Slot st = slot[kl[r]];
-                uint64_t h = qh[kl[r]];
+                uint64_t h = qh_widen(qh[kl[r]]);
                 bool smod = false, hmod = false, evaluated;
                 uint32_t status, rem;
                 // request times derived by the winner (not held across rounds: registers)
@@ -2916,7 +2939,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                        ev_cause, ev_id, ev_count, ev_cap, status, rem, evaluated);
                 put_wait(res, pos[r], status, evaluated, rem, narrow);
                 if (smod) slot[kl[r]] = st;
-                if (hmod) qh[kl[r]] = h;
+                if (hmod) qh[kl[r]] = qh_store<HW>(h);
                 if (smod) atomicOr(&dirty[kl[r] >> 5], 1u << (kl[r] & 31));
                 if (hmod) atomicOr(&hdirty[kl[r] >> 5], 1u << (kl[r] & 31));
             }
@@ -2998,7 +3021,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                                     tw_sorted[y] = v;
                                 }
                                 Slot st = slot[row];
-                                uint64_t h = qh[row];
+                                uint64_t h = qh_widen(qh[row]);
                                 bool smod = false, hmod = false;
                                 uint64_t *__restrict__ kr = ring + (row0 + row) * (uint64_t)Q.cap;
                                 for (uint32_t x = start; x < stop; ++x) {
@@ -3015,7 +3038,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
                                     atomicOr(&dirty[row >> 5], 1u << (row & 31));
                                 }
                                 if (hmod) {
-                                    qh[row] = h;
+                                    qh[row] = qh_store<HW>(h);
                                     atomicOr(&hdirty[row >> 5], 1u << (row & 31));
                                 }
                             }
@@ -3069,7 +3092,7 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             const uint32_t j = tid + u * kQBlock;
             if (j < nrows) {
                 Slot st = slot[j];
-                uint64_t h = qh[j];
+                uint64_t h = qh_widen(qh[j]);
                 bool sm = false;
                 const uint32_t g = drain_key<false>(row0 + j, st, h, sm, ring + (row0 + j) * (uint64_t)Q.cap, rqT, TB, P,
                                                     Q, L, 0);
@@ -3089,14 +3112,14 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
             const uint32_t j = tid + u * kQBlock;
             if ((need >> u) & 1u) {
                 Slot st = slot[j];
-                uint64_t h = qh[j];
+                uint64_t h = qh_widen(qh[j]);
                 const uint64_t h0 = h;
                 bool smod = false;
                 const uint32_t g = drain_key<true>(row0 + j, st, h, smod, ring + (row0 + j) * (uint64_t)Q.cap, rqT, TB, P,
                                                    Q, L, at);
                 at += g;
                 if (smod) slot[j] = st;
-                if (h != h0) qh[j] = h;
+                if (h != h0) qh[j] = qh_store<HW>(h);
                 if (smod) atomicOr(&dirty[j >> 5], 1u << (j & 31));
                 if (h != h0) atomicOr(&hdirty[j >> 5], 1u << (j & 31));
             }
@@ -3109,7 +3132,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
     // the whole 1.6 GB row table back every batch.
     for (uint32_t j = tid; j < nrows; j += kQBlock) {
         if (dense ? row_line_dirty(dirty, j) : row_dirty(dirty, j)) ST_S(rows + j, slot[j]);
-        if (dense ? ((hdirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0 : row_dirty(hdirty, j)) ST_U(hrows + j, qh[j]);
+        const bool hline = sizeof(HW) == 8 ? ((hdirty[j >> 5] >> (j & 16u)) & 0xFFFFu) != 0   // 16 per line
+                                           : hdirty[j >> 5] != 0;                            // 32 per line
+        if (dense ? hline : row_dirty(hdirty, j)) ST_U(hrows + j, qh[j]);
     }
 #if TBE_QFOLD_PREFETCH
     if (n_keys == 0) res[s] = pf_sink;   // never (no engine has 0 keys): keeps the touches
@@ -3119,8 +3144,9 @@ __global__ __launch_bounds__(kQBlock, TBE_Q_WAVES) void k_fold_q(
 // One replenish tick (Q:237-271) over every key: drain the head (OldestFirst) or tail
 // (NewestFirst) while the acquire script grants.  One thread per key.  Grants are logged
 // as (key, drain position, request id, remaining); the host orders them by key.
+template <typename HW>
 __global__ __launch_bounds__(kBlock) void k_drain(
-    uint64_t n_keys, Slot *__restrict__ table, uint64_t *__restrict__ qhdr,
+    uint64_t n_keys, Slot *__restrict__ table, HW *__restrict__ qhdr,
     const uint64_t *__restrict__ ring, TbParams P, QParams Q, int64_t ts_us,
     uint64_t *__restrict__ log_keyseq, int64_t *__restrict__ log_id, int32_t *__restrict__ log_rem,
     uint32_t *__restrict__ log_count, uint32_t log_cap) {
@@ -3134,7 +3160,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
     for (uint64_t k0 = (uint64_t)blockIdx.x * kBlock; k0 < n_keys; k0 += stride) {
         const uint64_t key = k0 + threadIdx.x;
         const bool valid = key < n_keys;
-        uint64_t h = valid ? qhdr[key] : 0ull;
+        uint64_t h = valid ? qh_widen(qhdr[key]) : 0ull;
         const bool queued = ((h >> 16) & 0xFFFFu) != 0;
         Slot st = (valid && queued) ? table[key] : Slot{0.0, 0};
         const uint64_t *__restrict__ kr = ring + key * (uint64_t)Q.cap;
@@ -3151,7 +3177,7 @@ __global__ __launch_bounds__(kBlock) void k_drain(
             const uint64_t hb = h;
             drain_key<true>(key, st, h, smod, kr, rqT, TB, P, Q, L, log_base + off);
             if (smod) table[key] = st;
-            if (h != hb) qhdr[key] = h;
+            if (h != hb) qhdr[key] = qh_store<HW>(h);
         }
         __syncthreads();   // log_base is rewritten by the next trip
     }
@@ -3618,14 +3644,15 @@ __global__ void k_sticky(const uint32_t *__restrict__ err, uint32_t *__restrict_
 
 // Entries in all queues: qhdr count bits (queueing kind) or ALocal.hc count bits
 // (approximate kind).  Re-establishes the host's count after device-pointer batches.
-__global__ __launch_bounds__(kBlock) void k_count_queued(uint64_t n_keys, const uint64_t *__restrict__ qhdr,
+template <typename HW>
+__global__ __launch_bounds__(kBlock) void k_count_queued(uint64_t n_keys, const HW *__restrict__ qhdr,
                                                         const ALocal *__restrict__ alocal,
                                                         unsigned long long *__restrict__ out) {
     __shared__ unsigned long long part[kBlock / 64];
     unsigned long long c = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n_keys; k += stride)
-        c += qhdr ? ((qhdr[k] >> 16) & 0xFFFFu) : ((alocal[k].hc >> 16) & 0xFFFFu);
+        c += qhdr ? ((qh_widen(qhdr[k]) >> 16) & 0xFFFFu) : ((alocal[k].hc >> 16) & 0xFFFFu);
     for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -3726,7 +3753,8 @@ struct tbe_engine {
     Slot *table = nullptr;
     // queueing kind
     QParams qp{};
-    uint64_t *qhdr = nullptr;      // per-key queue header
+    uint64_t *qhdr = nullptr;      // per-key queue header (32-bit words when qh32: qh_store)
+    bool qh32 = false;             // queue headers stored 32 bits wide (QueueLimit <= kQh32MaxLimit)
     uint64_t *ring = nullptr;      // per-key rings of qp.cap entries
     uint64_t queued_total = 0;     // entries in all queues (host-side count)
     // After a device-pointer wait batch or drain the host cannot see how many entries
@@ -3789,6 +3817,13 @@ struct tbe_engine {
     int open_stage = -1;
     std::string last_error = "ok";
 };
+
+// Calls f with the queue headers typed by their stored width (uint32_t* or uint64_t*).
+template <typename F>
+static void with_qhdr(tbe_engine *e, F &&f) {
+    if (e->qh32) f(reinterpret_cast<uint32_t *>(e->qhdr));
+    else f(e->qhdr);
+}
 
 namespace {
 
@@ -4223,18 +4258,21 @@ tbe_status run_batch(tbe_engine *e, const uint64_t *keys, const int32_t *permits
         q.id_base = id_base;
         q.wait = e->wait_mode;
         q.ai_base = ai_base;
-        if (e->packed)
-            k_fold_q<true><<<fold_grid, kQBlock, 0, sf>>>(
-                nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
-                e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
-                e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(),
-                e->qtick, G, rec0);
-        else
-            k_fold_q<false><<<e->nbuckets, kQBlock, 0, sf>>>(
-                sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
-                e->r_bits, e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params, q, w.res[0], e->ev_cause,
-                e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
-                e->wait_rw(), e->qtick, G, rec0);
+        with_qhdr(e, [&](auto *qh) {
+            using HW = std::remove_pointer_t<decltype(qh)>;
+            if (e->packed)
+                k_fold_q<true, HW><<<fold_grid, kQBlock, 0, sf>>>(
+                    nullptr, nullptr, nullptr, sorted.idx, sorted.rec, ts, e->pf, w.bstart, e->r_bits,
+                    e->cfg.n_keys, e->table, qh, e->ring, e->params, q, w.res[0], e->ev_cause, e->ev_id,
+                    e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err, e->wait_rw(),
+                    e->qtick, G, rec0);
+            else
+                k_fold_q<false, HW><<<e->nbuckets, kQBlock, 0, sf>>>(
+                    sorted.keys, sorted.permits, sorted.ts, sorted.idx, nullptr, nullptr, e->pf, w.bstart,
+                    e->r_bits, e->cfg.n_keys, e->table, qh, e->ring, e->params, q, w.res[0], e->ev_cause,
+                    e->ev_id, e->counters, (uint32_t)std::min<uint64_t>(e->ev_cap, 0xFFFFFFFFu), w.err,
+                    e->wait_rw(), e->qtick, G, rec0);
+        });
     } else if (sparse_tb) {
         // sparse batch: at most n / wmin buckets are dense (k_bscan listed them); one wave per
         // other bucket
@@ -4523,7 +4561,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     // one is then initialised on e->stream -- the rings and the headers' pad entry too, though
     // no decision reads a ring entry the engine did not write -- so a new engine never sees
     // bytes an earlier allocation left (tests/test_gpu_recreate.py).
-    const uint64_t qhdr_n = (c.n_keys + 1) & ~1ull;   // even: k_fold_q loads header pairs
+    const uint64_t qhdr_n = (c.n_keys + 3) & ~3ull;   // k_fold_q loads headers 16 bytes per lane
     uint64_t ring_n = 0;
     if (dalloc(&e->table, c.n_keys * sizeof(Slot)) != hipSuccess) return bail(TBE_ENOMEM);
     if (e->hot_cap)
@@ -4536,7 +4574,9 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
         e->qp.order = c.queue_order;
         e->qp.cap = (uint32_t)std::max(1, c.queue_limit);
         ring_n = c.n_keys * (uint64_t)e->qp.cap;
-        if (dalloc(&e->qhdr, qhdr_n * sizeof(uint64_t)) != hipSuccess) return bail(TBE_ENOMEM);
+        e->qh32 = TBE_QH32 && (uint32_t)c.queue_limit <= kQh32MaxLimit;
+        if (dalloc(&e->qhdr, qhdr_n * (e->qh32 ? sizeof(uint32_t) : sizeof(uint64_t))) != hipSuccess)
+            return bail(TBE_ENOMEM);
     } else if (c.kind == TBE_KIND_APPROXIMATE) {
         e->ap.token_limit = c.token_limit;
         e->ap.queue_limit = c.queue_limit;
@@ -4565,7 +4605,7 @@ tbe_status tbe_create(const tbe_config *config, tbe_engine **out_engine) {
     };
     for (auto &hs : e->hot) zero(hs, sizeof(HotSet));
     zero(e->sticky, sizeof(uint32_t));
-    zero(e->qhdr, qhdr_n * sizeof(uint64_t));
+    zero(e->qhdr, qhdr_n * (e->qh32 ? sizeof(uint32_t) : sizeof(uint64_t)));
     zero(e->ring, ring_n * sizeof(uint64_t));
     zero(e->counters, 2 * sizeof(uint32_t));
     for (auto &w : e->ws)
@@ -4863,8 +4903,13 @@ static tbe_status sync_queued(tbe_engine *e) {
     hipStream_t st = e->stream;
     HIP_TRY(e, hipMemsetAsync(e->qcount, 0, sizeof(unsigned long long), st));
     const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
-    k_count_queued<<<(unsigned)blocks, kBlock, 0, st>>>(
-        e->cfg.n_keys, e->cfg.kind == TBE_KIND_QUEUEING ? e->qhdr : nullptr, e->alocal, e->qcount);
+    if (e->cfg.kind == TBE_KIND_QUEUEING)
+        with_qhdr(e, [&](auto *qh) {
+            k_count_queued<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, qh, e->alocal, e->qcount);
+        });
+    else
+        k_count_queued<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, (const uint64_t *)nullptr, e->alocal,
+                                                            e->qcount);
     HIP_TRY(e, hipGetLastError());
     unsigned long long q = 0;
     HIP_TRY(e, hipMemcpyAsync(&q, e->qcount, sizeof q, hipMemcpyDeviceToHost, st));
@@ -5142,10 +5187,11 @@ tbe_status tbe_refresh(tbe_engine *e, int64_t ts_us, uint64_t *n_granted) {
     hipStream_t st = e->stream;
     HIP_TRY(e, hipMemsetAsync(e->counters + 1, 0, sizeof(uint32_t), st));
     const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
-    k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params,
-                                                e->qp, ts_us, e->log_keyseq, e->log_id, e->log_rem,
-                                                e->counters + 1,
-                                                (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu));
+    with_qhdr(e, [&](auto *qh) {
+        k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, qh, e->ring, e->params, e->qp, ts_us,
+                                                    e->log_keyseq, e->log_id, e->log_rem, e->counters + 1,
+                                                    (uint32_t)std::min<uint64_t>(e->log_cap, 0xFFFFFFFFu));
+    });
     HIP_TRY(e, hipGetLastError());
     uint32_t cnt = 0;
     HIP_TRY(e, hipMemcpyAsync(&cnt, e->counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -5197,9 +5243,11 @@ tbe_status tbe_refresh_device(tbe_engine *e, int64_t ts_us, uint64_t *d_keyseq, 
     HIP_TRY(e, hipMemsetAsync(d_count, 0, sizeof(uint32_t), st));
     if (bound == 0) return TBE_OK;   // nothing queued
     const uint64_t blocks = std::min<uint64_t>((e->cfg.n_keys + kBlock - 1) / kBlock, 8192);
-    k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, e->qhdr, e->ring, e->params,
-                                                e->qp, ts_us, d_keyseq, d_request_id, d_remaining, d_count,
-                                                (uint32_t)std::min<uint64_t>(capacity, 0xFFFFFFFFu));
+    with_qhdr(e, [&](auto *qh) {
+        k_drain<<<(unsigned)blocks, kBlock, 0, st>>>(e->cfg.n_keys, e->table, qh, e->ring, e->params, e->qp, ts_us,
+                                                    d_keyseq, d_request_id, d_remaining, d_count,
+                                                    (uint32_t)std::min<uint64_t>(capacity, 0xFFFFFFFFu));
+    });
     HIP_TRY(e, hipGetLastError());
     e->queued_exact = false;   // queued_total stays an upper bound
     return TBE_OK;
@@ -5434,7 +5482,13 @@ tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_
     uint32_t head = 0, cnt = 0;
     if (e->cfg.kind == TBE_KIND_QUEUEING) {
         uint64_t h = 0;
-        HIP_TRY(e, hipMemcpy(&h, e->qhdr + key, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        if (e->qh32) {
+            uint32_t h32 = 0;
+            HIP_TRY(e, hipMemcpy(&h32, reinterpret_cast<uint32_t *>(e->qhdr) + key, sizeof h32, hipMemcpyDeviceToHost));
+            h = qh_widen(h32);
+        } else {
+            HIP_TRY(e, hipMemcpy(&h, e->qhdr + key, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        }
         head = (uint32_t)(h & 0xFFFFu);
         cnt = (uint32_t)((h >> 16) & 0xFFFFu);
     } else {
@@ -5463,10 +5517,12 @@ tbe_status tbe_queue_of(tbe_engine *e, uint64_t key, int64_t *request_id, int32_
 // leaves a canceled registration in its deque until the drain reaches it, where it
 // consumes tokens and A:489 adds its count back a second time; a
 // bounded ring cannot hold entries that no longer count against QueueLimit.
+extern "C++" {   // (inside the C ABI's extern "C" block: a template needs C++ linkage)
+template <typename HW>
 __global__ __launch_bounds__(256) void k_cancel(
     const uint64_t *__restrict__ ckeys, const int64_t *__restrict__ cids,
     const uint32_t *__restrict__ run_start, uint32_t n_runs, int32_t approx,
-    uint64_t *__restrict__ qhdr, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring,
+    HW *__restrict__ qhdr, ALocal *__restrict__ alocal, uint64_t *__restrict__ ring,
     uint32_t cap, uint8_t *__restrict__ hit) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
@@ -5481,7 +5537,7 @@ __global__ __launch_bounds__(256) void k_cancel(
         cnt = a.hc >> 16;
         qsum = a.qsum;
     } else {
-        const uint64_t h = qhdr[key];
+        const uint64_t h = qh_widen(qhdr[key]);
         head = (uint32_t)(h & 0xFFFFu);
         cnt = (uint32_t)((h >> 16) & 0xFFFFu);
         qsum = (int64_t)(h >> 32);
@@ -5510,9 +5566,10 @@ __global__ __launch_bounds__(256) void k_cancel(
         a.hc = (head & 0xFFFFu) | (cnt << 16);
         alocal[key] = a;
     } else {
-        qhdr[key] = qh_pack(head, cnt, qsum);
+        qhdr[key] = qh_store<HW>(qh_pack(head, cnt, qsum));
     }
 }
+}   // extern "C++"
 
 tbe_status tbe_queue_cancel(tbe_engine *e, const uint64_t *keys, const int64_t *request_ids,
                             uint64_t n, uint8_t *cancelled, uint64_t *n_cancelled) {
@@ -5553,9 +5610,11 @@ tbe_status tbe_queue_cancel(tbe_engine *e, const uint64_t *keys, const int64_t *
                          hipMemcpyHostToDevice));
     const bool approx = e->cfg.kind == TBE_KIND_APPROXIMATE;
     const uint32_t rcap = approx ? e->ap.cap : e->qp.cap;
-    k_cancel<<<(n_runs + 255) / 256, 256, 0, e->stream>>>(
-        (const uint64_t *)s.p, (const int64_t *)(s.p + off_ids), (const uint32_t *)(s.p + off_runs),
-        n_runs, approx ? 1 : 0, e->qhdr, e->alocal, e->ring, rcap, (uint8_t *)(s.p + off_hit));
+    with_qhdr(e, [&](auto *qh) {
+        k_cancel<<<(n_runs + 255) / 256, 256, 0, e->stream>>>(
+            (const uint64_t *)s.p, (const int64_t *)(s.p + off_ids), (const uint32_t *)(s.p + off_runs),
+            n_runs, approx ? 1 : 0, qh, e->alocal, e->ring, rcap, (uint8_t *)(s.p + off_hit));
+    });
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     std::vector<uint8_t> hit(n);

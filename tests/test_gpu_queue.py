@@ -170,3 +170,39 @@ def test_queue_layouts(engine_lib, gpu, order, layout):
     assert np.array_equal(tt, tt2)
     m = tt2 != np.iinfo(np.int64).min
     assert np.array_equal(v[m].view(np.uint64), v2[m].view(np.uint64))
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("qlimit", [1024, 1025, 3000])
+def test_long_queues_and_header_width(engine_lib, gpu, order, qlimit):
+    """Queue headers are stored 32 bits wide up to QueueLimit 1024 (head 10 bits, count and
+    queued permits 11) and 64 bits above: queues filled to the limit on both sides of the
+    boundary -- a few keys, thousands of waits each, every permit count up to TokenLimit --
+    with evictions (NewestFirst), replenish ticks, cancels and queue listings against the C
+    restatement (Q:67-134, Q:237-271, Q:480-506)."""
+    n_keys, n = 6, 20_000
+    eng, ref = pair(n_keys, 7, 3, 10_000_000, qlimit, order)
+    assert eng.queue_limit == qlimit
+    rng = np.random.default_rng(qlimit * 2 + order)
+    t, rid = S_US, 0
+    for b in range(4):
+        keys = rng.integers(0, n_keys, n).astype(np.uint64)
+        permits = rng.choice([1, 1, 2, 3, 7, 8], n).astype(np.int32)
+        ts = (t + np.sort(rng.integers(0, 1_000, n))).astype(np.int64)
+        st = check_round(eng, ref, keys, permits, ts, rid)
+        if b == 1:
+            assert (st == 2).any()
+        rid += n
+        t += 2_000_000 if b % 2 else 20_000
+        k1, i1, r1 = eng.refresh(t)
+        k2, i2, r2 = ref.refresh(t)
+        assert np.array_equal(k1, k2) and np.array_equal(i1, i2) and np.array_equal(r1, r2)
+        qs = [eng.queue_of(k) for k in range(n_keys)]
+        assert qs == [ref.queue_of(k) for k in range(n_keys)]
+        # cancel every fifth queued request of key 0 (and one unknown id)
+        ids = [e[0] for e in qs[0][::5]] + [-7]
+        ck = np.zeros(len(ids), dtype=np.uint64)
+        c1 = eng.cancel(ck, np.array(ids, dtype=np.int64))
+        c2 = ref.cancel(ck, np.array(ids, dtype=np.int64))
+        assert np.array_equal(np.asarray(c1), np.asarray(c2))
+    assert max(sum(p for _, p in q) for q in qs) > min(qlimit, 1024) // 2   # queues ran long

@@ -204,6 +204,10 @@ VARIANT_SETS = {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "rb0_u": (["TBE_REL_BASE=0", "TBE_TICK_FT=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
     },
+    "qh32": {   # round 6: 32-bit queue headers (QueueLimit <= 1024) or 64-bit ones
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "qh64_q": (["TBE_QH32=0"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
