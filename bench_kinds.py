@@ -352,10 +352,11 @@ def run_queue(args, lib, dev, world, rank, dist):
     packed = bool(r["layout"].get("packed"))
     # the fold's own bytes: records (packed: u64 record 8 + arrival index 4; wide: key 4,
     # permits 4, ts 8, index 4) + packed reply 4 per request; per distinct key: bucket row
-    # 16 + queue header 8, read and written; 8 per enqueue
+    # 16 + queue header (4 bytes at QueueLimit <= 1024, else 8), read and written; 8 per enqueue
     rec = 12 if packed else 20
-    own = n * (rec + 4) + u * 48 + q_last * 8
-    own_note = f"fold: n*{rec + 4} + distinct*48 + enqueued*8 (last batch's enqueues)"
+    per_u = 2 * (16 + (4 if r["layout"].get("queue_header_32") else 8))
+    own = n * (rec + 4) + u * per_u + q_last * 8
+    own_note = f"fold: n*{rec + 4} + distinct*{per_u} + enqueued*8 (last batch's enqueues)"
     # the B formula (W ~ distinct keys x grant share) + 8 B per
     # enqueue + 8 B per dequeue (lower bound: headers of non-empty queues omitted)
     step_alg = n * 25 + u * 16 + u * granted * 16 + q_last * 8 + d_last * 8
@@ -397,7 +398,7 @@ def run_queue(args, lib, dev, world, rank, dist):
         if rank == 0 and args.drain_marked:
             write_fingerprint(dfp)
         d_step = n * 25 + u * 16 + u * d["granted"] * 16 + d["q_last"] * 8 + d["d_last"] * 8
-        d_own = n * (rec + 4) + u * 48 + d["q_last"] * 8 + d["d_last"] * 28
+        d_own = n * (rec + 4) + u * per_u + d["q_last"] * 8 + d["d_last"] * 28
         d_fold = (d["fold_timed"] if d["fold_timed"] > 0 else d["stages"].get("fold", 0.0)) / steps
         line["draining"] = {
             "period_ticks": pt, "tokens_per_period": args.tokens_per_period,

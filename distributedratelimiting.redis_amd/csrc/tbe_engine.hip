@@ -5635,7 +5635,7 @@ tbe_status tbe_layout(const tbe_engine *e, uint32_t *passes, uint32_t *r_bits, u
     *r_bits = (uint32_t)e->r_bits;
     *packed = (e->packed ? 1u : 0u) | (e->hot_cap ? 2u : 0u) | (e->pipeline ? 4u : 0u) |
               (e->narrow ? 8u : 0u) | (e->medium ? 16u : 0u) | (e->foldrec ? 32u : 0u) |
-              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u) | (e->n0 ? 256u : 0u);
+              (e->dig1 ? 64u : 0u) | (e->unrank ? 128u : 0u) | (e->n0 ? 256u : 0u) | (e->qh32 ? 512u : 0u);
     return TBE_OK;
 }
 

@@ -178,7 +178,8 @@ class TokenBucketEngine:
                                                t_us.ctypes.data))
 
     def layout(self) -> dict:
-        """{passes, r_bits, packed, hot, pipeline, narrow, medium, fold_records, digit_stream, rerank} of this engine's
+        """{passes, r_bits, packed, hot, pipeline, narrow, medium, fold_records, digit_stream, rerank,
+        narrow_pass0, queue_header_32} of this engine's
         batch pipeline (tbe_layout)."""
         a, b, c = c_uint32(), c_uint32(), c_uint32()
         self._check(self._lib.tbe_layout(self.handle, byref(a), byref(b), byref(c)))
@@ -186,7 +187,7 @@ class TokenBucketEngine:
                 "hot": bool(c.value & 2), "pipeline": bool(c.value & 4), "narrow": bool(c.value & 8),
                 "medium": bool(c.value & 16), "fold_records": bool(c.value & 32),
                 "digit_stream": bool(c.value & 64), "rerank": bool(c.value & 128),
-                "narrow_pass0": bool(c.value & 256)}
+                "narrow_pass0": bool(c.value & 256), "queue_header_32": bool(c.value & 512)}
 
     def batch_format(self, n: int) -> dict:
         """The record layout a batch of n requests takes (tbe_batch_format)."""

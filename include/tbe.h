@@ -373,7 +373,8 @@ tbe_status tbe_approx_import_state(tbe_engine *engine, uint64_t first, uint64_t 
  * bit 7 set when the final un-partition re-ranks pass 0's tiles (TBE_FLAG_RERANK sets
  * it), bit 8 set when pass 0 writes narrow 4-byte records (token bucket and queueing kinds
  * with fold records and the digit stream, and the approximate kind's AcquireCore batches; a
- * batch uses them when it uses fold records). */
+ * batch uses them when it uses fold records), bit 9 set when the queueing kind stores its
+ * per-key queue headers in 32 bits (QueueLimit <= 1024). */
 tbe_status tbe_layout(const tbe_engine *engine, uint32_t *passes, uint32_t *r_bits, uint32_t *packed);
 
 /* The record layout a batch of n requests takes (diagnostics and tests):

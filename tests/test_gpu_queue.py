@@ -182,7 +182,7 @@ def test_long_queues_and_header_width(engine_lib, gpu, order, qlimit):
     restatement (Q:67-134, Q:237-271, Q:480-506)."""
     n_keys, n = 6, 20_000
     eng, ref = pair(n_keys, 7, 3, 10_000_000, qlimit, order)
-    assert eng.queue_limit == qlimit
+    assert eng.queue_limit == qlimit and eng.layout()["queue_header_32"] == (qlimit <= 1024)
     rng = np.random.default_rng(qlimit * 2 + order)
     t, rid = S_US, 0
     for b in range(4):
