@@ -117,7 +117,13 @@ def _pmc_traffic(w, kernels):
     if w is None:
         return None
     d = w.get("kernels", {})
-    v = [d[k]["hbm_bytes_per_launch"] for k in kernels if "hbm_bytes_per_launch" in d.get(k, {})]
+
+    def entry(k):   # "k_fold_q<true>" also names k_fold_q<true, HW> (any queue-header width)
+        if k in d:
+            return d[k]
+        m = [d[x] for x in d if k.endswith(">") and x.startswith(k[:-1] + ",")]
+        return m[0] if len(m) == 1 else {}
+    v = [entry(k)["hbm_bytes_per_launch"] for k in kernels if "hbm_bytes_per_launch" in entry(k)]
     return round(sum(v) / len(v), 1) if len(v) == len(kernels) and v else None
 
 

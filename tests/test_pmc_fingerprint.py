@@ -80,3 +80,13 @@ def test_queue_roofline_traffic_follows_the_match(tmp_path, monkeypatch):
     r = bk._roofline(2.89, 2.88e9, "B_alg", 3.84e9, "own", "queue", dict(fp, keys_per_gpu=12_500_000), 4.2,
                      stages, 20)
     assert r["traffic"] is None and "keys_per_gpu" in r["traffic_null_reason"]
+
+
+def test_fold_kernel_names_cover_template_arguments():
+    """k_fold_q carries its queue-header width as a template argument (round 6): the PMC
+    entry "k_fold_q<true, unsigned int>" is the fold that PMC_KERNELS names "k_fold_q<true>"."""
+    w = {"kernels": {"k_fold_q<true, unsigned int>": {"hbm_bytes_per_launch": 5.5e9},
+                     "k_scatter_rec<true, false, true, false, false>": {"hbm_bytes_per_launch": 1.0}}}
+    assert bk._pmc_traffic(w, bk.PMC_KERNELS[("queue", "fold")]) == 5.5e9
+    assert bk._pmc_traffic({"kernels": {"k_fold_q<true>": {"hbm_bytes_per_launch": 6.0}}}, ["k_fold_q<true>"]) == 6.0
+    assert bk._pmc_traffic({"kernels": {}}, ["k_fold_q<true>"]) is None
