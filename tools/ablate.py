@@ -208,6 +208,14 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "qh64_q": (["TBE_QH32=0"], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
     },
+    "qh32b": {   # the same as bench.py --workload queue runs it (20 + 5 batches, draining variant)
+        "base_q": ([], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
+        "qh64_q": (["TBE_QH32=0"], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
+    },
+    "qvar": {   # run-to-run spread of config D's fold in the bench's schedule, with and without ring stores
+        "base_q": ([], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
+        "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
