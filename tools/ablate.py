@@ -76,12 +76,6 @@ VARIANT_SETS = {
         "b256i16_u": (["TBE_UN_BLOCK=256", "TBE_UN_ITEMS=16"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
         "b512i8_u": (["TBE_UN_BLOCK=512", "TBE_UN_ITEMS=8"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
     },
-    "hidx": {
-        "hidx_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "probe_z": (["TBE_HOT_HIDX=0"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "hidx_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
-        "probe_u": (["TBE_HOT_HIDX=0"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
-    },
     "probe": {
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir"]),
@@ -250,11 +244,9 @@ VARIANT_SETS = {
         "never_z": (["TBE_HOT_SPARSE_MIN_LOG2=40"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
         "hm20_z": (["TBE_HOT_SPARSE_MIN_LOG2=20"], ['--workload', 'uniform', '--no-host-buffer', '--no-strdir', '--sweep-log2', '16,18,20,22', '--sweep-zipf']),
     },
-    "r05b": {   # one-workgroup sampler vs many small ones; the queue kind pipelined or not
+    "r05b": {   # the queue kind pipelined or not (its sampler variants were removed with their hook)
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
-        "onewg_u": (["TBE_HOT_SAMPLE_ONE_WG=1"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "base_z": ([], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
-        "onewg_z": (["TBE_HOT_SAMPLE_ONE_WG=1"], ["--workload", "zipf", "--no-host-buffer", "--no-strdir"]),
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "nopipe_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant", "--no-pipeline"]),
     },
