@@ -210,6 +210,10 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
         "noring_q": (["TBE_Q_NO_RING_WRITE"], ["--workload", "queue", "--no-strdir", "--steps", "20", "--warmup", "5"]),
     },
+    "qtail": {   # round 6: the queue fold's pending requests after round 1 by the walk (tree) or by owner rounds on the list + solo wave (patch)
+        "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
+        "rounds_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"], "diag/q_tail_rounds.patch"),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
