@@ -214,6 +214,12 @@ VARIANT_SETS = {
         "base_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"]),
         "rounds_q": ([], ["--workload", "queue", "--no-host-buffer", "--no-strdir", "--no-drain-variant"], "diag/q_tail_rounds.patch"),
     },
+    "pf6": {   # round 6 (final tree): the dense fold's prefetch distance
+        "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf256_u": (["TBE_FOLD_PREFETCH=256"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pf512_u": (["TBE_FOLD_PREFETCH=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+        "pfmin512_u": (["TBE_FOLD_PREFETCH_MIN=512"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
+    },
     "floors": {
         "base_u": ([], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
         "copyonly_u": (["TBE_FOLD_COPY_ONLY"], ["--workload", "uniform", "--no-host-buffer", "--no-strdir", "--no-sparse"]),
